@@ -1,0 +1,155 @@
+/*
+ * plssvm_mi355x.h — C ABI of the MI355X-native PLSSVM CG hot path (libplssvm_mi355x.so).
+ *
+ * The reference exposes this path only as C++ virtuals of plssvm::csvm<T> /
+ * plssvm::detail::gpu_csvm<T, device_ptr_t, queue_t>; every entry point below names the
+ * reference member it replaces (paths relative to the reference repository root). The C++
+ * adapter plssvm::mi355x::csvm<T> (plssvm_sparse_fp22_amd/csrc/csvm.hpp) maps those virtuals
+ * onto these calls; ctypes/cgo/JNI bindings can call them directly.
+ *
+ * Conventions
+ *   - Every function returns PLSSVM_MI_OK (0) or a negative PLSSVM_MI_ERR_* code; no C++
+ *     exception crosses the ABI. plssvm_mi_last_error() returns the message of the last
+ *     failure on that context (the text the reference would put in its backend_exception).
+ *   - Host buffers are caller-owned. Calls taking host buffers are blocking: they return after
+ *     results are in host memory (the reference's synchronous hipMemcpy semantics,
+ *     src/plssvm/backends/HIP/detail/device_ptr.hip.cpp:40-68).
+ *   - "real" buffers hold float when the context was created with real_bytes == 4 and double
+ *     when real_bytes == 8 (the reference's template parameter T, include/plssvm/csvm.hpp:36).
+ *   - A context owns one GPU (one HIP stream). Several contexts — one per process and GPU —
+ *     form a row-block partitioned group through plssvm_mi_comm_init (RCCL over xGMI).
+ *   - m = n - 1 ("dept" in the reference): the last data point is eliminated by the LS-SVM
+ *     reformulation (src/plssvm/csvm.cpp:230-258).
+ */
+#ifndef PLSSVM_MI355X_H
+#define PLSSVM_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PLSSVM_MI_ABI_VERSION 1
+
+#if defined(PLSSVM_MI_BUILDING)
+#define PLSSVM_MI_API __attribute__((visibility("default")))
+#else
+#define PLSSVM_MI_API
+#endif
+
+/* return codes */
+#define PLSSVM_MI_OK 0
+#define PLSSVM_MI_ERR_ARG (-1)         /* invalid argument (plssvm::exception in the reference) */
+#define PLSSVM_MI_ERR_HIP (-2)         /* HIP runtime error (plssvm::hip::backend_exception)     */
+#define PLSSVM_MI_ERR_RCCL (-3)        /* RCCL error                                              */
+#define PLSSVM_MI_ERR_OOM (-4)         /* device allocation failed                                */
+#define PLSSVM_MI_ERR_UNSUPPORTED (-5) /* unsupported kernel/format combination                   */
+#define PLSSVM_MI_ERR_STATE (-6)       /* call out of order (e.g. generate_q before setup)        */
+#define PLSSVM_MI_ERR_NODEV (-7)       /* "HIP backend selected but no HIP devices were found!"   */
+
+/* kernel types: plssvm::kernel_type (include/plssvm/kernel_types.hpp:27-34) */
+#define PLSSVM_MI_KERNEL_LINEAR 0
+#define PLSSVM_MI_KERNEL_POLYNOMIAL 1
+#define PLSSVM_MI_KERNEL_RBF 2
+
+/* value formats of sparse feature data (build-defined; the reference has no sparse path) */
+#define PLSSVM_MI_VAL_REAL 0 /* float or double, as the context's real type */
+#define PLSSVM_MI_VAL_FP22 1 /* packed FP22 words, 16 values per 11 uint32 (float contexts only) */
+
+/* K·p algorithm selection (plssvm_mi_set_option key PLSSVM_MI_OPT_KP_MODE) */
+#define PLSSVM_MI_KP_AUTO 0     /* pairwise for poly/rbf, factored for linear on sparse data      */
+#define PLSSVM_MI_KP_PAIRWISE 1 /* implicit pairwise tiles (MFMA on dense data)                   */
+#define PLSSVM_MI_KP_FACTORED 2 /* linear kernel only: X (X^T p) + rank-1 terms, HBM-bound         */
+
+#define PLSSVM_MI_OPT_KP_MODE 1
+
+typedef struct plssvm_mi_ctx plssvm_mi_ctx;
+
+/* Number of visible HIP devices (>= 0), or a negative error code. */
+PLSSVM_MI_API int plssvm_mi_device_count(void);
+
+/* Replaces hip::csvm<T>::csvm(const parameter<T>&) (src/plssvm/backends/HIP/csvm.hip.cpp:38-81)
+ * for the parameters the hot path reads (include/plssvm/csvm.hpp:242-277): real_bytes 4|8 (T),
+ * kernel, degree, gamma, coef0, cost (C). device = HIP device ordinal this context drives. */
+PLSSVM_MI_API int plssvm_mi_create(int real_bytes, int kernel, int degree, double gamma, double coef0, double cost, int device,
+                     plssvm_mi_ctx **out);
+PLSSVM_MI_API void plssvm_mi_destroy(plssvm_mi_ctx *ctx);
+PLSSVM_MI_API const char *plssvm_mi_last_error(const plssvm_mi_ctx *ctx);
+PLSSVM_MI_API int plssvm_mi_set_option(plssvm_mi_ctx *ctx, int key, int64_t value);
+
+/* Test hooks mirroring mock_hip_csvm::set_cost / set_QA_cost (tests/backends/HIP/mock_hip_csvm.hpp:24-51). */
+PLSSVM_MI_API int plssvm_mi_set_cost(plssvm_mi_ctx *ctx, double cost);
+PLSSVM_MI_API int plssvm_mi_set_qa_cost(plssvm_mi_ctx *ctx, double qa_cost);
+
+/* Multi-GPU row-block group: one context per process/GPU. rank 0 calls
+ * plssvm_mi_get_unique_id, the id (PLSSVM_MI_UNIQUE_ID_BYTES bytes) is shared out of band (e.g.
+ * torch.distributed), every rank calls plssvm_mi_comm_init. Replaces the feature-split device
+ * list + host-staged device_reduction (src/plssvm/backends/gpu_csvm.cpp:136-139,366-386). */
+#define PLSSVM_MI_UNIQUE_ID_BYTES 128
+PLSSVM_MI_API int plssvm_mi_get_unique_id(void *id_out);
+PLSSVM_MI_API int plssvm_mi_comm_init(plssvm_mi_ctx *ctx, int rank, int world_size, const void *unique_id);
+
+/* gpu_csvm::setup_data_on_device (src/plssvm/backends/gpu_csvm.cpp:130-157) for dense data:
+ * X is row-major [n][d] host memory of the context's real type (all n points, the last one
+ * included, exactly the reference's data_ptr_). */
+PLSSVM_MI_API int plssvm_mi_setup_dense(plssvm_mi_ctx *ctx, const void *X, int64_t n, int64_t d);
+
+/* Sparse setup (build-defined format): CSR with int64 rowptr[n+1],
+ * int32 col[nnz] ascending per row, values in val_fmt (PLSSVM_MI_VAL_REAL: real[nnz];
+ * PLSSVM_MI_VAL_FP22: uint32 packed words, orc/fp22 layout). Semantics == dense setup on the
+ * densified matrix (the reference parser densifies, src/plssvm/parameter.cpp:66-87). */
+PLSSVM_MI_API int plssvm_mi_setup_csr(plssvm_mi_ctx *ctx, const int64_t *rowptr, const int32_t *col, const void *val,
+                        int val_fmt, int64_t n, int64_t d);
+
+/* gpu_csvm::generate_q (src/plssvm/backends/gpu_csvm.cpp:160-183) + the QA_cost line of
+ * csvm::learn (src/plssvm/csvm.cpp:243): q_out[m] = k(x_i, x_last); *qa_cost_out =
+ * k(x_last, x_last) + 1/C. Also stores q and QA_cost in the context for plssvm_mi_kp. */
+PLSSVM_MI_API int plssvm_mi_generate_q(plssvm_mi_ctx *ctx, void *q_out, double *qa_cost_out);
+
+/* gpu_csvm::run_device_kernel + device_reduction (src/plssvm/backends/gpu_csvm.cpp:353-386):
+ * ret[m] += add * Q~ p, Q~_ij = k(x_i,x_j) + QA_cost - q_i - q_j + [i==j]/C. q may be NULL to use
+ * the context's q (from generate_q); otherwise q[m] is uploaded first. All host buffers. */
+PLSSVM_MI_API int plssvm_mi_kp(plssvm_mi_ctx *ctx, const void *q, const void *p, void *ret, double add);
+
+/* gpu_csvm::solver_CG (src/plssvm/backends/gpu_csvm.cpp:186-324) with the OpenMP backend's
+ * normative semantics (src/plssvm/backends/OpenMP/csvm.cpp:82-170; including the every-50th
+ * explicit residual r = b - Q~x that the reference HIP path gets wrong on one GPU). b[m], q[m]
+ * (NULL = context q); x_out[m]; delta_trace (nullable, imax+1 doubles: delta0 then delta after
+ * each iteration); *iters = CG iterations run. Vectors stay device-resident throughout. */
+PLSSVM_MI_API int plssvm_mi_solve_cg(plssvm_mi_ctx *ctx, const void *b, const void *q, int64_t imax, double eps, void *x_out,
+                       double *delta_trace, int64_t *iters);
+
+/* Stepwise CG on the same device state (used by bench.py to time single iterations):
+ * begin = x0 = 1, r = b - Q~x, d = r; step runs n iterations (ignores convergence when
+ * force != 0); result copies x and the trace out. */
+PLSSVM_MI_API int plssvm_mi_cg_begin(plssvm_mi_ctx *ctx, const void *b, const void *q, double eps, double *delta0_out);
+PLSSVM_MI_API int plssvm_mi_cg_step(plssvm_mi_ctx *ctx, int64_t n, int force, int64_t *iters_done, int *converged);
+PLSSVM_MI_API int plssvm_mi_cg_result(plssvm_mi_ctx *ctx, void *x_out, double *delta_trace, int64_t trace_len, int64_t *iters);
+
+/* csvm<T>::learn (src/plssvm/csvm.cpp:207-267) on the context's data: y[n] labels (+-1),
+ * imax < 0 means num_features (the reference's imax, csvm.cpp:256). alpha_out[n] (alpha[m] =
+ * -sum), *bias_out (rho = -bias), delta_trace (nullable, imax+1). */
+PLSSVM_MI_API int plssvm_mi_learn(plssvm_mi_ctx *ctx, const void *y, int64_t imax, double eps, void *alpha_out, double *bias_out,
+                    double *delta_trace, int64_t *iters);
+
+/* Timing hook (bench.py): runs `reps` K·p launches (+ reduction/collective) on resident device
+ * buffers (p = a fixed device vector) and reports the average device time per K·p and per
+ * dominant-kernel launch, measured with hipEvents on the context's stream. */
+PLSSVM_MI_API int plssvm_mi_time_kp(plssvm_mi_ctx *ctx, int reps, double *ms_per_kp, double *ms_dominant_kernel);
+
+/* Introspection for roofline accounting: number of pairwise tiles / work units per K·p on this
+ * rank, tile edge, padded sizes, bytes of device memory held. */
+typedef struct {
+    int64_t n, d, m, n_pad, d_pad, nnz;
+    int64_t tiles_total, tiles_local, tile_rows, tile_cols;
+    int64_t device_bytes;
+    int kp_mode, rank, world_size, real_bytes, kernel, is_sparse, val_fmt;
+} plssvm_mi_info;
+PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PLSSVM_MI355X_H */

@@ -1,0 +1,250 @@
+"""plssvm_sparse_fp22_amd — MI355X-native PLSSVM CG hot path (implicit Q~·p), host-side mirror.
+
+Mirrors the reference's C++ surface for this path so tests read like the reference's own:
+
+* :class:`Parameter` ~ ``plssvm::parameter<T>`` (include/plssvm/parameter.hpp:181-194 defaults:
+  C = 1, epsilon = 1e-3, degree = 3, gamma = 1/d, coef0 = 0);
+* :class:`CSVM` ~ ``plssvm::hip::csvm<T>`` / ``detail::gpu_csvm<T, ...>``
+  (include/plssvm/csvm.hpp:33-278, include/plssvm/backends/gpu_csvm.hpp:37-190) including the
+  protected-for-mock hooks of ``mock_hip_csvm`` (tests/backends/HIP/mock_hip_csvm.hpp:24-51):
+  ``setup_data_on_device``, ``generate_q``, ``run_device_kernel`` (+ reduction), ``solver_CG``,
+  ``set_cost``, ``set_QA_cost``.
+
+Everything computes in libplssvm_mi355x.so (hand-written gfx950 HIP kernels) through the C ABI
+``include/plssvm_mi355x.h``; this module only marshals host buffers.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _abi
+from ._abi import BackendError, KERNELS
+from .io import parse_libsvm, parse_model
+
+__all__ = ["Parameter", "CSVM", "BackendError", "parse_libsvm", "parse_model", "device_count", "unique_id"]
+
+
+def device_count() -> int:
+    return int(_abi.lib().plssvm_mi_device_count())
+
+
+def unique_id() -> bytes:
+    """RCCL unique id for a row-block group (rank 0 creates it and shares it out of band)."""
+    buf = ctypes.create_string_buffer(_abi.UNIQUE_ID_BYTES)
+    _abi.check(_abi.lib().plssvm_mi_get_unique_id(buf))
+    return buf.raw
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Parameter:
+    """plssvm::parameter<T> subset used by the hot path."""
+
+    def __init__(self, kernel="linear", degree=3, gamma=0.0, coef0=0.0, cost=1.0, epsilon=1e-3,
+                 real_type=np.float64, print_info=False):
+        if kernel not in KERNELS:
+            raise ValueError(f"Unknown kernel type {kernel!r}")
+        self.kernel = kernel
+        self.degree = int(degree)
+        self.gamma = gamma
+        self.coef0 = coef0
+        self.cost = cost
+        self.epsilon = epsilon
+        self.real_type = np.dtype(real_type)
+        self.print_info = print_info
+        self.data = None  # dense [n][d]
+        self.csr = None  # (rowptr, col, val, n, d); val real or packed FP22 words
+        self.val_fmt = _abi.VAL_REAL
+        self.labels = None
+
+    def parse_train_file(self, path, sparse=False):
+        X, y = parse_libsvm(path, dtype=self.real_type, sparse=sparse)
+        if sparse:
+            self.csr, self.data = X, None
+            d = X[4]
+        else:
+            self.data, self.csr = X, None
+            d = X.shape[1]
+        self.labels = y
+        if self.gamma == 0:  # parameter.cpp:150-152
+            self.gamma = float(self.real_type.type(1) / self.real_type.type(d))
+        return self
+
+    @property
+    def num_features(self):
+        return self.data.shape[1] if self.data is not None else int(self.csr[4])
+
+    @property
+    def num_data_points(self):
+        return self.data.shape[0] if self.data is not None else int(self.csr[3])
+
+
+class CSVM:
+    """One MI355X context (one GPU, one HIP stream). ``world_size > 1`` joins a row-block group."""
+
+    def __init__(self, params: Parameter, device=0, rank=0, world_size=1, uid=None, kp_mode="auto"):
+        if params.data is None and params.csr is None:
+            raise ValueError("No data points provided!")
+        if params.data is not None:
+            if params.data.ndim != 2 or params.data.shape[0] == 0:
+                raise ValueError("Data set is empty!")
+            if params.data.shape[1] == 0:
+                raise ValueError("No features provided for the data points!")
+        self.params = params
+        self.dtype = params.real_type
+        self.num_data_points = params.num_data_points
+        self.num_features = params.num_features
+        gamma = params.gamma if params.gamma != 0 else 1.0 / self.num_features
+        self._ctx = ctypes.c_void_p()
+        L = _abi.lib()
+        _abi.check(L.plssvm_mi_create(self.dtype.itemsize, KERNELS[params.kernel], params.degree, float(gamma),
+                                      float(params.coef0), float(params.cost), device, ctypes.byref(self._ctx)))
+        mode = {"auto": _abi.KP_AUTO, "pairwise": _abi.KP_PAIRWISE, "factored": _abi.KP_FACTORED}[kp_mode]
+        if mode != _abi.KP_AUTO:
+            self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_KP_MODE, mode))
+        if world_size > 1:
+            self._uid = ctypes.create_string_buffer(uid, _abi.UNIQUE_ID_BYTES)
+            self._check(L.plssvm_mi_comm_init(self._ctx, rank, world_size, self._uid))
+        self.world_size = world_size
+        self.rank = rank
+        self.QA_cost = None
+        self.alpha = None
+        self.bias = None
+        self.trace = None
+        self.iters = None
+        self._on_device = False
+
+    # ---- lifetime ----
+    def close(self):
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            _abi.lib().plssvm_mi_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, code):
+        _abi.check(code, self._ctx)
+
+    @property
+    def m(self):
+        return self.num_data_points - 1
+
+    # ---- gpu_csvm hot-path surface ----
+    def setup_data_on_device(self):
+        L = _abi.lib()
+        p = self.params
+        if p.data is not None:
+            X = np.ascontiguousarray(p.data, dtype=self.dtype)
+            self._check(L.plssvm_mi_setup_dense(self._ctx, _ptr(X), X.shape[0], X.shape[1]))
+        else:
+            rowptr, col, val, n, d = p.csr
+            rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+            col = np.ascontiguousarray(col, dtype=np.int32)
+            val = np.ascontiguousarray(val, dtype=np.uint32 if p.val_fmt == _abi.VAL_FP22 else self.dtype)
+            self._check(L.plssvm_mi_setup_csr(self._ctx, _ptr(rowptr), _ptr(col), _ptr(val), p.val_fmt, n, d))
+        self._on_device = True
+
+    def generate_q(self):
+        q = np.zeros(max(self.m, 1), dtype=self.dtype)
+        qa = ctypes.c_double()
+        self._check(_abi.lib().plssvm_mi_generate_q(self._ctx, _ptr(q), ctypes.byref(qa)))
+        self.QA_cost = self.dtype.type(qa.value)
+        return q[: self.m]
+
+    def set_cost(self, cost):
+        self._check(_abi.lib().plssvm_mi_set_cost(self._ctx, float(cost)))
+
+    def set_QA_cost(self, qa):
+        self._check(_abi.lib().plssvm_mi_set_qa_cost(self._ctx, float(qa)))
+        self.QA_cost = self.dtype.type(qa)
+
+    def run_device_kernel(self, q, ret, d, add):
+        """ret += add * Q~ d (run_device_kernel + device_reduction); q=None uses the device q."""
+        assert ret.dtype == self.dtype and ret.flags.c_contiguous
+        qq = None if q is None else np.ascontiguousarray(q, dtype=self.dtype)
+        dd = np.ascontiguousarray(d, dtype=self.dtype)
+        self._check(_abi.lib().plssvm_mi_kp(self._ctx, _ptr(qq), _ptr(dd), _ptr(ret), float(add)))
+        return ret
+
+    def solver_CG(self, b, imax, eps, q=None):
+        b = np.ascontiguousarray(b, dtype=self.dtype)
+        qq = None if q is None else np.ascontiguousarray(q, dtype=self.dtype)
+        x = np.zeros(max(self.m, 1), dtype=self.dtype)
+        trace = np.full(imax + 1, np.nan)
+        it = ctypes.c_int64()
+        self._check(_abi.lib().plssvm_mi_solve_cg(self._ctx, _ptr(b), _ptr(qq), imax, float(eps), _ptr(x),
+                                                  _ptr(trace), ctypes.byref(it)))
+        self.iters = it.value
+        self.trace = trace[: it.value + 1]
+        return x[: self.m]
+
+    def learn(self, imax=-1):
+        """csvm<T>::learn(): setup, q, QA_cost, CG with imax = num_features, bias, alpha[m] = -sum."""
+        if self.params.labels is None:
+            raise ValueError("No labels given for training! Maybe the data is only usable for prediction?")
+        if not self._on_device:
+            self.setup_data_on_device()
+        y = np.ascontiguousarray(self.params.labels, dtype=self.dtype)
+        alpha = np.zeros(self.num_data_points, dtype=self.dtype)
+        bias = ctypes.c_double()
+        im = self.num_features if imax < 0 else imax
+        trace = np.full(im + 1, np.nan)
+        it = ctypes.c_int64()
+        self._check(_abi.lib().plssvm_mi_learn(self._ctx, _ptr(y), im, float(self.params.epsilon), _ptr(alpha),
+                                               ctypes.byref(bias), _ptr(trace), ctypes.byref(it)))
+        self.alpha = alpha
+        self.bias = self.dtype.type(bias.value)
+        self.rho = -self.bias
+        self.iters = it.value
+        self.trace = trace[: it.value + 1]
+        return self
+
+    # ---- stepwise CG + timing (bench.py) ----
+    def cg_begin(self, b, q=None, eps=None):
+        b = np.ascontiguousarray(b, dtype=self.dtype)
+        qq = None if q is None else np.ascontiguousarray(q, dtype=self.dtype)
+        d0 = ctypes.c_double()
+        e = self.params.epsilon if eps is None else eps
+        self._check(_abi.lib().plssvm_mi_cg_begin(self._ctx, _ptr(b), _ptr(qq), float(e), ctypes.byref(d0)))
+        return d0.value
+
+    def cg_step(self, n, force=False):
+        it = ctypes.c_int64()
+        conv = ctypes.c_int()
+        self._check(_abi.lib().plssvm_mi_cg_step(self._ctx, n, 1 if force else 0, ctypes.byref(it),
+                                                 ctypes.byref(conv)))
+        return it.value, bool(conv.value)
+
+    def cg_result(self, trace_len=0):
+        x = np.zeros(max(self.m, 1), dtype=self.dtype)
+        trace = np.full(max(trace_len, 1), np.nan)
+        it = ctypes.c_int64()
+        self._check(_abi.lib().plssvm_mi_cg_result(self._ctx, _ptr(x), _ptr(trace), trace_len, ctypes.byref(it)))
+        return x[: self.m], trace[: min(trace_len, it.value + 1)], it.value
+
+    def time_kp(self, reps=5):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        self._check(_abi.lib().plssvm_mi_time_kp(self._ctx, reps, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def info(self):
+        inf = _abi.Info()
+        self._check(_abi.lib().plssvm_mi_get_info(self._ctx, ctypes.byref(inf)))
+        return {k: getattr(inf, k) for k, _ in _abi.Info._fields_}
+
+    def get_num_devices(self):
+        return self.world_size

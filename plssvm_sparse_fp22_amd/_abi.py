@@ -1,0 +1,99 @@
+"""ctypes binding of libplssvm_mi355x.so (C ABI: include/plssvm_mi355x.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (``make -C
+plssvm_sparse_fp22_amd/csrc``). There is no fallback: if the library is missing or cannot be
+loaded, :func:`lib` raises, so nothing silently runs on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libplssvm_mi355x.so")
+
+OK = 0
+ERR = {-1: "ERR_ARG", -2: "ERR_HIP", -3: "ERR_RCCL", -4: "ERR_OOM", -5: "ERR_UNSUPPORTED", -6: "ERR_STATE",
+       -7: "ERR_NODEV"}
+KERNELS = {"linear": 0, "polynomial": 1, "poly": 1, "rbf": 2}
+VAL_REAL, VAL_FP22 = 0, 1
+KP_AUTO, KP_PAIRWISE, KP_FACTORED = 0, 1, 2
+OPT_KP_MODE = 1
+UNIQUE_ID_BYTES = 128
+
+# every symbol include/plssvm_mi355x.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "plssvm_mi_device_count", "plssvm_mi_create", "plssvm_mi_destroy", "plssvm_mi_last_error",
+    "plssvm_mi_set_option", "plssvm_mi_set_cost", "plssvm_mi_set_qa_cost", "plssvm_mi_get_unique_id",
+    "plssvm_mi_comm_init", "plssvm_mi_setup_dense", "plssvm_mi_setup_csr", "plssvm_mi_generate_q", "plssvm_mi_kp",
+    "plssvm_mi_solve_cg", "plssvm_mi_cg_begin", "plssvm_mi_cg_step", "plssvm_mi_cg_result", "plssvm_mi_learn",
+    "plssvm_mi_time_kp", "plssvm_mi_get_info",
+)
+
+
+class Info(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int64) for k in ("n", "d", "m", "n_pad", "d_pad", "nnz", "tiles_total", "tiles_local",
+                                              "tile_rows", "tile_cols", "device_bytes")] + \
+               [(k, ctypes.c_int) for k in ("kp_mode", "rank", "world_size", "real_bytes", "kernel", "is_sparse",
+                                            "val_fmt")]
+
+
+class BackendError(RuntimeError):
+    """plssvm::hip::backend_exception equivalent raised for a non-zero ABI return code."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"{ERR.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                              "(make -C plssvm_sparse_fp22_amd/csrc); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def _declare(L):
+    P, I64, I, D = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double
+    PP = ctypes.POINTER(ctypes.c_void_p)
+    PD, PI64, PI = ctypes.POINTER(D), ctypes.POINTER(I64), ctypes.POINTER(I)
+    sig = {
+        "plssvm_mi_device_count": ([], I),
+        "plssvm_mi_create": ([I, I, I, D, D, D, I, PP], I),
+        "plssvm_mi_destroy": ([P], None),
+        "plssvm_mi_last_error": ([P], ctypes.c_char_p),
+        "plssvm_mi_set_option": ([P, I, I64], I),
+        "plssvm_mi_set_cost": ([P, D], I),
+        "plssvm_mi_set_qa_cost": ([P, D], I),
+        "plssvm_mi_get_unique_id": ([P], I),
+        "plssvm_mi_comm_init": ([P, I, I, P], I),
+        "plssvm_mi_setup_dense": ([P, P, I64, I64], I),
+        "plssvm_mi_setup_csr": ([P, P, P, P, I, I64, I64], I),
+        "plssvm_mi_generate_q": ([P, P, PD], I),
+        "plssvm_mi_kp": ([P, P, P, P, D], I),
+        "plssvm_mi_solve_cg": ([P, P, P, I64, D, P, P, PI64], I),
+        "plssvm_mi_cg_begin": ([P, P, P, D, PD], I),
+        "plssvm_mi_cg_step": ([P, I64, I, PI64, PI], I),
+        "plssvm_mi_cg_result": ([P, P, P, I64, PI64], I),
+        "plssvm_mi_learn": ([P, P, I64, D, P, PD, P, PI64], I),
+        "plssvm_mi_time_kp": ([P, I, PD, PD], I),
+        "plssvm_mi_get_info": ([P, ctypes.POINTER(Info)], I),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+
+
+def check(code, ctx=None):
+    if code != OK:
+        msg = lib().plssvm_mi_last_error(ctx)
+        raise BackendError(code, msg.decode() if msg else "")

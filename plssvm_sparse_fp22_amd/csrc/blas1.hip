@@ -1,0 +1,208 @@
+// Device-resident CG vector kernels and deterministic reductions.
+//
+// Replaces the host BLAS-1 of gpu_csvm::solver_CG (src/plssvm/backends/gpu_csvm.cpp:262-303) and
+// the per-iteration H2D/D2H copies around it: x, r, d, Ad and every CG scalar stay on the GPU.
+// Operation order follows openmp::csvm::solver_CG (src/plssvm/backends/OpenMP/csvm.cpp:82-170):
+// x = x + (alpha*d), r = r - (alpha*Ad), d = (beta*d) + r, each product rounded before the add
+// (no contraction). Dots are two-stage tree reductions with a fixed grid: bitwise reproducible.
+#include "kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace plssvm_mi {
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T *red) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    T s = 0;
+    if (threadIdx.x == 0) {
+        for (int w = 0; w < (int) (blockDim.x >> 6); ++w) s += red[w];
+    }
+    return s;
+}
+
+// partials[blockIdx] = sum a*b (b null: sum a); second pair (c, e) into partials[RED_BLOCKS + blockIdx]
+template <typename T>
+__global__ __launch_bounds__(256) void dot2_kernel(const T *__restrict__ a, const T *__restrict__ b,
+                                                   const T *__restrict__ c, const T *__restrict__ e, int64_t n,
+                                                   T *__restrict__ partials, const cg_scalars<T> *status) {
+    if (status != nullptr && status->converged) return;
+    __shared__ T red[8];
+    T s1 = 0, s2 = 0;
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        const T av = a[i];
+        s1 += b ? av * b[i] : av;
+        if (c) s2 += c[i] * (e ? e[i] : T(1));
+    }
+    const T r1 = block_sum(s1, red);
+    __syncthreads();
+    const T r2 = c ? block_sum(s2, red) : T(0);
+    if (threadIdx.x == 0) {
+        partials[blockIdx.x] = r1;
+        partials[RED_BLOCKS + blockIdx.x] = r2;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dot_final_kernel(const T *__restrict__ partials, cg_scalars<T> *sc, int op,
+                                                        int64_t run, double *trace, int64_t trace_cap,
+                                                        T *plain_out) {
+    if (op != FIN_PLAIN && sc->converged) return;
+    __shared__ T red[8];
+    T s1 = 0, s2 = 0;
+    for (int i = threadIdx.x; i < RED_BLOCKS; i += blockDim.x) {
+        s1 += partials[i];
+        s2 += partials[RED_BLOCKS + i];
+    }
+    const T r1 = block_sum(s1, red);
+    __syncthreads();
+    const T r2 = block_sum(s2, red);
+    if (threadIdx.x != 0) return;
+    switch (op) {
+        case FIN_SP_SQP:
+            sc->sp = r1;
+            sc->sqp = r2;
+            break;
+        case FIN_DELTA0:  // delta = r.r after r = b - Q~x
+            sc->delta = r1;
+            sc->delta0 = r1;
+            sc->eps2delta0 = sc->force ? T(-1) : sc->eps2delta0 * r1;  // host preset eps^2
+            if (trace && trace_cap > 0) trace[0] = (double) r1;
+            break;
+        case FIN_ALPHA:  // alpha = delta / (d . Ad)
+            sc->dAd = r1;
+            sc->alpha = sc->delta / r1;
+            break;
+        case FIN_DELTA: {  // delta_new = r.r; convergence test; beta
+            const T delta_old = sc->delta;
+            sc->delta = r1;
+            sc->iters = run + 1;
+            if (trace && run + 1 < trace_cap) trace[run + 1] = (double) r1;
+            if (r1 <= sc->eps2delta0) {
+                sc->converged = 1;
+            } else {
+                sc->beta = r1 / delta_old;
+            }
+            break;
+        }
+        default:
+            if (plain_out) {
+                plain_out[0] = r1;
+                plain_out[1] = r2;
+            }
+            break;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void cg_init_kernel(const T *__restrict__ b, int64_t m, T *__restrict__ x,
+                                                      T *__restrict__ r) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    x[i] = T(1);
+    r[i] = b[i];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void copy_kernel(const T *__restrict__ src, int64_t n, T *__restrict__ dst,
+                                                   const cg_scalars<T> *status) {
+    if (status != nullptr && status->converged) return;
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void cg_update_kernel(T *__restrict__ x, T *__restrict__ r, const T *__restrict__ d,
+                                                        const T *__restrict__ Ad, const T *__restrict__ b, int reset,
+                                                        int64_t m, const cg_scalars<T> *sc) {
+    if (sc->converged) return;
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const T alpha = sc->alpha;
+    const T t = alpha * d[i];
+    x[i] = x[i] + t;
+    if (reset) {
+        r[i] = b[i];
+    } else {
+        const T u = alpha * Ad[i];
+        r[i] = r[i] - u;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void cg_direction_kernel(T *__restrict__ d, const T *__restrict__ r, int64_t m,
+                                                           const cg_scalars<T> *sc) {
+    if (sc->converged) return;
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const T t = sc->beta * d[i];
+    d[i] = t + r[i];
+}
+
+}  // namespace
+
+template <typename T>
+void launch_dot2(const T *a, const T *b, const T *c, const T *e, int64_t n, T *partials, const cg_scalars<T> *status,
+                 hipStream_t s) {
+    hipLaunchKernelGGL(dot2_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, s, a, b, c, e, n, partials, status);
+    MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_dot_final(const T *partials, cg_scalars<T> *sc, int op, int64_t run, double *trace, int64_t trace_cap,
+                      T *plain_out, hipStream_t s) {
+    hipLaunchKernelGGL(dot_final_kernel<T>, dim3(1), dim3(256), 0, s, partials, sc, op, run, trace, trace_cap,
+                       plain_out);
+    MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_cg_init(const T *b, int64_t m, T *x, T *r, hipStream_t s) {
+    if (m <= 0) return;
+    hipLaunchKernelGGL(cg_init_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, b, m, x, r);
+    MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_copy(const T *src, int64_t n, T *dst, const cg_scalars<T> *status, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(copy_kernel<T>, dim3((unsigned) ceil_div(n, 256)), dim3(256), 0, s, src, n, dst, status);
+    MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_cg_update(T *x, T *r, const T *d, const T *Ad, const T *b, int reset, int64_t m, const cg_scalars<T> *sc,
+                      hipStream_t s) {
+    if (m <= 0) return;
+    hipLaunchKernelGGL(cg_update_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, x, r, d, Ad, b, reset,
+                       m, sc);
+    MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_cg_direction(T *d, const T *r, int64_t m, const cg_scalars<T> *sc, hipStream_t s) {
+    if (m <= 0) return;
+    hipLaunchKernelGGL(cg_direction_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, d, r, m, sc);
+    MI_LAUNCH_CHECK();
+}
+
+#define INST(T)                                                                                                     \
+    template void launch_dot2<T>(const T *, const T *, const T *, const T *, int64_t, T *, const cg_scalars<T> *, \
+                                 hipStream_t);                                                                    \
+    template void launch_dot_final<T>(const T *, cg_scalars<T> *, int, int64_t, double *, int64_t, T *,           \
+                                      hipStream_t);                                                               \
+    template void launch_cg_init<T>(const T *, int64_t, T *, T *, hipStream_t);                                   \
+    template void launch_copy<T>(const T *, int64_t, T *, const cg_scalars<T> *, hipStream_t);                    \
+    template void launch_cg_update<T>(T *, T *, const T *, const T *, const T *, int, int64_t,                    \
+                                      const cg_scalars<T> *, hipStream_t);                                        \
+    template void launch_cg_direction<T>(T *, const T *, int64_t, const cg_scalars<T> *, hipStream_t);
+INST(float)
+INST(double)
+#undef INST
+
+}  // namespace plssvm_mi

@@ -1,0 +1,250 @@
+// C ABI (include/plssvm_mi355x.h): exception-free wrappers around engine<float|double>.
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../../include/plssvm_mi355x.h"
+#include "engine.hpp"
+
+using plssvm_mi::engine;
+using plssvm_mi::mi_error;
+
+struct plssvm_mi_ctx {
+    int real_bytes = 8;
+    int kernel = 0;
+    std::unique_ptr<plssvm_mi::engine_base> eng;
+    std::string err;
+
+    template <typename F>
+    int call(F &&f) {
+        try {
+            if (real_bytes == 4) {
+                f(*static_cast<engine<float> *>(eng.get()));
+            } else {
+                f(*static_cast<engine<double> *>(eng.get()));
+            }
+            err.clear();
+            return PLSSVM_MI_OK;
+        } catch (const mi_error &e) {
+            err = e.what();
+            return e.code;
+        } catch (const std::bad_alloc &) {
+            err = "host allocation failed";
+            return PLSSVM_MI_ERR_OOM;
+        } catch (const std::exception &e) {
+            err = e.what();
+            return PLSSVM_MI_ERR_ARG;
+        }
+    }
+};
+
+namespace {
+thread_local std::string g_create_error;
+}
+
+extern "C" {
+
+int plssvm_mi_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int plssvm_mi_create(int real_bytes, int kernel, int degree, double gamma, double coef0, double cost, int device,
+                     plssvm_mi_ctx **out) {
+    if (out == nullptr) return PLSSVM_MI_ERR_ARG;
+    *out = nullptr;
+    if (real_bytes != 4 && real_bytes != 8) return PLSSVM_MI_ERR_ARG;
+    if (kernel < 0 || kernel > 2) return PLSSVM_MI_ERR_UNSUPPORTED;  // unsupported_kernel_type_exception
+    if (kernel == 1 && degree < 0) return PLSSVM_MI_ERR_ARG;
+    if (!(cost > 0)) return PLSSVM_MI_ERR_ARG;
+    const int ndev = plssvm_mi_device_count();
+    if (ndev <= 0) {
+        g_create_error = "HIP backend selected but no HIP devices were found!";
+        return PLSSVM_MI_ERR_NODEV;
+    }
+    if (device < 0 || device >= ndev) return PLSSVM_MI_ERR_ARG;
+    try {
+        auto ctx = std::make_unique<plssvm_mi_ctx>();
+        ctx->real_bytes = real_bytes;
+        ctx->kernel = kernel;
+        if (real_bytes == 4) {
+            ctx->eng = std::make_unique<engine<float>>(kernel, degree, gamma, coef0, cost, device);
+        } else {
+            ctx->eng = std::make_unique<engine<double>>(kernel, degree, gamma, coef0, cost, device);
+        }
+        *out = ctx.release();
+        return PLSSVM_MI_OK;
+    } catch (const mi_error &e) {
+        g_create_error = e.what();
+        return e.code;
+    } catch (const std::exception &e) {
+        g_create_error = e.what();
+        return PLSSVM_MI_ERR_HIP;
+    }
+}
+
+void plssvm_mi_destroy(plssvm_mi_ctx *ctx) { delete ctx; }
+
+const char *plssvm_mi_last_error(const plssvm_mi_ctx *ctx) {
+    return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}
+
+int plssvm_mi_set_option(plssvm_mi_ctx *ctx, int key, int64_t value) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        if (key != PLSSVM_MI_OPT_KP_MODE || value < 0 || value > 2) throw mi_error(PLSSVM_MI_ERR_ARG, "bad option");
+        if (e.have_data) throw mi_error(PLSSVM_MI_ERR_STATE, "set options before setup");
+        e.kp_mode = (int) value;
+    });
+}
+
+int plssvm_mi_set_cost(plssvm_mi_ctx *ctx, double cost) {
+    if (!ctx || !(cost > 0)) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) { e.cost = (decltype(e.cost)) cost; });
+}
+
+int plssvm_mi_set_qa_cost(plssvm_mi_ctx *ctx, double qa) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        e.need_data();
+        e.QA_cost = (decltype(e.QA_cost)) qa;
+        e.have_q = true;
+    });
+}
+
+int plssvm_mi_get_unique_id(void *id_out) {
+    if (!id_out) return PLSSVM_MI_ERR_ARG;
+    static_assert(sizeof(ncclUniqueId) == PLSSVM_MI_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return PLSSVM_MI_ERR_RCCL;
+    std::memcpy(id_out, &id, sizeof(id));
+    return PLSSVM_MI_OK;
+}
+
+int plssvm_mi_comm_init(plssvm_mi_ctx *ctx, int rank, int world_size, const void *unique_id) {
+    if (!ctx || (world_size > 1 && !unique_id)) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) { e.comm_init(rank, world_size, unique_id); });
+}
+
+int plssvm_mi_setup_dense(plssvm_mi_ctx *ctx, const void *X, int64_t n, int64_t d) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        e.setup_dense(static_cast<const T *>(X), n, d);
+    });
+}
+
+int plssvm_mi_setup_csr(plssvm_mi_ctx *ctx, const int64_t *rowptr, const int32_t *col, const void *val, int val_fmt,
+                        int64_t n, int64_t d) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) { e.setup_csr(rowptr, col, val, val_fmt, n, d); });
+}
+
+int plssvm_mi_generate_q(plssvm_mi_ctx *ctx, void *q_out, double *qa_cost_out) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        e.generate_q(static_cast<T *>(q_out), qa_cost_out);
+    });
+}
+
+int plssvm_mi_kp(plssvm_mi_ctx *ctx, const void *q, const void *p, void *ret, double add) {
+    if (!ctx || !p || !ret) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        e.kp_host(static_cast<const T *>(q), static_cast<const T *>(p), static_cast<T *>(ret), (T) add);
+    });
+}
+
+int plssvm_mi_solve_cg(plssvm_mi_ctx *ctx, const void *b, const void *q, int64_t imax, double eps, void *x_out,
+                       double *delta_trace, int64_t *iters) {
+    if (!ctx || !b || !x_out) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        e.solve_cg(static_cast<const T *>(b), static_cast<const T *>(q), imax, (T) eps, static_cast<T *>(x_out),
+                   delta_trace, iters);
+    });
+}
+
+int plssvm_mi_cg_begin(plssvm_mi_ctx *ctx, const void *b, const void *q, double eps, double *delta0_out) {
+    if (!ctx || !b) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        e.cg_begin(static_cast<const T *>(b), static_cast<const T *>(q), (T) eps, false, delta0_out, 4096);
+    });
+}
+
+int plssvm_mi_cg_step(plssvm_mi_ctx *ctx, int64_t n, int force, int64_t *iters_done, int *converged) {
+    if (!ctx || n < 0) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        if (force) {
+            // bench mode: keep iterating past convergence with identical work per iteration
+            using T = std::remove_reference_t<decltype(e.gamma)>;
+            plssvm_mi::cg_scalars<T> h{};
+            MI_HIP_CHECK(hipMemcpyAsync(&h, e.sc.get(), sizeof(h), hipMemcpyDeviceToHost, e.stream));
+            MI_HIP_CHECK(hipStreamSynchronize(e.stream));
+            if (!h.force) {
+                h.force = 1;
+                h.eps2delta0 = T(-1);
+                h.converged = 0;
+                MI_HIP_CHECK(hipMemcpyAsync(e.sc.get(), &h, sizeof(h), hipMemcpyHostToDevice, e.stream));
+            }
+        }
+        bool conv = false;
+        int64_t it = 0;
+        e.cg_step(n, conv, it);
+        if (iters_done) *iters_done = it;
+        if (converged) *converged = conv ? 1 : 0;
+    });
+}
+
+int plssvm_mi_cg_result(plssvm_mi_ctx *ctx, void *x_out, double *delta_trace, int64_t trace_len, int64_t *iters) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        e.cg_result(static_cast<T *>(x_out), delta_trace, trace_len, iters);
+    });
+}
+
+int plssvm_mi_learn(plssvm_mi_ctx *ctx, const void *y, int64_t imax, double eps, void *alpha_out, double *bias_out,
+                    double *delta_trace, int64_t *iters) {
+    if (!ctx || !alpha_out) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        e.learn(static_cast<const T *>(y), imax, (T) eps, static_cast<T *>(alpha_out), bias_out, delta_trace, iters);
+    });
+}
+
+int plssvm_mi_time_kp(plssvm_mi_ctx *ctx, int reps, double *ms_per_kp, double *ms_dominant_kernel) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) { e.time_kp(reps, ms_per_kp, ms_dominant_kernel); });
+}
+
+int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
+    if (!cctx || !info) return PLSSVM_MI_ERR_ARG;
+    auto *ctx = const_cast<plssvm_mi_ctx *>(cctx);
+    return ctx->call([&](auto &e) {
+        std::memset(info, 0, sizeof(*info));
+        info->n = e.n;
+        info->d = e.d;
+        info->m = e.m;
+        info->n_pad = e.n_pad;
+        info->d_pad = e.d_pad;
+        info->nnz = e.csr.nnz;
+        info->tiles_total = e.t_total;
+        info->tiles_local = e.t1 - e.t0;
+        info->tile_rows = plssvm_mi::KP_TILE;
+        info->tile_cols = plssvm_mi::KP_TILE;
+        info->device_bytes = e.device_bytes();
+        info->kp_mode = e.factored() ? PLSSVM_MI_KP_FACTORED : PLSSVM_MI_KP_PAIRWISE;
+        info->rank = e.rank;
+        info->world_size = e.world;
+        info->real_bytes = (int) sizeof(e.gamma);
+        info->kernel = e.kernel;
+        info->is_sparse = e.sparse ? 1 : 0;
+        info->val_fmt = e.csr.val_fmt;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,419 @@
+// engine<T>: setup, q, K·p and the device-resident CG (host orchestration on one HIP stream).
+//
+// Reference call stack replaced: csvm::learn -> gpu_csvm::setup_data_on_device
+// (src/plssvm/backends/gpu_csvm.cpp:130-157) -> generate_q (:160-183) -> solver_CG (:186-324) ->
+// run_device_kernel (:353-363) -> device_reduction (:366-386).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "engine.hpp"
+
+namespace plssvm_mi {
+
+namespace {
+
+template <typename T>
+ncclDataType_t nccl_type() {
+    return sizeof(T) == 8 ? ncclFloat64 : ncclFloat32;
+}
+
+#define MI_NCCL_CHECK(expr)                                                                                          \
+    do {                                                                                                             \
+        ncclResult_t r_ = (expr);                                                                                    \
+        if (r_ != ncclSuccess) {                                                                                     \
+            throw ::plssvm_mi::mi_error(-3, std::string("RCCL error '") + ncclGetErrorString(r_) + "' (" #expr ")"); \
+        }                                                                                                            \
+    } while (0)
+
+// host kernel_function<k> (include/plssvm/kernel_types.hpp:63-85) for QA_cost = k(x_m, x_m) + 1/C
+template <typename T>
+T host_kernel(int kernel, int degree, T gamma, T coef0, const T *a, const T *b, int64_t d) {
+    T v = 0;
+    if (kernel == 2) {
+        for (int64_t k = 0; k < d; ++k) {
+            const T diff = a[k] - b[k];
+            v = std::fma(diff, diff, v);
+        }
+        return std::exp(-gamma * v);
+    }
+    for (int64_t k = 0; k < d; ++k) v = std::fma(a[k], b[k], v);
+    if (kernel == 0) return v;
+    return std::pow(std::fma(gamma, v, coef0), (T) degree);
+}
+
+}  // namespace
+
+template <typename T>
+engine<T>::engine(int kernel_, int degree_, double gamma_, double coef0_, double cost_, int device_) :
+    kernel(kernel_), degree(degree_), gamma((T) gamma_), coef0((T) coef0_), cost((T) cost_), device(device_) {
+    MI_HIP_CHECK(hipSetDevice(device));
+    MI_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    sc.alloc(1, stream);
+    red.alloc(2 * RED_BLOCKS, stream);
+}
+
+template <typename T>
+engine<T>::~engine() {
+    (void) hipSetDevice(device);
+    if (stream) (void) hipStreamSynchronize(stream);
+    if (comm) (void) ncclCommDestroy(comm);
+    XT.reset();
+    partial.reset();
+    if (stream) (void) hipStreamDestroy(stream);
+}
+
+template <typename T>
+bool engine<T>::factored() const {
+    if (kernel != 0) return false;
+    if (kp_mode == 2) return true;
+    if (kp_mode == 1) return false;
+    return sparse;  // AUTO: dense linear runs the MFMA pairwise tiles, sparse linear the factored SpMVs
+}
+
+template <typename T>
+void engine<T>::need_data() const {
+    if (!have_data) throw mi_error(-6, "No data on the device! Maybe a call to setup_data_on_device() is missing?");
+}
+
+template <typename T>
+void engine<T>::need_q() const {
+    if (!have_q) throw mi_error(-6, "No q vector! Maybe a call to generate_q() is missing?");
+}
+
+template <typename T>
+void engine<T>::comm_init(int rank_, int world_, const void *uid) {
+    if (world_ < 1 || rank_ < 0 || rank_ >= world_) throw mi_error(-1, "invalid rank/world_size");
+    if (have_data) throw mi_error(-6, "plssvm_mi_comm_init must be called before setup");
+    MI_HIP_CHECK(hipSetDevice(device));
+    if (comm) {
+        (void) ncclCommDestroy(comm);
+        comm = nullptr;
+    }
+    rank = rank_;
+    world = world_;
+    if (world > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, uid, sizeof(id));
+        MI_NCCL_CHECK(ncclCommInitRank(&comm, world, id, rank));
+    }
+}
+
+template <typename T>
+void engine<T>::allreduce(T *buf, int64_t count) {
+    if (world == 1 || count <= 0) return;
+    MI_NCCL_CHECK(ncclAllReduce(buf, buf, (size_t) count, nccl_type<T>(), ncclSum, comm, stream));
+}
+
+template <typename T>
+void engine<T>::allgather_rows(T *buf) {
+    if (world == 1) return;
+    MI_NCCL_CHECK(ncclAllGather(buf + (int64_t) rank * chunk, buf, (size_t) chunk, nccl_type<T>(), comm, stream));
+}
+
+template <typename T>
+void engine<T>::setup_dense(const T *X, int64_t n_, int64_t d_) {
+    if (X == nullptr || n_ < 1 || d_ < 1) throw mi_error(-1, "Data set is empty!");
+    MI_HIP_CHECK(hipSetDevice(device));
+    sparse = false;
+    n = n_;
+    d = d_;
+    m = n - 1;
+    nb = ceil_div(m, KP_TILE);
+    n_pad = std::max<int64_t>(nb, 1) * KP_TILE;
+    d_pad = round_up(d, kp_bk<T>());
+    // device layout: feature-major XT[d_pad][n_pad] of the first m points; the last point separately
+    // (the reference's data_d_ / data_last_d_, gpu_csvm.cpp:142-155, with 64-bit offsets and tile padding)
+    XT.alloc(d_pad * n_pad, stream);
+    {
+        dev_buf<T> tmp;
+        tmp.alloc(std::max<int64_t>(m, 1) * d, stream, false);
+        if (m > 0) {
+            MI_HIP_CHECK(hipMemcpyAsync(tmp.get(), X, sizeof(T) * (size_t) (m * d), hipMemcpyHostToDevice, stream));
+            launch_transpose<T>(tmp.get(), m, d, XT.get(), n_pad, stream);
+        }
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+    xlast_h.assign(X + m * d, X + m * d + d);
+    xlast.alloc(d_pad, stream);
+    MI_HIP_CHECK(hipMemcpyAsync(xlast.get(), xlast_h.data(), sizeof(T) * (size_t) d, hipMemcpyHostToDevice, stream));
+    norms.alloc(n_pad, stream);
+    if (kernel == 2) launch_row_norms<T>(XT.get(), n_pad, d, norms.get(), stream);
+    finish_setup();
+}
+
+template <typename T>
+void engine<T>::setup_csr(const int64_t *, const int32_t *, const void *, int, int64_t, int64_t) {
+    throw mi_error(-5, "sparse setup not built yet");
+}
+
+template <typename T>
+void engine<T>::finish_setup() {
+    // work split of the implicit matrix over the group (replaces feature_ranges_, gpu_csvm.cpp:136-139)
+    t_total = nb * (nb + 1) / 2;
+    t0 = (t_total * rank) / world;
+    t1 = (t_total * (rank + 1)) / world;
+    chunk = ceil_div(std::max<int64_t>(m, 1), world);
+    r0 = std::min<int64_t>(m, rank * chunk);
+    r1 = std::min<int64_t>(m, r0 + chunk);
+    const int64_t vec_len = std::max<int64_t>(n_pad, chunk * world);
+    if (!sparse && !factored()) {
+        partial.alloc(std::max<int64_t>(nb, 1) * n_pad, stream, false);
+    } else {
+        partial.reset();
+    }
+    q.alloc(vec_len, stream);
+    pv.alloc(vec_len, stream);
+    ret.alloc(vec_len, stream);
+    x.alloc(vec_len, stream);
+    r.alloc(vec_len, stream);
+    dv.alloc(vec_len, stream);
+    Ad.alloc(vec_len, stream);
+    b.alloc(vec_len, stream);
+    raw.alloc(vec_len, stream);
+    w.alloc(std::max<int64_t>(d_pad, 1), stream);
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    have_data = true;
+    have_q = false;
+    cg_active = false;
+}
+
+template <typename T>
+void engine<T>::generate_q(T *q_out, double *qa_out) {
+    need_data();
+    MI_HIP_CHECK(hipSetDevice(device));
+    if (sparse) {
+        launch_q_sparse<T>(kf(), csr, m, xlast.get(), q.get(), stream);
+    } else {
+        launch_q_dense<T>(kf(), XT.get(), n_pad, d, m, xlast.get(), q.get(), stream);
+    }
+    QA_cost = host_kernel<T>(kernel, degree, gamma, coef0, xlast_h.data(), xlast_h.data(), d) + T(1) / cost;
+    if (q_out && m > 0)
+        MI_HIP_CHECK(hipMemcpyAsync(q_out, q.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    if (qa_out) *qa_out = (double) QA_cost;
+    have_q = true;
+}
+
+template <typename T>
+void engine<T>::set_q(const T *q_host) {
+    need_data();
+    if (q_host == nullptr) {
+        need_q();
+        return;
+    }
+    if (m > 0) MI_HIP_CHECK(hipMemcpyAsync(q.get(), q_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
+    if (!have_q) {
+        QA_cost = host_kernel<T>(kernel, degree, gamma, coef0, xlast_h.data(), xlast_h.data(), d) + T(1) / cost;
+        have_q = true;
+    }
+}
+
+// out = (overwrite ? 0 : out) + add * Q~ p   — run_device_kernel + device_reduction
+template <typename T>
+void engine<T>::kp_device(const T *p, T *out, T add, bool overwrite, const cg_scalars<T> *status) {
+    if (m <= 0) return;
+    cg_scalars<T> *scp = sc.get();
+    // sum(p) and sum(q p): the rank-1 parts of Q~ (QA_cost - q_i - q_j) never enter the tiles
+    launch_dot2<T>(p, nullptr, q.get(), p, m, red.get(), status, stream);
+    launch_dot_final<T>(red.get(), scp, FIN_SP_SQP, 0, nullptr, 0, nullptr, stream);
+    if (sparse) {
+        sparse_kp_raw(p, status);
+    } else if (factored()) {
+        launch_gemv_t<T>(XT.get(), n_pad, d, r0, r1, p, w.get(), status, stream);
+        allreduce(w.get(), d);
+        launch_gemv_n<T>(XT.get(), n_pad, d, r0, r1, w.get(), raw.get(), status, stream);
+        allgather_rows(raw.get());
+    } else {
+        launch_kp_tiles<T>(kf(), XT.get(), norms.get(), p, partial.get(), n_pad, d_pad, t0, t1 - t0, status, stream);
+        launch_kp_reduce<T>(partial.get(), nb, n_pad, m, t0, t1, raw.get(), status, stream);
+        allreduce(raw.get(), m);
+    }
+    launch_kp_finalize<T>(raw.get(), q.get(), p, scp, QA_cost, cost_inv(), add, overwrite ? 1 : 0, m, out, status,
+                          stream);
+}
+
+template <typename T>
+void engine<T>::kp_host(const T *q_host, const T *p, T *ret_host, T add) {
+    need_data();
+    MI_HIP_CHECK(hipSetDevice(device));
+    set_q(q_host);
+    cg_active = false;
+    MI_HIP_CHECK(hipMemsetAsync(sc.get(), 0, sizeof(cg_scalars<T>), stream));
+    if (m > 0) {
+        MI_HIP_CHECK(hipMemcpyAsync(pv.get(), p, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
+        MI_HIP_CHECK(hipMemcpyAsync(ret.get(), ret_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
+        kp_device(pv.get(), ret.get(), add, false, nullptr);
+        MI_HIP_CHECK(hipMemcpyAsync(ret_host, ret.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
+    }
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+// ---- CG: openmp::csvm::solver_CG semantics (src/plssvm/backends/OpenMP/csvm.cpp:82-170) -------------
+template <typename T>
+void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, double *delta0_out, int64_t trace_len) {
+    need_data();
+    MI_HIP_CHECK(hipSetDevice(device));
+    set_q(q_host);
+    cg_scalars<T> init{};
+    init.eps2delta0 = eps * eps;
+    init.force = force ? 1 : 0;
+    MI_HIP_CHECK(hipMemcpyAsync(sc.get(), &init, sizeof(init), hipMemcpyHostToDevice, stream));
+    trace_cap = std::max<int64_t>(trace_len, 1);
+    if (trace.size() < trace_cap) trace.alloc(trace_cap, stream);
+    if (m > 0) MI_HIP_CHECK(hipMemcpyAsync(b.get(), b_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
+    // x = 1; r = b; r -= Q~x   (csvm.cpp:85-90)
+    launch_cg_init<T>(b.get(), m, x.get(), r.get(), stream);
+    kp_device(x.get(), r.get(), T(-1), false, nullptr);
+    // delta = r.r ; delta0 ; d = r   (:92-97)
+    launch_dot2<T>(r.get(), r.get(), nullptr, nullptr, m, red.get(), nullptr, stream);
+    launch_dot_final<T>(red.get(), sc.get(), FIN_DELTA0, 0, trace.get(), trace_cap, nullptr, stream);
+    launch_copy<T>(r.get(), m, dv.get(), nullptr, stream);
+    run = 0;
+    cg_active = true;
+    if (delta0_out) {
+        cg_scalars<T> h{};
+        MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        *delta0_out = (double) h.delta0;
+    }
+}
+
+template <typename T>
+void engine<T>::cg_step(int64_t nsteps, bool &converged, int64_t &iters) {
+    if (!cg_active) throw mi_error(-6, "cg_step without cg_begin");
+    MI_HIP_CHECK(hipSetDevice(device));
+    const cg_scalars<T> *st = sc.get();
+    for (int64_t s = 0; s < nsteps; ++s, ++run) {
+        // Ad = Q~ d   (:111-113)
+        kp_device(dv.get(), Ad.get(), T(1), true, st);
+        // alpha = delta / (d . Ad)   (:116)
+        launch_dot2<T>(dv.get(), Ad.get(), nullptr, nullptr, m, red.get(), st, stream);
+        launch_dot_final<T>(red.get(), sc.get(), FIN_ALPHA, run, nullptr, 0, nullptr, stream);
+        // x += alpha d; r = b - Q~x every 50th iteration, else r -= alpha Ad   (:119-132)
+        const int reset = (run % 50 == 49) ? 1 : 0;
+        launch_cg_update<T>(x.get(), r.get(), dv.get(), Ad.get(), b.get(), reset, m, st, stream);
+        if (reset) kp_device(x.get(), r.get(), T(-1), false, st);
+        // delta = r.r ; stop test ; beta   (:135-146)
+        launch_dot2<T>(r.get(), r.get(), nullptr, nullptr, m, red.get(), st, stream);
+        launch_dot_final<T>(red.get(), sc.get(), FIN_DELTA, run, trace.get(), trace_cap, nullptr, stream);
+        // d = beta d + r   (:149-151)
+        launch_cg_direction<T>(dv.get(), r.get(), m, st, stream);
+    }
+    cg_scalars<T> h{};
+    MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    converged = h.converged != 0;
+    iters = h.iters;
+}
+
+template <typename T>
+void engine<T>::cg_result(T *x_out, double *trace_out, int64_t trace_len, int64_t *iters) {
+    if (!cg_active) throw mi_error(-6, "cg_result without cg_begin");
+    MI_HIP_CHECK(hipSetDevice(device));
+    cg_scalars<T> h{};
+    MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));
+    if (x_out && m > 0)
+        MI_HIP_CHECK(hipMemcpyAsync(x_out, x.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    const int64_t it = h.iters;
+    if (iters) *iters = it;
+    if (trace_out && trace_len > 0) {
+        const int64_t cnt = std::min<int64_t>(std::min<int64_t>(trace_len, it + 1), trace_cap);
+        MI_HIP_CHECK(hipMemcpy(trace_out, trace.get(), sizeof(double) * (size_t) cnt, hipMemcpyDeviceToHost));
+    }
+}
+
+template <typename T>
+void engine<T>::solve_cg(const T *b_host, const T *q_host, int64_t imax, T eps, T *x_out, double *trace_out,
+                         int64_t *iters) {
+    if (imax < 0) throw mi_error(-1, "imax must be >= 0");
+    cg_begin(b_host, q_host, eps, false, nullptr, imax + 1);
+    bool conv = false;
+    int64_t it = 0;
+    // batches of iterations between host polls; kernels after convergence exit at entry
+    int64_t batch = 4;
+    while (!conv && run < imax) {
+        const int64_t ns = std::min<int64_t>(batch, imax - run);
+        cg_step(ns, conv, it);
+        batch = std::min<int64_t>(batch * 2, 64);
+    }
+    cg_result(x_out, trace_out, imax + 1, iters);
+}
+
+// csvm<T>::learn (src/plssvm/csvm.cpp:207-267)
+template <typename T>
+void engine<T>::learn(const T *y, int64_t imax, T eps, T *alpha_out, double *bias_out, double *trace_out,
+                      int64_t *iters) {
+    need_data();
+    if (y == nullptr) throw mi_error(-1, "No labels given for training! Maybe the data is only usable for prediction?");
+    std::vector<T> qh(std::max<int64_t>(m, 1)), bh(std::max<int64_t>(m, 1));
+    generate_q(qh.data(), nullptr);
+    for (int64_t i = 0; i < m; ++i) bh[i] = y[i] - y[m];  // b = y[0..m) - y[m]   (:238-239)
+    if (imax < 0) imax = d;                                // solver_CG(b, num_features_, ...)  (:256)
+    solve_cg(bh.data(), nullptr, imax, eps, alpha_out, trace_out, iters);
+    T s = 0, qa = 0;
+    for (int64_t i = 0; i < m; ++i) s += alpha_out[i];
+    for (int64_t i = 0; i < m; ++i) qa = std::fma(qh[i], alpha_out[i], qa);
+    const T bias = y[m] + QA_cost * s - qa;  // (:257)
+    alpha_out[m] = -s;                       // (:258)
+    if (bias_out) *bias_out = (double) bias;
+}
+
+template <typename T>
+void engine<T>::time_kp(int reps, double *ms_kp, double *ms_dom) {
+    need_data();
+    need_q();
+    MI_HIP_CHECK(hipSetDevice(device));
+    if (reps < 1) reps = 1;
+    std::vector<T> ph(std::max<int64_t>(m, 1));
+    for (int64_t i = 0; i < m; ++i) ph[i] = T(1) + T((i * 2654435761ull) % 1000) / T(1000);
+    if (m > 0) MI_HIP_CHECK(hipMemcpyAsync(pv.get(), ph.data(), sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
+    MI_HIP_CHECK(hipMemsetAsync(sc.get(), 0, sizeof(cg_scalars<T>), stream));
+    hipEvent_t e0, e1, d0, d1;
+    MI_HIP_CHECK(hipEventCreate(&e0));
+    MI_HIP_CHECK(hipEventCreate(&e1));
+    MI_HIP_CHECK(hipEventCreate(&d0));
+    MI_HIP_CHECK(hipEventCreate(&d1));
+    kp_device(pv.get(), ret.get(), T(1), true, nullptr);  // warm-up
+    double dom = 0;
+    MI_HIP_CHECK(hipEventRecord(e0, stream));
+    for (int it = 0; it < reps; ++it) kp_device(pv.get(), ret.get(), T(1), true, nullptr);
+    MI_HIP_CHECK(hipEventRecord(e1, stream));
+    MI_HIP_CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    MI_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    // dominant kernel alone, same stream, same launches
+    for (int it = 0; it < reps; ++it) {
+        MI_HIP_CHECK(hipEventRecord(d0, stream));
+        if (sparse) {
+            sparse_dominant(pv.get());
+        } else if (factored()) {
+            launch_gemv_n<T>(XT.get(), n_pad, d, r0, r1, w.get(), raw.get(), nullptr, stream);
+        } else {
+            launch_kp_tiles<T>(kf(), XT.get(), norms.get(), pv.get(), partial.get(), n_pad, d_pad, t0, t1 - t0,
+                               nullptr, stream);
+        }
+        MI_HIP_CHECK(hipEventRecord(d1, stream));
+        MI_HIP_CHECK(hipEventSynchronize(d1));
+        float t = 0;
+        MI_HIP_CHECK(hipEventElapsedTime(&t, d0, d1));
+        dom += t;
+    }
+    (void) hipEventDestroy(e0);
+    (void) hipEventDestroy(e1);
+    (void) hipEventDestroy(d0);
+    (void) hipEventDestroy(d1);
+    if (ms_kp) *ms_kp = ms / reps;
+    if (ms_dom) *ms_dom = dom / reps;
+}
+
+template <typename T>
+int64_t engine<T>::device_bytes() const {
+    return XT.bytes() + norms.bytes() + xlast.bytes() + partial.bytes() + q.bytes() * 10 + w.bytes() + csr_bytes();
+}
+
+template struct engine<float>;
+template struct engine<double>;
+
+}  // namespace plssvm_mi

@@ -1,0 +1,132 @@
+// Per-GPU engine behind the C ABI: device memory, one HIP stream, optional RCCL communicator,
+// device-resident CG. One engine<T> per context; T = float | double (the reference's real_type).
+#pragma once
+
+#include <rccl/rccl.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+#include "sparse.hpp"
+
+namespace plssvm_mi {
+
+// RAII device buffer (the reference's move-only device_ptr, src/plssvm/backends/gpu_device_ptr.cpp:58-109,
+// without its per-call hipSetDevice/synchronous copies: all traffic is async on the engine stream)
+template <typename T>
+class dev_buf {
+  public:
+    dev_buf() = default;
+    dev_buf(const dev_buf &) = delete;
+    dev_buf &operator=(const dev_buf &) = delete;
+    dev_buf(dev_buf &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr, o.n_ = 0; }
+    dev_buf &operator=(dev_buf &&o) noexcept {
+        if (this != &o) {
+            reset();
+            p_ = o.p_;
+            n_ = o.n_;
+            o.p_ = nullptr;
+            o.n_ = 0;
+        }
+        return *this;
+    }
+    ~dev_buf() { reset(); }
+    void alloc(int64_t n, hipStream_t s, bool zero = true) {
+        reset();
+        if (n <= 0) return;
+        MI_HIP_CHECK(hipMalloc(&p_, sizeof(T) * (size_t) n));
+        n_ = n;
+        if (zero) MI_HIP_CHECK(hipMemsetAsync(p_, 0, sizeof(T) * (size_t) n, s));
+    }
+    void reset() {
+        if (p_) (void) hipFree(p_);
+        p_ = nullptr;
+        n_ = 0;
+    }
+    T *get() const { return p_; }
+    int64_t size() const { return n_; }
+    int64_t bytes() const { return n_ * (int64_t) sizeof(T); }
+
+  private:
+    T *p_ = nullptr;
+    int64_t n_ = 0;
+};
+
+struct engine_base {
+    virtual ~engine_base() = default;
+};
+
+template <typename T>
+struct engine : engine_base {
+    // ---- parameters (csvm<T> protected state, include/plssvm/csvm.hpp:242-277) ----
+    int kernel = 0, degree = 3;
+    T gamma = 1, coef0 = 0, cost = 1;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int kp_mode = 0;  // PLSSVM_MI_KP_*
+
+    // ---- multi-GPU row-block group ----
+    int rank = 0, world = 1;
+    ncclComm_t comm = nullptr;
+
+    // ---- data ----
+    bool have_data = false, sparse = false;
+    int64_t n = 0, d = 0, m = 0, n_pad = 0, d_pad = 0, nb = 0;
+    std::vector<T> xlast_h;
+    dev_buf<T> XT, norms, xlast;  // dense: XT[d_pad][n_pad]
+    csr_data<T> csr;              // sparse
+
+    // work split
+    int64_t t_total = 0, t0 = 0, t1 = 0;  // pairwise tiles owned by this rank
+    int64_t r0 = 0, r1 = 0, chunk = 0;    // rows owned by this rank (factored / sparse row paths)
+
+    // ---- vectors (n_pad, zero padded) ----
+    dev_buf<T> partial, q, pv, ret, x, r, dv, Ad, b, raw, w, red;
+    dev_buf<cg_scalars<T>> sc;
+    dev_buf<double> trace;
+    int64_t trace_cap = 0;
+    T QA_cost = 0;
+    bool have_q = false;
+    int64_t run = 0;
+    bool cg_active = false;
+
+    engine(int kernel_, int degree_, double gamma_, double coef0_, double cost_, int device_);
+    ~engine() override;
+
+    kfun<T> kf() const { return kfun<T>{ kernel, degree, gamma, coef0 }; }
+    T cost_inv() const { return T(1) / cost; }
+    bool factored() const;
+    void need_data() const;
+    void need_q() const;
+
+    void comm_init(int rank_, int world_, const void *uid);
+    void setup_dense(const T *X, int64_t n_, int64_t d_);
+    void setup_csr(const int64_t *rowptr, const int32_t *col, const void *val, int val_fmt, int64_t n_, int64_t d_);
+    void finish_setup();
+    void generate_q(T *q_out, double *qa_out);
+    void set_q(const T *q_host);
+
+    // out = (overwrite ? 0 : out) + add * Q~ p  (device vectors, length >= m)
+    void kp_device(const T *p, T *out, T add, bool overwrite, const cg_scalars<T> *status);
+    void kp_host(const T *q_host, const T *p, T *ret_host, T add);
+
+    void cg_begin(const T *b_host, const T *q_host, T eps, bool force, double *delta0_out, int64_t trace_len);
+    void cg_step(int64_t nsteps, bool &converged, int64_t &iters);
+    void cg_result(T *x_out, double *trace_out, int64_t trace_len, int64_t *iters);
+    void solve_cg(const T *b, const T *q_host, int64_t imax, T eps, T *x_out, double *trace_out, int64_t *iters);
+    void learn(const T *y, int64_t imax, T eps, T *alpha_out, double *bias_out, double *trace_out, int64_t *iters);
+    void time_kp(int reps, double *ms_kp, double *ms_dom);
+
+    // sparse paths (sparse.hip)
+    void sparse_kp_raw(const T *p, const cg_scalars<T> *status);  // raw[i] = sum_j k_ij p_j, i < m
+    void sparse_dominant(const T *p);                             // the dominant sparse kernel alone (timing)
+    int64_t csr_bytes() const;
+
+    void allreduce(T *buf, int64_t count);
+    void allgather_rows(T *buf);
+    int64_t device_bytes() const;
+};
+
+}  // namespace plssvm_mi

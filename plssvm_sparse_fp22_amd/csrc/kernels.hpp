@@ -1,0 +1,95 @@
+// Launcher declarations for the MI355X PLSSVM hot-path kernels (implemented in *.hip).
+#pragma once
+
+#include "common.hpp"
+
+namespace plssvm_mi {
+
+// kernel parameters of the LS-SVM kernel function (include/plssvm/kernel_types.hpp:63-85)
+template <typename T>
+struct kfun {
+    int kernel;  // 0 linear, 1 polynomial, 2 rbf
+    int degree;
+    T gamma;
+    T coef0;
+};
+
+// device-resident CG scalars (all CG scalars live on the GPU; the host only polls `converged`)
+template <typename T>
+struct cg_scalars {
+    T delta, delta0, alpha, beta, sp, sqp, eps2delta0, dAd;
+    int converged;
+    int force;  // bench mode: never converge (same work per iteration)
+    int64_t iters;
+};
+
+// ---- dense pairwise tiles -----------------------------------------------------------------------
+// tile edge of the implicit Q~ tiles (rows and columns); n_pad is a multiple of this.
+constexpr int KP_TILE = 128;
+template <typename T>
+constexpr int kp_bk() { return sizeof(T) == 8 ? 16 : 32; }
+
+// XT[k][i] = X[i][k] for i < rows, k < d (X row-major [rows][d]); XT is [>=d][n_pad], pre-zeroed
+template <typename T>
+void launch_transpose(const T *X, int64_t rows, int64_t d, T *XT, int64_t n_pad, hipStream_t s);
+
+// row norms ||x_i||^2 (sequential fma chain in feature order) for the RBF norm trick
+template <typename T>
+void launch_row_norms(const T *XT, int64_t n_pad, int64_t d, T *norms, hipStream_t s);
+
+// q_i = k(x_i, x_last), i < m (device_kernel_q_*, include/plssvm/backends/HIP/q_kernel.hip.hpp:32-83)
+template <typename T>
+void launch_q_dense(kfun<T> kf, const T *XT, int64_t n_pad, int64_t d, int64_t m, const T *xlast, T *q,
+                    hipStream_t s);
+
+// partial[c][i]: sum_j in col-block c of k(x_i,x_j) p_j for the lower-triangle tiles [t0, t0+ntiles)
+template <typename T>
+void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *partial, int64_t n_pad, int64_t d_pad,
+                     int64_t t0, int64_t ntiles, const cg_scalars<T> *status, hipStream_t s);
+
+// raw[i] = sum_c partial[c][i] over tiles owned by this rank ([t0, t1)); i < m
+template <typename T>
+void launch_kp_reduce(const T *partial, int64_t nb, int64_t n_pad, int64_t m, int64_t t0, int64_t t1, T *raw,
+                      const cg_scalars<T> *status, hipStream_t s);
+
+// ret[i] = (overwrite ? 0 : ret[i]) + add * (raw[i] + (QA - q_i) * sum(p) - sum(q p) + p_i / C)
+// raw may alias ret only when overwrite is false and ... (never aliased by callers).
+template <typename T>
+void launch_kp_finalize(const T *raw, const T *q, const T *p, const cg_scalars<T> *sc, T QA_cost, T cost_inv, T add,
+                        int overwrite, int64_t m, T *ret, const cg_scalars<T> *status, hipStream_t s);
+
+// ---- linear factored path: Q~p = X_m (X_m^T p) + rank-1 terms --------------------------------------
+template <typename T>
+void launch_gemv_t(const T *XT, int64_t n_pad, int64_t d, int64_t r0, int64_t r1, const T *p, T *w,
+                   const cg_scalars<T> *status, hipStream_t s);  // w[k] = sum_{r0<=i<r1} XT[k][i] p_i
+template <typename T>
+void launch_gemv_n(const T *XT, int64_t n_pad, int64_t d, int64_t r0, int64_t r1, const T *w, T *raw,
+                   const cg_scalars<T> *status, hipStream_t s);  // raw[i] = sum_k XT[k][i] w_k, r0<=i<r1
+
+// ---- BLAS-1 / CG --------------------------------------------------------------------------------
+constexpr int RED_BLOCKS = 512;
+// partials[b] for b < RED_BLOCKS; out = sum(a*b) (b == nullptr: sum(a)); second pair optional
+template <typename T>
+void launch_dot2(const T *a, const T *b, const T *c, const T *e, int64_t n, T *partials, const cg_scalars<T> *status,
+                 hipStream_t s);
+// final reductions with CG scalar updates; `what` selects the update (see blas1.hip)
+enum final_op { FIN_SP_SQP = 0, FIN_DELTA0 = 1, FIN_ALPHA = 2, FIN_DELTA = 3, FIN_PLAIN = 4 };
+template <typename T>
+void launch_dot_final(const T *partials, cg_scalars<T> *sc, int op, int64_t run, double *trace, int64_t trace_cap,
+                      T *plain_out, hipStream_t s);
+template <typename T>
+void launch_cg_init(const T *b, int64_t m, T *x, T *r, hipStream_t s);
+template <typename T>
+void launch_copy(const T *src, int64_t n, T *dst, const cg_scalars<T> *status, hipStream_t s);
+// x += alpha d; if !reset: r -= alpha Ad  else r = b
+template <typename T>
+void launch_cg_update(T *x, T *r, const T *d, const T *Ad, const T *b, int reset, int64_t m, const cg_scalars<T> *sc,
+                      hipStream_t s);
+// d = beta d + r
+template <typename T>
+void launch_cg_direction(T *d, const T *r, int64_t m, const cg_scalars<T> *sc, hipStream_t s);
+
+// ---- sparse (CSR / FP22) ------------------------------------------------------------------------
+// declared in sparse.hpp
+
+}  // namespace plssvm_mi

@@ -1,0 +1,167 @@
+"""GPU parity: the HIP path (through the C ABI) against the C oracle and the reference fixtures.
+
+Tolerances: fp64 K·p <= 1e-12 relative to max|K·p|, alpha/rho <= 1e-9 rel,
+CG delta trace <= 1e-6 rel per iteration; fp32 K·p <= 1e-4 of max|K·p| (norm-trick RBF and a
+different summation order), alpha <= 2e-2 rel, delta <= 1e-3 rel on the first iterations.
+"""
+import numpy as np
+import pytest
+
+from conftest import fixture_path
+import plssvm_sparse_fp22_amd as pm
+from plssvm_sparse_fp22_amd import datagen
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = ["linear", "polynomial", "rbf"]
+DTYPES = [np.float64, np.float32]
+KP_TOL = {np.float64: 1e-12, np.float32: 1e-4}
+
+
+def make_svm(X, y, kernel, dtype, cost=1.0, gamma=None, degree=3, coef0=0.0, kp_mode="auto"):
+    p = pm.Parameter(kernel, degree=degree, gamma=gamma if gamma is not None else 1.0 / X.shape[1], coef0=coef0,
+                     cost=cost, real_type=dtype)
+    p.data = np.ascontiguousarray(X, dtype=dtype)
+    p.labels = None if y is None else np.asarray(y, dtype=dtype)
+    return pm.CSVM(p, kp_mode=kp_mode)
+
+
+def oracle_args(svm):
+    p = svm.params
+    dt = svm.dtype.type
+    return dict(degree=p.degree, gamma=dt(p.gamma), coef0=dt(p.coef0))
+
+
+def check_kp(oracle, X, kernel, dtype, kp_mode="auto", seed=0):
+    svm = make_svm(X, None, kernel, dtype, kp_mode=kp_mode)
+    svm.setup_data_on_device()
+    q = svm.generate_q()
+    data = oracle.Data(X, dtype=dtype)
+    q_ref = oracle.generate_q(kernel, data, **oracle_args(svm))
+    np.testing.assert_allclose(q, q_ref, rtol=KP_TOL[dtype], atol=KP_TOL[dtype] * max(1e-30, np.abs(q_ref).max()))
+    m = X.shape[0] - 1
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(1.0, 2.0, m).astype(dtype)
+    for add in (-1.0, 1.0):
+        ret = np.zeros(m, dtype=dtype)
+        svm.run_device_kernel(None, ret, x, add)
+        want = oracle.kp(kernel, data, q_ref, svm.QA_cost, dtype(1.0), add, x, **oracle_args(svm))
+        scale = max(np.abs(want).max(), 1e-30)
+        np.testing.assert_allclose(ret, want, rtol=0, atol=KP_TOL[dtype] * scale,
+                                   err_msg=f"{kernel} {np.dtype(dtype).name} add={add} shape={X.shape}")
+    svm.close()
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_kp_reference_fixture_500x200(oracle, kernel, dtype):
+    X, _ = pm.parse_libsvm(fixture_path("500x200.libsvm"), dtype=dtype)
+    check_kp(oracle, X, kernel, dtype)
+
+
+@pytest.mark.parametrize("shape", [(2, 1), (3, 5), (129, 7), (130, 17), (257, 64), (700, 33), (1025, 3)])
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_kp_ragged_shapes(oracle, kernel, dtype, shape):
+    rng = np.random.default_rng(shape[0] * 31 + shape[1])
+    X = rng.uniform(-1, 1, size=shape).astype(dtype)
+    check_kp(oracle, X, kernel, dtype, seed=shape[0])
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_kp_linear_factored_mode(oracle, dtype):
+    X, _ = datagen.blobs(777, 45, seed=3, dtype=dtype)
+    check_kp(oracle, X, "linear", dtype, kp_mode="factored")
+
+
+def test_mfma_layout_asymmetric_integer_data(oracle):
+    """Exact small-integer data: any swapped MFMA row/col map breaks bitwise equality of the linear K·p."""
+    rng = np.random.default_rng(5)
+    for dtype in DTYPES:
+        X = rng.integers(-3, 4, size=(300, 24)).astype(dtype)
+        svm = make_svm(X, None, "linear", dtype)
+        svm.setup_data_on_device()
+        q = svm.generate_q()
+        x = rng.integers(1, 3, size=299).astype(dtype)
+        ret = np.zeros(299, dtype=dtype)
+        svm.run_device_kernel(None, ret, x, 1.0)
+        want = oracle.kp("linear", oracle.Data(X, dtype=dtype), q, svm.QA_cost, dtype(1), 1.0, x)
+        assert np.array_equal(ret, want), np.abs(ret - want).max()
+        svm.close()
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_kp_bitwise_reproducible(dtype):
+    X, _ = datagen.blobs(600, 40, seed=9, dtype=dtype)
+    svm = make_svm(X, None, "rbf", dtype)
+    svm.setup_data_on_device()
+    svm.generate_q()
+    x = np.linspace(1, 2, 599).astype(dtype)
+    a = svm.run_device_kernel(None, np.zeros(599, dtype), x, 1.0)
+    b = svm.run_device_kernel(None, np.zeros(599, dtype), x, 1.0)
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_learn_reproduces_golden_5x4_model(dtype):
+    X, y = pm.parse_libsvm(fixture_path("5x4.libsvm"), dtype=dtype)
+    model = pm.parse_model(fixture_path("5x4.libsvm.model"))
+    svm = make_svm(X, y, "linear", dtype)
+    svm.learn()
+    order = [int(np.argmin(np.abs(X - sv).sum(axis=1))) for sv in model["SV"]]
+    tol = 1e-9 if dtype == np.float64 else 2e-2
+    assert abs(svm.rho - model["rho"]) <= tol * abs(model["rho"])
+    np.testing.assert_allclose(svm.alpha[order], model["alpha"], rtol=tol, atol=tol * 1e-3)
+    assert svm.iters == 3
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_learn_matches_oracle_config1(oracle, kernel, dtype):
+    """Config 1: generate_data.py-style blobs 500x4 (seeded); full learn(), imax = d = 4."""
+    X, y = datagen.blobs(500, 4, seed=1, dtype=dtype)
+    svm = make_svm(X, y, kernel, dtype)
+    svm.learn()
+    ref = oracle.learn(kernel, oracle.Data(X, dtype=dtype), y, **oracle_args(svm))
+    assert svm.iters == ref["iters"]
+    if dtype == np.float64:
+        np.testing.assert_allclose(svm.trace, ref["trace"], rtol=1e-6)
+        np.testing.assert_allclose(svm.alpha, ref["alpha"], rtol=1e-9, atol=1e-9 * np.abs(ref["alpha"]).max())
+        assert abs(svm.rho - ref["rho"]) <= 1e-9 * max(1.0, abs(ref["rho"]))
+    else:
+        np.testing.assert_allclose(svm.trace[:3], ref["trace"][:3], rtol=1e-3)
+        np.testing.assert_allclose(svm.alpha, ref["alpha"], rtol=2e-2, atol=2e-2 * np.abs(ref["alpha"]).max())
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_cg_trace_across_explicit_residual(oracle, kernel):
+    """> 50 iterations (run % 50 == 49 recomputes r = b - Q~x, OpenMP/csvm.cpp:130-139): fp64 trace to 1e-6."""
+    X, y = datagen.blobs(400, 48, seed=5, cluster_std=4.0)
+    svm = make_svm(X, y, kernel, np.float64, cost=100.0)
+    svm.setup_data_on_device()
+    q = svm.generate_q()
+    b = (y[:-1] - y[-1]).astype(np.float64)
+    x = svm.solver_CG(b, 80, 1e-12, q)
+    ref_x, ref_trace, ref_it = oracle.solve_cg(kernel, oracle.Data(X), b, 80, 1e-12, q, svm.QA_cost, 100.0,
+                                               **oracle_args(svm))
+    assert svm.iters == ref_it
+    n = min(60, ref_it + 1)
+    np.testing.assert_allclose(svm.trace[:n], ref_trace[:n], rtol=1e-6)
+    np.testing.assert_allclose(x, ref_x, rtol=1e-6, atol=1e-6 * np.abs(ref_x).max())
+
+
+def test_state_errors():
+    X, _ = datagen.blobs(50, 3, seed=2)
+    svm = make_svm(X, None, "rbf", np.float64)
+    with pytest.raises(pm.BackendError):
+        svm.generate_q()
+    svm.setup_data_on_device()
+    with pytest.raises(pm.BackendError):
+        svm.run_device_kernel(None, np.zeros(49), np.ones(49), 1.0)
+
+
+def test_single_point_degenerate():
+    X = np.array([[0.5, -0.25]])
+    svm = make_svm(X, np.array([1.0]), "rbf", np.float64)
+    svm.learn()
+    assert svm.alpha.shape == (1,) and svm.alpha[0] == 0.0
