@@ -63,6 +63,10 @@ extern "C" {
 #define PLSSVM_MI_KP_FACTORED 2 /* linear kernel only: X (X^T p) + rank-1 terms, HBM-bound         */
 
 #define PLSSVM_MI_OPT_KP_MODE 1
+/* Test hook (single GPU): value = rank | (world << 16) makes this context compute only that rank's
+ * share of the implicit matrix with no collective; the rank-1 Q~ terms are added by rank 0 only,
+ * so the K·p results of all simulated ranks sum to the full K·p. */
+#define PLSSVM_MI_OPT_SIM_RANK 2
 
 typedef struct plssvm_mi_ctx plssvm_mi_ctx;
 
@@ -89,6 +93,11 @@ PLSSVM_MI_API int plssvm_mi_set_qa_cost(plssvm_mi_ctx *ctx, double qa_cost);
 #define PLSSVM_MI_UNIQUE_ID_BYTES 128
 PLSSVM_MI_API int plssvm_mi_get_unique_id(void *id_out);
 PLSSVM_MI_API int plssvm_mi_comm_init(plssvm_mi_ctx *ctx, int rank, int world_size, const void *unique_id);
+
+/* Host-only (no GPU needed): the work split of the implicit matrix for m = n - 1 rows.
+ * out4 = { first super-block, end super-block, total tiles, tiles owned by `rank` } where a tile
+ * is 128x128 of the lower triangle and a super-block 8x8 tiles (linear index I(I+1)/2 + J). */
+PLSSVM_MI_API int plssvm_mi_partition(int64_t m, int rank, int world_size, int64_t *out4);
 
 /* gpu_csvm::setup_data_on_device (src/plssvm/backends/gpu_csvm.cpp:130-157) for dense data:
  * X is row-major [n][d] host memory of the context's real type (all n points, the last one

@@ -23,7 +23,8 @@ from . import _abi
 from ._abi import BackendError, KERNELS
 from .io import parse_libsvm, parse_model
 
-__all__ = ["Parameter", "CSVM", "BackendError", "parse_libsvm", "parse_model", "device_count", "unique_id"]
+__all__ = ["Parameter", "CSVM", "BackendError", "parse_libsvm", "parse_model", "device_count", "unique_id",
+           "partition"]
 
 
 def device_count() -> int:
@@ -35,6 +36,14 @@ def unique_id() -> bytes:
     buf = ctypes.create_string_buffer(_abi.UNIQUE_ID_BYTES)
     _abi.check(_abi.lib().plssvm_mi_get_unique_id(buf))
     return buf.raw
+
+
+def partition(m, rank, world_size):
+    """Work split of the implicit matrix (host-only): (first super-block, end super-block,
+    total tiles, tiles owned by rank); see plssvm_mi_partition in include/plssvm_mi355x.h."""
+    out = (ctypes.c_int64 * 4)()
+    _abi.check(_abi.lib().plssvm_mi_partition(m, rank, world_size, out))
+    return tuple(out)
 
 
 def _ptr(a):
@@ -86,7 +95,8 @@ class Parameter:
 class CSVM:
     """One MI355X context (one GPU, one HIP stream). ``world_size > 1`` joins a row-block group."""
 
-    def __init__(self, params: Parameter, device=0, rank=0, world_size=1, uid=None, kp_mode="auto"):
+    def __init__(self, params: Parameter, device=0, rank=0, world_size=1, uid=None, kp_mode="auto",
+                 sim_rank=None):
         if params.data is None and params.csr is None:
             raise ValueError("No data points provided!")
         if params.data is not None:
@@ -106,6 +116,8 @@ class CSVM:
         mode = {"auto": _abi.KP_AUTO, "pairwise": _abi.KP_PAIRWISE, "factored": _abi.KP_FACTORED}[kp_mode]
         if mode != _abi.KP_AUTO:
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_KP_MODE, mode))
+        if sim_rank is not None:  # (rank, world): single-GPU test hook, see PLSSVM_MI_OPT_SIM_RANK
+            self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_SIM_RANK, sim_rank[0] | (sim_rank[1] << 16)))
         if world_size > 1:
             self._uid = ctypes.create_string_buffer(uid, _abi.UNIQUE_ID_BYTES)
             self._check(L.plssvm_mi_comm_init(self._ctx, rank, world_size, self._uid))

@@ -27,8 +27,9 @@ EXPORTS = (
     "plssvm_mi_set_option", "plssvm_mi_set_cost", "plssvm_mi_set_qa_cost", "plssvm_mi_get_unique_id",
     "plssvm_mi_comm_init", "plssvm_mi_setup_dense", "plssvm_mi_setup_csr", "plssvm_mi_generate_q", "plssvm_mi_kp",
     "plssvm_mi_solve_cg", "plssvm_mi_cg_begin", "plssvm_mi_cg_step", "plssvm_mi_cg_result", "plssvm_mi_learn",
-    "plssvm_mi_time_kp", "plssvm_mi_get_info",
+    "plssvm_mi_time_kp", "plssvm_mi_get_info", "plssvm_mi_partition",
 )
+OPT_SIM_RANK = 2
 
 
 class Info(ctypes.Structure):
@@ -86,6 +87,7 @@ def _declare(L):
         "plssvm_mi_learn": ([P, P, I64, D, P, PD, P, PI64], I),
         "plssvm_mi_time_kp": ([P, I, PD, PD], I),
         "plssvm_mi_get_info": ([P, ctypes.POINTER(Info)], I),
+        "plssvm_mi_partition": ([I64, I, I, PI64], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -93,10 +93,29 @@ const char *plssvm_mi_last_error(const plssvm_mi_ctx *ctx) {
 int plssvm_mi_set_option(plssvm_mi_ctx *ctx, int key, int64_t value) {
     if (!ctx) return PLSSVM_MI_ERR_ARG;
     return ctx->call([&](auto &e) {
-        if (key != PLSSVM_MI_OPT_KP_MODE || value < 0 || value > 2) throw mi_error(PLSSVM_MI_ERR_ARG, "bad option");
         if (e.have_data) throw mi_error(PLSSVM_MI_ERR_STATE, "set options before setup");
-        e.kp_mode = (int) value;
+        if (key == PLSSVM_MI_OPT_KP_MODE && value >= 0 && value <= 2) {
+            e.kp_mode = (int) value;
+        } else if (key == PLSSVM_MI_OPT_SIM_RANK && value >= 0) {
+            const int r = (int) (value & 0xFFFF), w = (int) (value >> 16);
+            if (w < 0 || (w > 0 && r >= w) || e.world > 1) throw mi_error(PLSSVM_MI_ERR_ARG, "bad simulated rank");
+            e.sim_rank = r;
+            e.sim_world = w;
+        } else {
+            throw mi_error(PLSSVM_MI_ERR_ARG, "bad option");
+        }
     });
+}
+
+int plssvm_mi_partition(int64_t m, int rank, int world_size, int64_t *out4) {
+    if (m < 0 || world_size < 1 || rank < 0 || rank >= world_size || !out4) return PLSSVM_MI_ERR_ARG;
+    int64_t s0, s1, st, tt, tl;
+    plssvm_mi::partition_superblocks(plssvm_mi::ceil_div(m, plssvm_mi::KP_TILE), rank, world_size, s0, s1, st, tt, tl);
+    out4[0] = s0;
+    out4[1] = s1;
+    out4[2] = tt;
+    out4[3] = tl;
+    return PLSSVM_MI_OK;
 }
 
 int plssvm_mi_set_cost(plssvm_mi_ctx *ctx, double cost) {
@@ -232,8 +251,8 @@ int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
         info->n_pad = e.n_pad;
         info->d_pad = e.d_pad;
         info->nnz = e.csr.nnz;
-        info->tiles_total = e.t_total;
-        info->tiles_local = e.t1 - e.t0;
+        info->tiles_total = e.tiles_total;
+        info->tiles_local = e.tiles_local;
         info->tile_rows = plssvm_mi::KP_TILE;
         info->tile_cols = plssvm_mi::KP_TILE;
         info->device_bytes = e.device_bytes();

@@ -89,170 +89,6 @@ __global__ __launch_bounds__(256) void q_dense_kernel(kfun<T> kf, const T *__res
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Pairwise tile kernel. 4 waves as 2x2; wave (wr, wc) owns the 64x64 sub-tile, i.e. 4x4 MFMA
-// 16x16 accumulators. K loop over BK-deep feature panels staged in LDS as [k][i] with a row
-// stride of 144 elements (conflict-free: k and k+1 rows land on opposite bank halves).
-template <typename T, int KERNEL>
-__global__ __launch_bounds__(256, 2) void kp_tile_kernel(kfun<T> kf, const T *__restrict__ XT,
-                                                      const T *__restrict__ norms, const T *__restrict__ p,
-                                                      T *__restrict__ partial, int64_t n_pad, int64_t d_pad,
-                                                      int64_t t0, int64_t ntiles,
-                                                      const cg_scalars<T> *__restrict__ status) {
-    using M = mfma16<T>;
-    using acc_t = typename M::acc_t;
-    constexpr int BK = kp_bk<T>();
-    constexpr int LDA = KP_TILE + 16;
-    constexpr int VEC = 16 / (int) sizeof(T);       // elements per 16-byte load
-    constexpr int VPR = KP_TILE / VEC;              // 16-byte vectors per panel row
-    constexpr int NV = BK * VPR / 256;              // vectors per thread per operand
-    using vec_t = typename std::conditional<sizeof(T) == 8, double2, float4>::type;
-
-    __shared__ __attribute__((aligned(16))) T As[BK * LDA];
-    __shared__ __attribute__((aligned(16))) T Bs[BK * LDA];
-    __shared__ T rowbuf[2][KP_TILE];
-    __shared__ T colbuf[2][KP_TILE];
-
-    if (status != nullptr && status->converged) return;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int w = tid >> 6;
-    const int wr = w >> 1, wc = w & 1;
-
-    int64_t I, J;
-    tri_tile(t0 + xcd_remap(blockIdx.x, ntiles), I, J);
-    const int64_t I0 = I * KP_TILE, J0 = J * KP_TILE;
-    const bool diag = (I == J);
-
-    acc_t acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = acc_t{ 0, 0, 0, 0 };
-
-    vec_t ra[NV], rb[NV];
-    auto load_panel = [&](int64_t k0) {
-#pragma unroll
-        for (int u = 0; u < NV; ++u) {
-            const int idx = tid + 256 * u;
-            const int row = idx / VPR, cv = idx % VPR;
-            const int64_t off = (k0 + row) * n_pad + cv * VEC;
-            ra[u] = *reinterpret_cast<const vec_t *>(XT + off + I0);
-            rb[u] = *reinterpret_cast<const vec_t *>(XT + off + J0);
-        }
-    };
-    auto store_panel = [&]() {
-#pragma unroll
-        for (int u = 0; u < NV; ++u) {
-            const int idx = tid + 256 * u;
-            const int row = idx / VPR, cv = idx % VPR;
-            *reinterpret_cast<vec_t *>(As + row * LDA + cv * VEC) = ra[u];
-            *reinterpret_cast<vec_t *>(Bs + row * LDA + cv * VEC) = rb[u];
-        }
-    };
-
-    const int64_t nk = d_pad / BK;
-    load_panel(0);
-    for (int64_t kc = 0; kc < nk; ++kc) {
-        __syncthreads();
-        store_panel();
-        __syncthreads();
-        if (kc + 1 < nk) load_panel((kc + 1) * BK);
-#pragma unroll
-        for (int ks = 0; ks < BK / 4; ++ks) {
-            const int kr = ks * 4 + (lane >> 4);
-            T a[4], b[4];
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) a[mt] = As[kr * LDA + wr * 64 + mt * 16 + (lane & 15)];
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) b[nt] = Bs[kr * LDA + wc * 64 + nt * 16 + (lane & 15)];
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-                for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = M::op(a[mt], b[nt], acc[mt][nt]);
-        }
-    }
-
-    // ---- epilogue: kernel function, times p, row and column sums ----
-    T pj[4], nj[4];
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-        const int64_t j = J0 + wc * 64 + nt * 16 + (lane & 15);
-        pj[nt] = p[j];
-        nj[nt] = (KERNEL == 2) ? norms[j] : T(0);
-    }
-    T cs[4] = { 0, 0, 0, 0 };
-    T rs[4][4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t i = I0 + wr * 64 + mt * 16 + M::row(lane, r);
-            const T pi = p[i];
-            const T ni = (KERNEL == 2) ? norms[i] : T(0);
-            T s = 0;
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                const T kv = kernel_apply<T>(KERNEL, kf.degree, kf.gamma, kf.coef0, acc[mt][nt][r], ni, nj[nt]);
-                s = fma(kv, pj[nt], s);
-                cs[nt] = fma(kv, pi, cs[nt]);
-            }
-            rs[mt][r] = s;
-        }
-    }
-    // rows: lanes sharing (lane >> 4) hold the same row -> reduce over lane & 15
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            T v = rs[mt][r];
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 4);
-            v += __shfl_xor(v, 8);
-            if ((lane & 15) == 0) rowbuf[wc][wr * 64 + mt * 16 + M::row(lane, r)] = v;
-        }
-    }
-    if (!diag) {
-        // columns: lanes sharing (lane & 15) hold the same column -> reduce over lane >> 4
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            T v = cs[nt];
-            v += __shfl_xor(v, 16);
-            v += __shfl_xor(v, 32);
-            if (lane < 16) colbuf[wr][wc * 64 + nt * 16 + lane] = v;
-        }
-    }
-    __syncthreads();
-    if (tid < KP_TILE) {
-        partial[J * n_pad + I0 + tid] = rowbuf[0][tid] + rowbuf[1][tid];
-    } else if (!diag) {
-        const int t = tid - KP_TILE;
-        partial[I * n_pad + J0 + t] = colbuf[0][t] + colbuf[1][t];
-    }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void kp_reduce_kernel(const T *__restrict__ partial, int64_t nb, int64_t n_pad,
-                                                        int64_t m, int64_t t0, int64_t t1, T *__restrict__ raw,
-                                                        const cg_scalars<T> *__restrict__ status) {
-    if (status != nullptr && status->converged) return;
-    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const int64_t R = i / KP_TILE;
-    T s = 0;
-    if (t0 == 0 && t1 == nb * (nb + 1) / 2) {
-        for (int64_t c = 0; c < nb; ++c) s += partial[c * n_pad + i];
-    } else {
-        for (int64_t c = 0; c < nb; ++c) {
-            const int64_t t = (R >= c) ? tri_index(R, c) : tri_index(c, R);
-            if (t >= t0 && t < t1) s += partial[c * n_pad + i];
-        }
-    }
-    raw[i] = s;
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void kp_finalize_kernel(const T *__restrict__ raw, const T *__restrict__ q,
                                                           const T *__restrict__ p, const cg_scalars<T> *sc,
@@ -263,8 +99,9 @@ __global__ __launch_bounds__(256) void kp_finalize_kernel(const T *__restrict__ 
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     const T sp = sc->sp, sqp = sc->sqp;
-    const T v = raw[i] + (QA_cost - q[i]) * sp - sqp + cost_inv * p[i];
-    ret[i] = (overwrite ? T(0) : ret[i]) + add * v;
+    // flags (overwrite): bit 0 = overwrite ret, bit 1 = raw share only (simulated rank != 0)
+    const T v = (overwrite & 2) ? raw[i] : raw[i] + (QA_cost - q[i]) * sp - sqp + cost_inv * p[i];
+    ret[i] = ((overwrite & 1) ? T(0) : ret[i]) + add * v;
 }
 
 // ---- factored linear: two coalesced passes over XT ----------------------------------------------
@@ -335,37 +172,6 @@ void launch_q_dense(kfun<T> kf, const T *XT, int64_t n_pad, int64_t d, int64_t m
 }
 
 template <typename T>
-void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *partial, int64_t n_pad, int64_t d_pad,
-                     int64_t t0, int64_t ntiles, const cg_scalars<T> *status, hipStream_t s) {
-    if (ntiles <= 0) return;
-    const dim3 grid((unsigned) ntiles), block(256);
-    switch (kf.kernel) {
-        case 0:
-            hipLaunchKernelGGL((kp_tile_kernel<T, 0>), grid, block, 0, s, kf, XT, norms, p, partial, n_pad, d_pad, t0,
-                               ntiles, status);
-            break;
-        case 1:
-            hipLaunchKernelGGL((kp_tile_kernel<T, 1>), grid, block, 0, s, kf, XT, norms, p, partial, n_pad, d_pad, t0,
-                               ntiles, status);
-            break;
-        default:
-            hipLaunchKernelGGL((kp_tile_kernel<T, 2>), grid, block, 0, s, kf, XT, norms, p, partial, n_pad, d_pad, t0,
-                               ntiles, status);
-            break;
-    }
-    MI_LAUNCH_CHECK();
-}
-
-template <typename T>
-void launch_kp_reduce(const T *partial, int64_t nb, int64_t n_pad, int64_t m, int64_t t0, int64_t t1, T *raw,
-                      const cg_scalars<T> *status, hipStream_t s) {
-    if (m <= 0) return;
-    hipLaunchKernelGGL(kp_reduce_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, partial, nb, n_pad, m,
-                       t0, t1, raw, status);
-    MI_LAUNCH_CHECK();
-}
-
-template <typename T>
 void launch_kp_finalize(const T *raw, const T *q, const T *p, const cg_scalars<T> *sc, T QA_cost, T cost_inv, T add,
                         int overwrite, int64_t m, T *ret, const cg_scalars<T> *status, hipStream_t s) {
     if (m <= 0) return;
@@ -395,10 +201,6 @@ void launch_gemv_n(const T *XT, int64_t n_pad, int64_t d, int64_t r0, int64_t r1
     template void launch_transpose<T>(const T *, int64_t, int64_t, T *, int64_t, hipStream_t);                   \
     template void launch_row_norms<T>(const T *, int64_t, int64_t, T *, hipStream_t);                            \
     template void launch_q_dense<T>(kfun<T>, const T *, int64_t, int64_t, int64_t, const T *, T *, hipStream_t); \
-    template void launch_kp_tiles<T>(kfun<T>, const T *, const T *, const T *, T *, int64_t, int64_t, int64_t,   \
-                                     int64_t, const cg_scalars<T> *, hipStream_t);                               \
-    template void launch_kp_reduce<T>(const T *, int64_t, int64_t, int64_t, int64_t, int64_t, T *,               \
-                                      const cg_scalars<T> *, hipStream_t);                                       \
     template void launch_kp_finalize<T>(const T *, const T *, const T *, const cg_scalars<T> *, T, T, T, int,    \
                                         int64_t, T *, const cg_scalars<T> *, hipStream_t);                       \
     template void launch_gemv_t<T>(const T *, int64_t, int64_t, int64_t, int64_t, const T *, T *,                \

@@ -44,6 +44,35 @@ T host_kernel(int kernel, int degree, T gamma, T coef0, const T *a, const T *b, 
 
 }  // namespace
 
+// Balanced contiguous ranges of 8x8-tile super-blocks of the lower triangle (each holds 64 tiles,
+// diagonal ones 36, edge ones fewer): rank r gets the super-blocks whose cumulative tile count
+// crosses [r, r+1) * total / world. Host-only (plssvm_mi_partition exposes it for CPU tests).
+void partition_superblocks(int64_t nb, int rank, int world, int64_t &s0, int64_t &s1, int64_t &s_total,
+                           int64_t &tiles_total, int64_t &tiles_local) {
+    const int64_t ns = ceil_div(nb, KP_SUPER);
+    s_total = ns * (ns + 1) / 2;
+    tiles_total = nb * (nb + 1) / 2;
+    std::vector<int64_t> cum(s_total + 1, 0);  // tiles before super-block s
+    for (int64_t s = 0; s < s_total; ++s) {
+        int64_t SI, SJ;
+        tri_tile(s, SI, SJ);
+        const int64_t rows = std::min<int64_t>(KP_SUPER, nb - SI * KP_SUPER);
+        int64_t cnt = 0;
+        for (int64_t a = 0; a < rows; ++a) {
+            const int64_t I = SI * KP_SUPER + a;
+            cnt += std::max<int64_t>(0, std::min<int64_t>(KP_SUPER, I - SJ * KP_SUPER + 1));
+        }
+        cum[s + 1] = cum[s] + cnt;
+    }
+    auto split = [&](int r) {
+        return (int64_t) (std::lower_bound(cum.begin(), cum.end(), (tiles_total * r) / world) - cum.begin());
+    };
+    s0 = rank == 0 ? 0 : split(rank);
+    s1 = rank == world - 1 ? s_total : split(rank + 1);
+    if (s1 < s0) s1 = s0;
+    tiles_local = cum[s1] - cum[s0];
+}
+
 template <typename T>
 engine<T>::engine(int kernel_, int degree_, double gamma_, double coef0_, double cost_, int device_) :
     kernel(kernel_), degree(degree_), gamma((T) gamma_), coef0((T) coef0_), cost((T) cost_), device(device_) {
@@ -150,13 +179,13 @@ void engine<T>::setup_csr(const int64_t *, const int32_t *, const void *, int, i
 template <typename T>
 void engine<T>::finish_setup() {
     // work split of the implicit matrix over the group (replaces feature_ranges_, gpu_csvm.cpp:136-139)
-    t_total = nb * (nb + 1) / 2;
-    t0 = (t_total * rank) / world;
-    t1 = (t_total * (rank + 1)) / world;
-    chunk = ceil_div(std::max<int64_t>(m, 1), world);
-    r0 = std::min<int64_t>(m, rank * chunk);
+    partition_superblocks(nb, sim_world > 0 ? sim_rank : rank, sim_world > 0 ? sim_world : world, t0, t1, t_total,
+                          tiles_total, tiles_local);
+    const int eff_world = sim_world > 0 ? sim_world : world, eff_rank = sim_world > 0 ? sim_rank : rank;
+    chunk = ceil_div(std::max<int64_t>(m, 1), eff_world);
+    r0 = std::min<int64_t>(m, eff_rank * chunk);
     r1 = std::min<int64_t>(m, r0 + chunk);
-    const int64_t vec_len = std::max<int64_t>(n_pad, chunk * world);
+    const int64_t vec_len = std::max<int64_t>(n_pad, chunk * eff_world);
     if (!sparse && !factored()) {
         partial.alloc(std::max<int64_t>(nb, 1) * n_pad, stream, false);
     } else {
@@ -220,17 +249,18 @@ void engine<T>::kp_device(const T *p, T *out, T add, bool overwrite, const cg_sc
     if (sparse) {
         sparse_kp_raw(p, status);
     } else if (factored()) {
-        launch_gemv_t<T>(XT.get(), n_pad, d, r0, r1, p, w.get(), status, stream);
+        launch_gemv_t<T>(XT.get(), n_pad, d, sim_world > 0 ? 0 : r0, sim_world > 0 ? m : r1, p, w.get(), status, stream);
         allreduce(w.get(), d);
         launch_gemv_n<T>(XT.get(), n_pad, d, r0, r1, w.get(), raw.get(), status, stream);
         allgather_rows(raw.get());
     } else {
-        launch_kp_tiles<T>(kf(), XT.get(), norms.get(), p, partial.get(), n_pad, d_pad, t0, t1 - t0, status, stream);
+        launch_kp_tiles<T>(kf(), XT.get(), norms.get(), p, partial.get(), n_pad, d_pad, nb, t0, t1 - t0, status,
+                           stream);
         launch_kp_reduce<T>(partial.get(), nb, n_pad, m, t0, t1, raw.get(), status, stream);
         allreduce(raw.get(), m);
     }
-    launch_kp_finalize<T>(raw.get(), q.get(), p, scp, QA_cost, cost_inv(), add, overwrite ? 1 : 0, m, out, status,
-                          stream);
+    const int flags = (overwrite ? 1 : 0) | ((sim_world > 0 && sim_rank != 0) ? 2 : 0);
+    launch_kp_finalize<T>(raw.get(), q.get(), p, scp, QA_cost, cost_inv(), add, flags, m, out, status, stream);
 }
 
 template <typename T>
@@ -391,7 +421,7 @@ void engine<T>::time_kp(int reps, double *ms_kp, double *ms_dom) {
         } else if (factored()) {
             launch_gemv_n<T>(XT.get(), n_pad, d, r0, r1, w.get(), raw.get(), nullptr, stream);
         } else {
-            launch_kp_tiles<T>(kf(), XT.get(), norms.get(), pv.get(), partial.get(), n_pad, d_pad, t0, t1 - t0,
+            launch_kp_tiles<T>(kf(), XT.get(), norms.get(), pv.get(), partial.get(), n_pad, d_pad, nb, t0, t1 - t0,
                                nullptr, stream);
         }
         MI_HIP_CHECK(hipEventRecord(d1, stream));

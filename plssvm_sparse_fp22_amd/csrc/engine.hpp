@@ -54,6 +54,9 @@ class dev_buf {
     int64_t n_ = 0;
 };
 
+void partition_superblocks(int64_t nb, int rank, int world, int64_t &s0, int64_t &s1, int64_t &s_total,
+                           int64_t &tiles_total, int64_t &tiles_local);
+
 struct engine_base {
     virtual ~engine_base() = default;
 };
@@ -70,6 +73,9 @@ struct engine : engine_base {
     // ---- multi-GPU row-block group ----
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
+    // test hook: compute only rank sim_rank's share of a sim_world group, no collective, rank-1
+    // terms only on sim rank 0 (so the shares of all sim ranks sum to the full K·p)
+    int sim_rank = 0, sim_world = 0;
 
     // ---- data ----
     bool have_data = false, sparse = false;
@@ -79,7 +85,8 @@ struct engine : engine_base {
     csr_data<T> csr;              // sparse
 
     // work split
-    int64_t t_total = 0, t0 = 0, t1 = 0;  // pairwise tiles owned by this rank
+    int64_t t_total = 0, t0 = 0, t1 = 0;  // pairwise tile super-blocks owned by this rank: [t0, t1) of t_total
+    int64_t tiles_total = 0, tiles_local = 0;
     int64_t r0 = 0, r1 = 0, chunk = 0;    // rows owned by this rank (factored / sparse row paths)
 
     // ---- vectors (n_pad, zero padded) ----

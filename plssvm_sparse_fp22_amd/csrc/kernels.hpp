@@ -42,14 +42,18 @@ template <typename T>
 void launch_q_dense(kfun<T> kf, const T *XT, int64_t n_pad, int64_t d, int64_t m, const T *xlast, T *q,
                     hipStream_t s);
 
-// partial[c][i]: sum_j in col-block c of k(x_i,x_j) p_j for the lower-triangle tiles [t0, t0+ntiles)
+// Tiles are scheduled in KP_SUPER x KP_SUPER super-blocks of the lower triangle (super-block
+// (SI, SJ), SI >= SJ, linear index tri_index(SI, SJ)); a rank owns a contiguous super-block range.
+constexpr int KP_SUPER = 8;
+
+// partial[c][i]: sum_{j in col-block c} k(x_i,x_j) p_j for the tiles of super-blocks [s0, s0+nsuper)
 template <typename T>
 void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *partial, int64_t n_pad, int64_t d_pad,
-                     int64_t t0, int64_t ntiles, const cg_scalars<T> *status, hipStream_t s);
+                     int64_t nb, int64_t s0, int64_t nsuper, const cg_scalars<T> *status, hipStream_t s);
 
-// raw[i] = sum_c partial[c][i] over tiles owned by this rank ([t0, t1)); i < m
+// raw[i] = sum_c partial[c][i] over the tiles whose super-block lies in [s0, s1); i < m
 template <typename T>
-void launch_kp_reduce(const T *partial, int64_t nb, int64_t n_pad, int64_t m, int64_t t0, int64_t t1, T *raw,
+void launch_kp_reduce(const T *partial, int64_t nb, int64_t n_pad, int64_t m, int64_t s0, int64_t s1, T *raw,
                       const cg_scalars<T> *status, hipStream_t s);
 
 // ret[i] = (overwrite ? 0 : ret[i]) + add * (raw[i] + (QA - q_i) * sum(p) - sum(q p) + p_i / C)

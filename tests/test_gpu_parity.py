@@ -133,21 +133,70 @@ def test_learn_matches_oracle_config1(oracle, kernel, dtype):
         np.testing.assert_allclose(svm.alpha, ref["alpha"], rtol=2e-2, atol=2e-2 * np.abs(ref["alpha"]).max())
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
-def test_cg_trace_across_explicit_residual(oracle, kernel):
-    """> 50 iterations (run % 50 == 49 recomputes r = b - Q~x, OpenMP/csvm.cpp:130-139): fp64 trace to 1e-6."""
-    X, y = datagen.blobs(400, 48, seed=5, cluster_std=4.0)
-    svm = make_svm(X, y, kernel, np.float64, cost=100.0)
+def test_learn_config2_scaled_down(oracle):
+    """Config 2 shape (dense RBF, d = 256, fp64, C = 1, eps = 1e-3) at N = 3000: residual curve to 1e-6."""
+    X, y = datagen.blobs(3000, 256, seed=2, cluster_std=4.0)
+    svm = make_svm(X, y, "rbf", np.float64)
+    svm.learn()
+    ref = oracle.learn("rbf", oracle.Data(X), y, gamma=1.0 / 256)
+    assert svm.iters == ref["iters"]
+    np.testing.assert_allclose(svm.trace, ref["trace"], rtol=1e-6)
+    np.testing.assert_allclose(svm.alpha, ref["alpha"], rtol=1e-9, atol=1e-9 * np.abs(ref["alpha"]).max())
+
+
+@pytest.mark.parametrize("kernel,cost,std",[("linear", 1e4, 4.0), ("polynomial", 1e4, 1.0), ("rbf", 100.0, 1.0)])
+def test_cg_trace_across_explicit_residual(oracle, kernel, cost, std):
+    """> 50 iterations (run % 50 == 49 recomputes r = b - Q~x, OpenMP/csvm.cpp:130-139).
+
+    These systems are ill-conditioned (C >= 100), so rounding differences grow along the CG
+    recurrence: the reference OpenMP kernel itself (atomics) gives traces that differ by > 1e-6
+    between 1 and 8 threads after a few iterations. The bar is therefore 1e-6 on the first
+    iterations where OpenMP itself is reproducible (its 1-vs-8-thread deviation < 1e-9); after
+    that, the same iteration count (+-2) and the same converged solution."""
+    X, y = datagen.blobs(300, 64, seed=5, cluster_std=std)
+    svm = make_svm(X, y, kernel, np.float64, cost=cost)
     svm.setup_data_on_device()
     q = svm.generate_q()
     b = (y[:-1] - y[-1]).astype(np.float64)
-    x = svm.solver_CG(b, 80, 1e-12, q)
-    ref_x, ref_trace, ref_it = oracle.solve_cg(kernel, oracle.Data(X), b, 80, 1e-12, q, svm.QA_cost, 100.0,
-                                               **oracle_args(svm))
-    assert svm.iters == ref_it
-    n = min(60, ref_it + 1)
-    np.testing.assert_allclose(svm.trace[:n], ref_trace[:n], rtol=1e-6)
-    np.testing.assert_allclose(x, ref_x, rtol=1e-6, atol=1e-6 * np.abs(ref_x).max())
+    x = svm.solver_CG(b, 150, 1e-10, q)
+    args = dict(degree=3, gamma=1.0 / 64, coef0=0.0)
+    data = oracle.Data(X)
+    ref_x, ref_t, ref_it = oracle.solve_cg(kernel, data, b, 150, 1e-10, q, svm.QA_cost, cost, nthreads=1, **args)
+    _, ref_t8, _ = oracle.solve_cg(kernel, data, b, 150, 1e-10, q, svm.QA_cost, cost, nthreads=8, **args)
+    assert ref_it > 50, "test must cross the explicit-residual iteration"
+    assert abs(svm.iters - ref_it) <= 2
+    n = min(len(svm.trace), len(ref_t), len(ref_t8))
+    self_noise = np.maximum.accumulate(np.abs(ref_t8[:n] / ref_t[:n] - 1))
+    dev = np.abs(svm.trace[:n] / ref_t[:n] - 1)
+    reproducible = self_noise < 1e-9
+    assert reproducible[:3].all()
+    assert np.all(dev[reproducible] <= 1e-6), (dev, self_noise)
+    # both converged (delta <= eps^2 delta0): solutions agree to the conditioning of the system
+    np.testing.assert_allclose(x, ref_x, rtol=1e-3, atol=1e-3 * np.abs(ref_x).max())
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("kernel,mode", [("rbf", "auto"), ("polynomial", "auto"), ("linear", "factored")])
+def test_simulated_ranks_sum_to_full_kp(oracle, world, kernel, mode):
+    """The multi-GPU work split on one GPU: each simulated rank computes only its super-blocks
+    (pairwise) or rows (factored); the shares sum to the single-rank K·p (the RCCL all-reduce)."""
+    X, _ = datagen.blobs(2600, 24, seed=4)
+    m = X.shape[0] - 1
+    x = np.linspace(1, 2, m)
+    full = make_svm(X, None, kernel, np.float64, kp_mode=mode)
+    full.setup_data_on_device()
+    q = full.generate_q()
+    want = full.run_device_kernel(None, np.zeros(m), x, 1.0)
+    total = np.zeros(m)
+    for r in range(world):
+        p = pm.Parameter(kernel, gamma=1.0 / 24)
+        p.data = X
+        svm = pm.CSVM(p, kp_mode=mode, sim_rank=(r, world))
+        svm.setup_data_on_device()
+        svm.generate_q()
+        total += svm.run_device_kernel(None, np.zeros(m), x, 1.0)
+        svm.close()
+    np.testing.assert_allclose(total, want, rtol=1e-12, atol=1e-12 * np.abs(want).max())
 
 
 def test_state_errors():
