@@ -172,11 +172,6 @@ void engine<T>::setup_dense(const T *X, int64_t n_, int64_t d_) {
 }
 
 template <typename T>
-void engine<T>::setup_csr(const int64_t *, const int32_t *, const void *, int, int64_t, int64_t) {
-    throw mi_error(-5, "sparse setup not built yet");
-}
-
-template <typename T>
 void engine<T>::finish_setup() {
     // work split of the implicit matrix over the group (replaces feature_ranges_, gpu_csvm.cpp:136-139)
     partition_superblocks(nb, sim_world > 0 ? sim_rank : rank, sim_world > 0 ? sim_world : world, t0, t1, t_total,
@@ -212,7 +207,7 @@ void engine<T>::generate_q(T *q_out, double *qa_out) {
     need_data();
     MI_HIP_CHECK(hipSetDevice(device));
     if (sparse) {
-        launch_q_sparse<T>(kf(), csr, m, xlast.get(), q.get(), stream);
+        sparse_q();
     } else {
         launch_q_dense<T>(kf(), XT.get(), n_pad, d, m, xlast.get(), q.get(), stream);
     }
@@ -417,7 +412,7 @@ void engine<T>::time_kp(int reps, double *ms_kp, double *ms_dom) {
     for (int it = 0; it < reps; ++it) {
         MI_HIP_CHECK(hipEventRecord(d0, stream));
         if (sparse) {
-            sparse_dominant(pv.get());
+            sparse_dominant(pv.get(), nullptr);
         } else if (factored()) {
             launch_gemv_n<T>(XT.get(), n_pad, d, r0, r1, w.get(), raw.get(), nullptr, stream);
         } else {

@@ -8,51 +8,11 @@
 #include <string>
 #include <vector>
 
+#include "buffer.hpp"
 #include "kernels.hpp"
 #include "sparse.hpp"
 
 namespace plssvm_mi {
-
-// RAII device buffer (the reference's move-only device_ptr, src/plssvm/backends/gpu_device_ptr.cpp:58-109,
-// without its per-call hipSetDevice/synchronous copies: all traffic is async on the engine stream)
-template <typename T>
-class dev_buf {
-  public:
-    dev_buf() = default;
-    dev_buf(const dev_buf &) = delete;
-    dev_buf &operator=(const dev_buf &) = delete;
-    dev_buf(dev_buf &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr, o.n_ = 0; }
-    dev_buf &operator=(dev_buf &&o) noexcept {
-        if (this != &o) {
-            reset();
-            p_ = o.p_;
-            n_ = o.n_;
-            o.p_ = nullptr;
-            o.n_ = 0;
-        }
-        return *this;
-    }
-    ~dev_buf() { reset(); }
-    void alloc(int64_t n, hipStream_t s, bool zero = true) {
-        reset();
-        if (n <= 0) return;
-        MI_HIP_CHECK(hipMalloc(&p_, sizeof(T) * (size_t) n));
-        n_ = n;
-        if (zero) MI_HIP_CHECK(hipMemsetAsync(p_, 0, sizeof(T) * (size_t) n, s));
-    }
-    void reset() {
-        if (p_) (void) hipFree(p_);
-        p_ = nullptr;
-        n_ = 0;
-    }
-    T *get() const { return p_; }
-    int64_t size() const { return n_; }
-    int64_t bytes() const { return n_ * (int64_t) sizeof(T); }
-
-  private:
-    T *p_ = nullptr;
-    int64_t n_ = 0;
-};
 
 void partition_superblocks(int64_t nb, int rank, int world, int64_t &s0, int64_t &s1, int64_t &s_total,
                            int64_t &tiles_total, int64_t &tiles_local);
@@ -127,9 +87,11 @@ struct engine : engine_base {
     void time_kp(int reps, double *ms_kp, double *ms_dom);
 
     // sparse paths (sparse.hip)
+    void sparse_q();                                              // q, norms, e on CSR data
+    void build_gram_blocks(const int64_t *cpos, int64_t max_inc);  // sparse Gram pattern (pairwise kernels)
     void sparse_kp_raw(const T *p, const cg_scalars<T> *status);  // raw[i] = sum_j k_ij p_j, i < m
-    void sparse_dominant(const T *p);                             // the dominant sparse kernel alone (timing)
-    int64_t csr_bytes() const;
+    void sparse_dominant(const T *p, const cg_scalars<T> *status);  // the dominant sparse kernel
+    int64_t csr_bytes() const { return csr.bytes(); }
 
     void allreduce(T *buf, int64_t count);
     void allgather_rows(T *buf);

@@ -1,35 +1,646 @@
-// Sparse (CSR / CSC / packed FP22) K·p paths — see sparse.hpp.
+// Sparse (CSR / CSC / packed-FP22) data paths: setup, q, norms, factored linear K·p and the
+// sparse-Gram-pattern K·p for the polynomial and RBF kernels. See DESIGN.md §4.
+//
+// Math (exact identities, m = n - 1, i, j < m):
+//   linear (factored):  sum_j k_ij p_j = x_i . (X_m^T p)                       -> two SpMVs, HBM bound
+//   rbf:  k_ij = exp(-g (n_i + n_j - 2 s_ij)),  s_ij = x_i . x_j,  e_i = exp(-g n_i)
+//         pairs with no shared feature have s_ij = 0 and k_ij = e_i e_j, so
+//         sum_j k_ij p_j = e_i sum_j e_j p_j + (1 - e_i^2) p_i + sum_{j in ov(i)} (k_ij - e_i e_j) p_j
+//   poly: k_ij = (g s_ij + c0)^deg, kappa = c0^deg:
+//         sum_j k_ij p_j = kappa sum_j p_j + (k_ii - kappa) p_i + sum_{j in ov(i)} (k_ij - kappa) p_j
+// where ov(i) = { j != i : rows i and j share a feature }. The pattern ov (lower triangle, j < i)
+// with s_ij is built once at setup (sort + reduce-by-key of the column-join incidences); every K·p
+// re-evaluates the kernel function on each stored pair (the kernel matrix is never stored).
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+
+#include "../../include/plssvm_mi355x.h"
 #include "engine.hpp"
 
 namespace plssvm_mi {
 
+namespace {
+
+// ---- norms / e / q ----------------------------------------------------------------------------------
+// 16 lanes per row, 16 rows per 256-thread block
 template <typename T>
-void launch_q_sparse(kfun<T>, const csr_data<T> &, int64_t, const T *, T *, hipStream_t) {
-    throw mi_error(-5, "sparse q not built yet");
+__global__ __launch_bounds__(256) void csr_norms_kernel(const int64_t *__restrict__ rowptr, vals_t<T> val, int64_t m,
+                                                        T gamma, T *__restrict__ norms, T *__restrict__ e) {
+    const int64_t row = (int64_t) blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int sl = threadIdx.x & 15;
+    if (row >= m) return;
+    // sequential fma chain in column order (== the dense chain: zeros add nothing) — lane 0 walks the row
+    if (sl == 0) {
+        T v = 0;
+        for (int64_t k = rowptr[row]; k < rowptr[row + 1]; ++k) {
+            const T x = val[k];
+            v = fma(x, x, v);
+        }
+        norms[row] = v;
+        if (e) e[row] = exp(-gamma * v);
+    }
+}
+
+// q_i = k(x_i, x_last) with x_last dense; dot/dist via the row's non-zeros
+template <typename T>
+__global__ __launch_bounds__(256) void csr_q_kernel(kfun<T> kf, const int64_t *__restrict__ rowptr,
+                                                    const int32_t *__restrict__ col, vals_t<T> val, int64_t m,
+                                                    const T *__restrict__ xlast, T nlast, const T *__restrict__ norms,
+                                                    T *__restrict__ q) {
+    const int64_t row = (int64_t) blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int sl = threadIdx.x & 15;
+    if (row >= m) return;
+    T dot = 0;
+    if (sl == 0) {
+        for (int64_t k = rowptr[row]; k < rowptr[row + 1]; ++k) dot = fma(val[k], xlast[col[k]], dot);
+        T out;
+        if (kf.kernel == 0) {
+            out = dot;
+        } else if (kf.kernel == 1) {
+            const T base = fma(kf.gamma, dot, kf.coef0);
+            out = T(1);
+            for (int e = 0; e < kf.degree; ++e) out *= base;
+        } else {
+            T dist = norms[row] + nlast - T(2) * dot;
+            dist = dist > T(0) ? dist : T(0);
+            out = exp(-kf.gamma * dist);
+        }
+        q[row] = out;
+    }
+}
+
+// ---- factored linear ---------------------------------------------------------------------------------
+// w[f] = sum_{i in rows of this rank} x_if p_i : one wave per column (CSC)
+template <typename T>
+__global__ __launch_bounds__(256) void csc_gemv_kernel(const int64_t *__restrict__ lo, const int64_t *__restrict__ hi,
+                                                       const int32_t *__restrict__ crow, vals_t<T> cval, int64_t d,
+                                                       const T *__restrict__ p, T *__restrict__ w,
+                                                       const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    const int64_t f = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (f >= d) return;
+    T s = 0;
+    const int64_t b = hi[f];
+    for (int64_t k = lo[f] + lane; k < b; k += 64) s = fma(cval[k], p[crow[k]], s);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) w[f] = s;
+}
+
+// raw[i] = sum_f x_if w_f for r0 <= i < r1 : 16 lanes per row
+template <typename T>
+__global__ __launch_bounds__(256) void csr_gemv_kernel(const int64_t *__restrict__ rowptr,
+                                                       const int32_t *__restrict__ col, vals_t<T> val, int64_t r0,
+                                                       int64_t r1, const T *__restrict__ w, T *__restrict__ raw,
+                                                       const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    const int64_t row = r0 + (int64_t) blockIdx.x * 16 + (threadIdx.x >> 4);
+    const int sl = threadIdx.x & 15;
+    T s = 0;
+    if (row < r1) {
+        const int64_t b = rowptr[row + 1];
+        for (int64_t k = rowptr[row] + sl; k < b; k += 16) s = fma(val[k], w[col[k]], s);
+    }
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 4);
+    s += __shfl_xor(s, 8);
+    if (row < r1 && sl == 0) raw[row] = s;
+}
+
+// ---- Gram pattern build ---------------------------------------------------------------------------------
+// incidences of row i: sum over its entries e of #{ j < i in column col[e] } = cpos[e] - colptr[col[e]]
+__global__ __launch_bounds__(256) void gram_count_kernel(const int64_t *__restrict__ rowptr,
+                                                         const int32_t *__restrict__ col,
+                                                         const int64_t *__restrict__ cpos,
+                                                         const int64_t *__restrict__ colptr, int64_t i0, int64_t i1,
+                                                         int64_t *__restrict__ cnt) {
+    const int64_t i = i0 + (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= i1) return;
+    int64_t c = 0;
+    for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) c += cpos[k] - colptr[col[k]];
+    cnt[i - i0] = c;
+}
+
+// one workgroup per row: key = (W << 32) | (i_local << 16) | (j - W*CW), val = x_if x_jf
+template <typename T>
+__global__ __launch_bounds__(256) void gram_gen_kernel(const int64_t *__restrict__ rowptr,
+                                                       const int32_t *__restrict__ col, vals_t<T> val,
+                                                       const int64_t *__restrict__ cpos,
+                                                       const int64_t *__restrict__ colptr,
+                                                       const int32_t *__restrict__ crow, vals_t<T> cval, int64_t i0,
+                                                       const int64_t *__restrict__ off, uint64_t *__restrict__ keys,
+                                                       T *__restrict__ vals) {
+    const int64_t i = i0 + blockIdx.x;
+    const uint64_t il = (uint64_t) blockIdx.x;
+    int64_t out = off[blockIdx.x];
+    for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        const int64_t c0 = colptr[col[k]], c1 = cpos[k];
+        const T xi = val[k];
+        for (int64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
+            const uint64_t j = (uint64_t) crow[t];
+            keys[out + (t - c0)] = ((j / GRAM_CW) << 32) | (il << 16) | (j % GRAM_CW);
+            vals[out + (t - c0)] = xi * cval[t];
+        }
+        out += c1 - c0;
+    }
+}
+
+__global__ __launch_bounds__(256) void gram_rowcount_kernel(const uint64_t *__restrict__ ukeys,
+                                                            const int64_t *__restrict__ nruns,
+                                                            int32_t *__restrict__ rowcnt) {
+    const int64_t u = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= *nruns) return;
+    const uint64_t k = ukeys[u];
+    atomicAdd(&rowcnt[(k >> 32) * GRAM_RB + ((k >> 16) & 0xFFFF)], 1);
 }
 
 template <typename T>
-void engine<T>::sparse_kp_raw(const T *, const cg_scalars<T> *) {
-    throw mi_error(-5, "sparse K·p not built yet");
+__global__ __launch_bounds__(256) void gram_store_kernel(const uint64_t *__restrict__ ukeys,
+                                                         const T *__restrict__ usum, const int64_t *__restrict__ nruns,
+                                                         uint16_t *__restrict__ pj, T *__restrict__ ps) {
+    const int64_t u = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= *nruns) return;
+    pj[u] = (uint16_t) (ukeys[u] & 0xFFFF);
+    ps[u] = usum[u];
+}
+
+// ---- Gram K·p ---------------------------------------------------------------------------------------------
+template <typename T, int KERNEL>
+__global__ __launch_bounds__(512) void gram_kp_kernel(const gram_cell *__restrict__ cells,
+                                                      const int64_t *__restrict__ rb_base,
+                                                      const int32_t *__restrict__ rowoff,
+                                                      const uint16_t *__restrict__ pj, const T *__restrict__ ps,
+                                                      const T *__restrict__ norms, const T *__restrict__ ev,
+                                                      const T *__restrict__ p, T *__restrict__ slab_row,
+                                                      T *__restrict__ slab_col, int64_t m, int64_t m_pad, kfun<T> kf,
+                                                      T kappa, const cg_scalars<T> *__restrict__ status) {
+    __shared__ T colacc[GRAM_CW];
+    if (status != nullptr && status->converged) return;
+    const gram_cell cell = cells[xcd_remap(blockIdx.x, gridDim.x)];
+    for (int t = threadIdx.x; t < GRAM_CW; t += 512) colacc[t] = T(0);
+    __syncthreads();
+    const int64_t I0 = (int64_t) cell.I * GRAM_RB, W0 = (int64_t) cell.W * GRAM_CW;
+    const int rows = (int) min<int64_t>(GRAM_RB, m - I0);
+    const int64_t base = rb_base[cell.I];
+    const int32_t *ro = rowoff + cell.rowoff;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int il = wave; il < rows; il += 8) {
+        const int64_t i = I0 + il;
+        const int64_t a = base + ro[il], b = base + ro[il + 1];
+        const T pi = p[i];
+        const T ni = norms[i];
+        const T ei = (KERNEL == 2) ? ev[i] : T(0);
+        T acc = 0;
+        for (int64_t e = a + lane; e < b; e += 64) {
+            const int jl = pj[e];
+            const T s = ps[e];
+            const int64_t j = W0 + jl;
+            T c;
+            if (KERNEL == 2) {
+                T dist = ni + norms[j] - T(2) * s;
+                dist = dist > T(0) ? dist : T(0);
+                c = exp(-kf.gamma * dist) - ei * ev[j];
+            } else if (KERNEL == 1) {
+                const T bse = fma(kf.gamma, s, kf.coef0);
+                T kv = T(1);
+                for (int q = 0; q < kf.degree; ++q) kv *= bse;
+                c = kv - kappa;
+            } else {
+                c = s;
+            }
+            acc = fma(c, p[j], acc);
+            atomicAdd(&colacc[jl], c * pi);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == 0) slab_row[(int64_t) cell.W * m_pad + i] = acc;
+    }
+    __syncthreads();
+    const int wlen = (int) min<int64_t>(GRAM_CW, m - W0);
+    for (int t = threadIdx.x; t < wlen; t += 512) slab_col[(int64_t) cell.I * m_pad + W0 + t] = colacc[t];
+}
+
+__host__ __device__ inline int64_t gram_nw(int64_t I, int64_t m) {
+    const int64_t hi = m < (I + 1) * GRAM_RB ? m : (I + 1) * GRAM_RB;  // rows of block I are < hi, so j < hi
+    return (hi + GRAM_CW - 1) / GRAM_CW;
 }
 
 template <typename T>
-void engine<T>::sparse_dominant(const T *) {
-    throw mi_error(-5, "sparse K·p not built yet");
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const T *__restrict__ slab_row,
+                                                          const T *__restrict__ slab_col, int64_t m, int64_t m_pad,
+                                                          int64_t rb0, int64_t rb1, T *__restrict__ raw,
+                                                          const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int64_t I = i / GRAM_RB, W = i / GRAM_CW;
+    T s = 0;
+    if (I >= rb0 && I < rb1) {
+        const int64_t nw = gram_nw(I, m);
+        for (int64_t w = 0; w < nw; ++w) s += slab_row[w * m_pad + i];
+    }
+    for (int64_t J = max<int64_t>(rb0, I); J < rb1; ++J) {  // blocks with rows > i may pair with j = i
+        if (W < gram_nw(J, m)) s += slab_col[J * m_pad + i];
+    }
+    raw[i] = s;
+}
+
+// raw_i += separable part + diagonal (added once, after the all-reduce)
+template <typename T>
+__global__ __launch_bounds__(256) void gram_base_kernel(int kernel, kfun<T> kf, T kappa, const T *__restrict__ ssc,
+                                                        const T *__restrict__ norms, const T *__restrict__ ev,
+                                                        const T *__restrict__ p, int64_t m, T *__restrict__ raw,
+                                                        const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const T S = ssc[0];
+    T add;
+    if (kernel == 2) {
+        const T ei = ev[i];
+        add = ei * S + (T(1) - ei * ei) * p[i];
+    } else if (kernel == 1) {
+        const T bse = fma(kf.gamma, norms[i], kf.coef0);
+        T kii = T(1);
+        for (int q = 0; q < kf.degree; ++q) kii *= bse;
+        add = kappa * S + (kii - kappa) * p[i];
+    } else {
+        add = norms[i] * p[i];
+    }
+    raw[i] += add;
 }
 
 template <typename T>
-int64_t engine<T>::csr_bytes() const {
-    return 0;
+void host_check_csr(const int64_t *rowptr, const int32_t *col, int64_t n, int64_t d) {
+    if (!rowptr || !col || n < 1 || d < 1) throw mi_error(-1, "Data set is empty!");
+    if (rowptr[0] != 0) throw mi_error(-1, "CSR rowptr[0] must be 0");
+    for (int64_t i = 0; i < n; ++i) {
+        if (rowptr[i + 1] < rowptr[i]) throw mi_error(-1, "CSR rowptr must be non-decreasing");
+        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+            if (col[k] < 0 || col[k] >= d) throw mi_error(-1, "CSR column index out of range");
+            if (k > rowptr[i] && col[k] <= col[k - 1]) throw mi_error(-1, "CSR columns must be strictly ascending");
+        }
+    }
 }
 
-template void launch_q_sparse<float>(kfun<float>, const csr_data<float> &, int64_t, const float *, float *, hipStream_t);
-template void launch_q_sparse<double>(kfun<double>, const csr_data<double> &, int64_t, const double *, double *,
-                                      hipStream_t);
-#define INST(T)                                                                 \
-    template void engine<T>::sparse_kp_raw(const T *, const cg_scalars<T> *);   \
-    template void engine<T>::sparse_dominant(const T *);                        \
-    template int64_t engine<T>::csr_bytes() const;
+}  // namespace
+
+// ---- engine members ----------------------------------------------------------------------------------
+template <typename T>
+void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void *val, int val_fmt, int64_t n_,
+                          int64_t d_) {
+    host_check_csr<T>(rowptr, col, n_, d_);
+    if (!val && rowptr[n_] > 0) throw mi_error(-1, "CSR values missing");
+    if (val_fmt != PLSSVM_MI_VAL_REAL && val_fmt != PLSSVM_MI_VAL_FP22) throw mi_error(-1, "unknown value format");
+    if (val_fmt == PLSSVM_MI_VAL_FP22 && sizeof(T) != 4) throw mi_error(-5, "FP22 values need a float context");
+    MI_HIP_CHECK(hipSetDevice(device));
+    sparse = true;
+    n = n_;
+    d = d_;
+    m = n - 1;
+    nb = ceil_div(m, KP_TILE);
+    n_pad = std::max<int64_t>(nb, 1) * KP_TILE;
+    d_pad = d;
+    csr = csr_data<T>{};
+    csr.val_fmt = val_fmt;
+    const int64_t nnz = rowptr[m];  // rows 0..m-1
+    csr.nnz = nnz;
+    auto hval = [&](int64_t k) -> T {
+        return val_fmt == PLSSVM_MI_VAL_FP22 ? (T) fp22_get(static_cast<const uint32_t *>(val), k)
+                                             : static_cast<const T *>(val)[k];
+    };
+    // last point, densified (the reference's data_last_d_)
+    xlast_h.assign(d, T(0));
+    for (int64_t k = rowptr[m]; k < rowptr[n]; ++k) xlast_h[col[k]] = hval(k);
+    xlast.alloc(d, stream);
+    MI_HIP_CHECK(hipMemcpyAsync(xlast.get(), xlast_h.data(), sizeof(T) * (size_t) d, hipMemcpyHostToDevice, stream));
+
+    // CSR of rows 0..m-1
+    csr.rowptr.alloc(m + 1, stream);
+    MI_HIP_CHECK(hipMemcpyAsync(csr.rowptr.get(), rowptr, sizeof(int64_t) * (size_t) (m + 1), hipMemcpyHostToDevice,
+                                stream));
+    csr.col.alloc(std::max<int64_t>(nnz, 1), stream);
+    if (nnz) MI_HIP_CHECK(hipMemcpyAsync(csr.col.get(), col, sizeof(int32_t) * (size_t) nnz, hipMemcpyHostToDevice, stream));
+    if (val_fmt == PLSSVM_MI_VAL_FP22) {
+        const int64_t nw = fp22_words(std::max<int64_t>(nnz, 1));
+        csr.val22.alloc(nw + 1, stream);
+        if (nnz)
+            MI_HIP_CHECK(hipMemcpyAsync(csr.val22.get(), val, sizeof(uint32_t) * (size_t) fp22_words(nnz),
+                                        hipMemcpyHostToDevice, stream));
+    } else {
+        csr.val.alloc(std::max<int64_t>(nnz, 1), stream);
+        if (nnz) MI_HIP_CHECK(hipMemcpyAsync(csr.val.get(), val, sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice, stream));
+    }
+
+    // CSC of rows 0..m-1 (counting sort: rows ascending inside each column) and, per CSR entry, its
+    // CSC position (the column-join needs "rows < i in this column" = cpos - colptr)
+    std::vector<int64_t> colptr(d + 1, 0), cpos(std::max<int64_t>(nnz, 1));
+    for (int64_t k = 0; k < nnz; ++k) ++colptr[col[k] + 1];
+    for (int64_t f = 0; f < d; ++f) colptr[f + 1] += colptr[f];
+    std::vector<int64_t> fill(colptr.begin(), colptr.end() - 1);
+    std::vector<int32_t> crow(std::max<int64_t>(nnz, 1));
+    std::vector<T> cval_real;
+    std::vector<float> cval_f;
+    if (val_fmt == PLSSVM_MI_VAL_FP22) cval_f.resize(std::max<int64_t>(nnz, 1));
+    else cval_real.resize(std::max<int64_t>(nnz, 1));
+    for (int64_t i = 0; i < m; ++i) {
+        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+            const int64_t t = fill[col[k]]++;
+            crow[t] = (int32_t) i;
+            cpos[k] = t;
+            if (val_fmt == PLSSVM_MI_VAL_FP22) cval_f[t] = (float) hval(k);
+            else cval_real[t] = hval(k);
+        }
+    }
+    csr.colptr.alloc(d + 1, stream);
+    MI_HIP_CHECK(hipMemcpyAsync(csr.colptr.get(), colptr.data(), sizeof(int64_t) * (size_t) (d + 1),
+                                hipMemcpyHostToDevice, stream));
+    csr.crow.alloc(std::max<int64_t>(nnz, 1), stream);
+    if (nnz)
+        MI_HIP_CHECK(hipMemcpyAsync(csr.crow.get(), crow.data(), sizeof(int32_t) * (size_t) nnz, hipMemcpyHostToDevice,
+                                    stream));
+    if (val_fmt == PLSSVM_MI_VAL_FP22) {
+        std::vector<uint32_t> w(fp22_words(std::max<int64_t>(nnz, 1)) + 1, 0u);
+        for (int64_t t = 0; t < nnz; ++t) {  // re-pack in CSC order (decode(encode(decoded)) is exact)
+            const uint64_t code = fp22_encode_host(cval_f[t]);
+            const int64_t g = t >> 4;
+            const int bit = 22 * (int) (t & 15);
+            const int64_t wi = g * 11 + (bit >> 5);
+            const int s = bit & 31;
+            w[wi] |= (uint32_t) (code << s);
+            if (s > 10) w[wi + 1] |= (uint32_t) (code >> (32 - s));
+        }
+        csr.cval22.alloc((int64_t) w.size(), stream);
+        MI_HIP_CHECK(hipMemcpyAsync(csr.cval22.get(), w.data(), sizeof(uint32_t) * w.size(), hipMemcpyHostToDevice,
+                                    stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+    } else {
+        csr.cval.alloc(std::max<int64_t>(nnz, 1), stream);
+        if (nnz)
+            MI_HIP_CHECK(hipMemcpyAsync(csr.cval.get(), cval_real.data(), sizeof(T) * (size_t) nnz,
+                                        hipMemcpyHostToDevice, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+
+    norms.alloc(std::max<int64_t>(n_pad, 1), stream);
+    csr.e.alloc(std::max<int64_t>(n_pad, 1), stream);
+    if (m > 0)
+        hipLaunchKernelGGL(csr_norms_kernel<T>, dim3((unsigned) ceil_div(m, 16)), dim3(256), 0, stream,
+                           csr.rowptr.get(), csr.rvals(), m, gamma, norms.get(), csr.e.get());
+    MI_LAUNCH_CHECK();
+    finish_setup();
+
+    // per-column CSC range of this rank's rows (factored multi-rank); all rows in simulated mode
+    {
+        std::vector<int64_t> lo(d), hi(d);
+        const bool all_rows = (world == 1) || sim_world > 0;
+        for (int64_t f = 0; f < d; ++f) {
+            if (all_rows) {
+                lo[f] = colptr[f];
+                hi[f] = colptr[f + 1];
+            } else {
+                lo[f] = std::lower_bound(crow.begin() + colptr[f], crow.begin() + colptr[f + 1], (int32_t) r0) -
+                        crow.begin();
+                hi[f] = std::lower_bound(crow.begin() + colptr[f], crow.begin() + colptr[f + 1], (int32_t) r1) -
+                        crow.begin();
+            }
+        }
+        csr.col_lo.alloc(d, stream);
+        csr.col_hi.alloc(d, stream);
+        MI_HIP_CHECK(hipMemcpyAsync(csr.col_lo.get(), lo.data(), sizeof(int64_t) * (size_t) d, hipMemcpyHostToDevice,
+                                    stream));
+        MI_HIP_CHECK(hipMemcpyAsync(csr.col_hi.get(), hi.data(), sizeof(int64_t) * (size_t) d, hipMemcpyHostToDevice,
+                                    stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+
+    if (!factored()) {
+        // Gram pattern: row blocks owned by this rank, balanced by column-join incidences
+        const int64_t nRB = ceil_div(std::max<int64_t>(m, 1), GRAM_RB);
+        std::vector<int64_t> inc_rb(nRB, 0);
+        for (int64_t i = 0; i < m; ++i)
+            for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) inc_rb[i / GRAM_RB] += cpos[k] - colptr[col[k]];
+        const int eff_world = sim_world > 0 ? sim_world : world, eff_rank = sim_world > 0 ? sim_rank : rank;
+        std::vector<int64_t> cum(nRB + 1, 0);
+        for (int64_t I = 0; I < nRB; ++I) cum[I + 1] = cum[I] + inc_rb[I];
+        auto split = [&](int r) {
+            if (r <= 0) return (int64_t) 0;
+            if (r >= eff_world) return nRB;
+            return (int64_t) (std::lower_bound(cum.begin(), cum.end(), (cum[nRB] * r) / eff_world) - cum.begin());
+        };
+        csr.nRB = nRB;
+        csr.nW = ceil_div(std::max<int64_t>(m, 1), GRAM_CW);
+        csr.rb0 = std::min(split(eff_rank), nRB);
+        csr.rb1 = std::max(csr.rb0, std::min(split(eff_rank + 1), nRB));
+        csr.pair_bound = cum[csr.rb1] - cum[csr.rb0];
+        // device copy of cpos for the generator
+        dev_buf<int64_t> cpos_d;
+        cpos_d.alloc(std::max<int64_t>(nnz, 1), stream);
+        if (nnz)
+            MI_HIP_CHECK(hipMemcpyAsync(cpos_d.get(), cpos.data(), sizeof(int64_t) * (size_t) nnz, hipMemcpyHostToDevice,
+                                        stream));
+        int64_t max_inc = 0;
+        for (int64_t I = csr.rb0; I < csr.rb1; ++I) max_inc = std::max(max_inc, inc_rb[I]);
+        build_gram_blocks(cpos_d.get(), max_inc);
+    }
+}
+
+template <typename T>
+void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
+    csr.m_pad = round_up(std::max<int64_t>(m, 1), 256);
+    // host cell table
+    std::vector<gram_cell> cells;
+    std::vector<int64_t> rowoff_base(csr.nRB, 0);
+    int64_t ro_total = 0;
+    for (int64_t I = csr.rb0; I < csr.rb1; ++I) {
+        const int64_t nw = gram_nw(I, m);
+        rowoff_base[I] = ro_total;
+        for (int64_t W = 0; W < nw; ++W) cells.push_back(gram_cell{ (int32_t) I, (int32_t) W, ro_total + W * GRAM_RB });
+        ro_total += nw * GRAM_RB + 1;
+    }
+    csr.ncells = (int64_t) cells.size();
+    csr.cells.alloc(std::max<int64_t>(csr.ncells, 1), stream);
+    if (csr.ncells)
+        MI_HIP_CHECK(hipMemcpyAsync(csr.cells.get(), cells.data(), sizeof(gram_cell) * cells.size(),
+                                    hipMemcpyHostToDevice, stream));
+    csr.rowoff.alloc(std::max<int64_t>(ro_total, 1), stream);
+    csr.rb_base.alloc(std::max<int64_t>(csr.nRB, 1), stream);
+    csr.pj.alloc(std::max<int64_t>(csr.pair_bound, 1), stream, false);
+    csr.ps.alloc(std::max<int64_t>(csr.pair_bound, 1), stream, false);
+    csr.slab_row.alloc(std::max<int64_t>(csr.nW, 1) * csr.m_pad, stream);
+    csr.slab_col.alloc(std::max<int64_t>(csr.nRB, 1) * csr.m_pad, stream);
+    csr.ssc.alloc(2, stream);
+
+    // temporaries for one row block
+    const int64_t cap = std::max<int64_t>(max_inc, 1);
+    dev_buf<uint64_t> keys, keys_s;
+    dev_buf<T> vals, vals_s;
+    dev_buf<int64_t> cnt, off, nruns;
+    dev_buf<int32_t> rowcnt;
+    keys.alloc(cap, stream, false);
+    keys_s.alloc(cap, stream, false);
+    vals.alloc(cap, stream, false);
+    vals_s.alloc(cap, stream, false);
+    cnt.alloc(GRAM_RB + 1, stream);
+    off.alloc(GRAM_RB + 1, stream);
+    nruns.alloc(1, stream);
+    rowcnt.alloc(csr.nW * GRAM_RB + 1, stream);
+    size_t tmp_sort = 0, tmp_scan = 0, tmp_red = 0, tmp_scan32 = 0;
+    MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, keys.get(), keys_s.get(), vals.get(),
+                                                    vals_s.get(), (int) std::min<int64_t>(cap, INT32_MAX), 0, 64,
+                                                    stream));
+    MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_scan, cnt.get(), off.get(), GRAM_RB + 1, stream));
+    MI_HIP_CHECK(hipcub::DeviceReduce::ReduceByKey(nullptr, tmp_red, keys_s.get(), keys.get(), vals_s.get(),
+                                                   vals.get(), nruns.get(), hipcub::Sum(),
+                                                   (int) std::min<int64_t>(cap, INT32_MAX), stream));
+    MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_scan32, rowcnt.get(), rowcnt.get(),
+                                                  (int) (csr.nW * GRAM_RB + 1), stream));
+    dev_buf<unsigned char> tmp;
+    tmp.alloc((int64_t) std::max({ tmp_sort, tmp_scan, tmp_red, tmp_scan32, (size_t) 16 }), stream, false);
+    if (cap > INT32_MAX) throw mi_error(-5, "a Gram row block exceeds 2^31 incidences");
+
+    std::vector<int64_t> rb_base(csr.nRB, 0);
+    int64_t pos = 0;
+    const int end_bit = 32 + std::max(1, (int) std::ceil(std::log2((double) csr.nW + 1.0)));
+    for (int64_t I = csr.rb0; I < csr.rb1; ++I) {
+        const int64_t i0 = I * GRAM_RB, i1 = std::min<int64_t>(m, i0 + GRAM_RB), rows = i1 - i0;
+        const int64_t nw = gram_nw(I, m);
+        rb_base[I] = pos;
+        MI_HIP_CHECK(hipMemsetAsync(cnt.get(), 0, sizeof(int64_t) * (GRAM_RB + 1), stream));
+        hipLaunchKernelGGL(gram_count_kernel, dim3((unsigned) ceil_div(rows, 256)), dim3(256), 0, stream,
+                           csr.rowptr.get(), csr.col.get(), cpos, csr.colptr.get(), i0, i1, cnt.get());
+        MI_LAUNCH_CHECK();
+        size_t ts = tmp_scan;
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.get(), ts, cnt.get(), off.get(), (int) (rows + 1), stream));
+        int64_t total = 0;
+        MI_HIP_CHECK(hipMemcpyAsync(&total, off.get() + rows, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        MI_HIP_CHECK(hipMemsetAsync(rowcnt.get(), 0, sizeof(int32_t) * (size_t) (nw * GRAM_RB + 1), stream));
+        int64_t nu = 0;
+        if (total > 0) {
+            hipLaunchKernelGGL(gram_gen_kernel<T>, dim3((unsigned) rows), dim3(256), 0, stream, csr.rowptr.get(),
+                               csr.col.get(), csr.rvals(), cpos, csr.colptr.get(), csr.crow.get(), csr.cvals(), i0,
+                               off.get(), keys.get(), vals.get());
+            MI_LAUNCH_CHECK();
+            size_t t1s = tmp_sort;
+            MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp.get(), t1s, keys.get(), keys_s.get(), vals.get(),
+                                                            vals_s.get(), (int) total, 0, end_bit, stream));
+            size_t t2s = tmp_red;
+            MI_HIP_CHECK(hipcub::DeviceReduce::ReduceByKey(tmp.get(), t2s, keys_s.get(), keys.get(), vals_s.get(),
+                                                           vals.get(), nruns.get(), hipcub::Sum(), (int) total,
+                                                           stream));
+            MI_HIP_CHECK(hipMemcpyAsync(&nu, nruns.get(), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            hipLaunchKernelGGL(gram_rowcount_kernel, dim3((unsigned) ceil_div(nu, 256)), dim3(256), 0, stream,
+                               keys.get(), nruns.get(), rowcnt.get());
+            MI_LAUNCH_CHECK();
+            hipLaunchKernelGGL(gram_store_kernel<T>, dim3((unsigned) ceil_div(nu, 256)), dim3(256), 0, stream,
+                               keys.get(), vals.get(), nruns.get(), csr.pj.get() + pos, csr.ps.get() + pos);
+            MI_LAUNCH_CHECK();
+        }
+        size_t t3s = tmp_scan32;
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.get(), t3s, rowcnt.get(), csr.rowoff.get() + rowoff_base[I],
+                                                      (int) (nw * GRAM_RB + 1), stream));
+        pos += nu;
+    }
+    csr.pairs = pos;
+    MI_HIP_CHECK(hipMemcpyAsync(csr.rb_base.get(), rb_base.data(), sizeof(int64_t) * (size_t) csr.nRB,
+                                hipMemcpyHostToDevice, stream));
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    csr.have_gram = true;
+}
+
+template <typename T>
+void engine<T>::sparse_q() {
+    if (m <= 0) return;
+    T nlast = 0;
+    for (int64_t k = 0; k < d; ++k) nlast = std::fma(xlast_h[k], xlast_h[k], nlast);
+    hipLaunchKernelGGL(csr_q_kernel<T>, dim3((unsigned) ceil_div(m, 16)), dim3(256), 0, stream, kf(),
+                       csr.rowptr.get(), csr.col.get(), csr.rvals(), m, xlast.get(), nlast, norms.get(), q.get());
+    MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status) {
+    if (factored()) {
+        hipLaunchKernelGGL(csc_gemv_kernel<T>, dim3((unsigned) ceil_div(d, 4)), dim3(256), 0, stream,
+                           csr.col_lo.get(), csr.col_hi.get(), csr.crow.get(), csr.cvals(), d, p, w.get(), status);
+        MI_LAUNCH_CHECK();
+        allreduce(w.get(), d);
+        if (r1 > r0)
+            hipLaunchKernelGGL(csr_gemv_kernel<T>, dim3((unsigned) ceil_div(r1 - r0, 16)), dim3(256), 0, stream,
+                               csr.rowptr.get(), csr.col.get(), csr.rvals(), r0, r1, w.get(), raw.get(), status);
+        MI_LAUNCH_CHECK();
+        allgather_rows(raw.get());
+        return;
+    }
+    // separable sum: sum(e p) (rbf) or sum(p) (poly)
+    launch_dot2<T>(p, kernel == 2 ? csr.e.get() : nullptr, nullptr, nullptr, m, red.get(), status, stream);
+    launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+    sparse_dominant(p, status);
+    hipLaunchKernelGGL(gram_reduce_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream,
+                       csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, csr.rb0, csr.rb1, raw.get(), status);
+    MI_LAUNCH_CHECK();
+    allreduce(raw.get(), m);
+    if (!(sim_world > 0 && sim_rank != 0)) {
+        T kappa = 0;
+        if (kernel == 1) {
+            kappa = 1;
+            for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
+        }
+        hipLaunchKernelGGL(gram_base_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream, kernel, kf(),
+                           kappa, csr.ssc.get(), norms.get(), csr.e.get(), p, m, raw.get(), status);
+        MI_LAUNCH_CHECK();
+    }
+}
+
+template <typename T>
+void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
+    if (factored()) {
+        if (r1 > r0)
+            hipLaunchKernelGGL(csr_gemv_kernel<T>, dim3((unsigned) ceil_div(r1 - r0, 16)), dim3(256), 0, stream,
+                               csr.rowptr.get(), csr.col.get(), csr.rvals(), r0, r1, w.get(), raw.get(), status);
+        MI_LAUNCH_CHECK();
+        return;
+    }
+    if (csr.ncells == 0) return;
+    T kappa = 0;
+    if (kernel == 1) {
+        kappa = 1;
+        for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
+    }
+    const dim3 grid((unsigned) csr.ncells), block(512);
+    switch (kernel) {
+        case 0:
+            hipLaunchKernelGGL((gram_kp_kernel<T, 0>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
+                               csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
+                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status);
+            break;
+        case 1:
+            hipLaunchKernelGGL((gram_kp_kernel<T, 1>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
+                               csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
+                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status);
+            break;
+        default:
+            hipLaunchKernelGGL((gram_kp_kernel<T, 2>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
+                               csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
+                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status);
+            break;
+    }
+    MI_LAUNCH_CHECK();
+}
+
+#define INST(T)                                                                                                 \
+    template void engine<T>::setup_csr(const int64_t *, const int32_t *, const void *, int, int64_t, int64_t); \
+    template void engine<T>::build_gram_blocks(const int64_t *, int64_t);                                     \
+    template void engine<T>::sparse_q();                                                                      \
+    template void engine<T>::sparse_kp_raw(const T *, const cg_scalars<T> *);                                 \
+    template void engine<T>::sparse_dominant(const T *, const cg_scalars<T> *);
 INST(float)
 INST(double)
 #undef INST

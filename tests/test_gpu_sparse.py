@@ -1,0 +1,126 @@
+"""GPU parity of the sparse paths (CSR / packed FP22) against the oracle's CSR restatement.
+
+The reference has no sparse device path (its parser densifies, src/plssvm/parameter.cpp:66-87), so
+parity is "same math as the dense OpenMP semantics on the densified (and FP22-dequantised) matrix":
+the oracle's CSR functions are bitwise equal to its dense ones (tests/test_oracle.py).
+Tolerances as in test_gpu_parity.py (fp64 1e-12 / fp32 1e-4 of max|K·p|).
+"""
+import numpy as np
+import pytest
+
+import plssvm_sparse_fp22_amd as pm
+from plssvm_sparse_fp22_amd import datagen
+
+pytestmark = pytest.mark.gpu
+
+TOL = {np.float64: 1e-12, np.float32: 1e-4}
+
+
+def sparse_svm(csr, kernel, dtype, fp22=False, mode="auto", sim=None, gamma=None, coef0=1.0, y=None, cost=1.0):
+    rowptr, col, val, n, d = csr
+    p = pm.Parameter(kernel, gamma=gamma if gamma is not None else 1.0 / d, coef0=coef0, real_type=dtype, cost=cost)
+    if fp22:
+        from oracle import pyoracle
+
+        p.csr = (rowptr, col, pyoracle.fp22_pack(val), n, d)
+        p.val_fmt = pm._abi.VAL_FP22
+    else:
+        p.csr = (rowptr, col, val.astype(dtype), n, d)
+    p.labels = y
+    return pm.CSVM(p, kp_mode=mode, sim_rank=sim)
+
+
+def oracle_data(oracle, csr, dtype, fp22=False):
+    rowptr, col, val, n, d = csr
+    if fp22:
+        val = oracle.fp22_unpack(oracle.fp22_pack(val), val.size)
+    return oracle.Data(rowptr=rowptr, col=col, val=val.astype(dtype), n=n, d=d, dtype=dtype)
+
+
+def check_sparse_kp(oracle, csr, kernel, dtype, fp22=False, mode="auto", coef0=1.0):
+    svm = sparse_svm(csr, kernel, dtype, fp22=fp22, mode=mode, coef0=coef0)
+    svm.setup_data_on_device()
+    q = svm.generate_q()
+    data = oracle_data(oracle, csr, dtype, fp22)
+    g = dtype(1.0 / csr[4])
+    q_ref = oracle.generate_q(kernel, data, gamma=g, coef0=dtype(coef0))
+    np.testing.assert_allclose(q, q_ref, rtol=TOL[dtype], atol=TOL[dtype] * np.abs(q_ref).max())
+    m = csr[3] - 1
+    x = np.random.default_rng(m).uniform(1, 2, m).astype(dtype)
+    for add in (-1.0, 1.0):
+        ret = np.zeros(m, dtype=dtype)
+        svm.run_device_kernel(None, ret, x, add)
+        want = oracle.kp(kernel, data, q_ref, svm.QA_cost, dtype(1.0), add, x, gamma=g, coef0=dtype(coef0))
+        np.testing.assert_allclose(ret, want, rtol=0, atol=TOL[dtype] * np.abs(want).max(),
+                                   err_msg=f"{kernel} {np.dtype(dtype).name} fp22={fp22} mode={mode}")
+    info = svm.info()
+    svm.close()
+    return info
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("kernel,mode", [("linear", "auto"), ("linear", "pairwise"), ("polynomial", "auto"),
+                                         ("rbf", "auto")])
+@pytest.mark.parametrize("shape", [(300, 500, 10), (2500, 3000, 20), (9000, 20000, 15)])
+def test_sparse_kp(oracle, kernel, mode, dtype, shape):
+    n, d, k = shape
+    csr, _ = datagen.sparse_csr(n, d, k, seed=n + d, dtype=dtype)
+    info = check_sparse_kp(oracle, csr, kernel, dtype, mode=mode)
+    assert info["is_sparse"] == 1
+
+
+@pytest.mark.parametrize("kernel", ["linear", "rbf", "polynomial"])
+def test_sparse_fp22(oracle, kernel):
+    csr, _ = datagen.sparse_csr(3000, 4000, 25, seed=5, dtype=np.float32)
+    info = check_sparse_kp(oracle, csr, kernel, np.float32, fp22=True)
+    assert info["val_fmt"] == pm._abi.VAL_FP22
+
+
+def test_sparse_ragged_rows(oracle):
+    """empty rows, a dense row, duplicate-free but uneven rows, d not a multiple of anything."""
+    rng = np.random.default_rng(9)
+    n, d = 700, 333
+    rows = []
+    for i in range(n):
+        k = 0 if i % 97 == 0 else (d if i == 5 else int(rng.integers(1, 30)))
+        rows.append(np.sort(rng.choice(d, size=k, replace=False)))
+    rowptr = np.zeros(n + 1, np.int64)
+    rowptr[1:] = np.cumsum([r.size for r in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    val = rng.uniform(-1, 1, col.size)
+    csr = (rowptr, col, val, n, d)
+    for kernel in ("rbf", "polynomial", "linear"):
+        check_sparse_kp(oracle, csr, kernel, np.float64)
+        check_sparse_kp(oracle, csr, kernel, np.float64, mode="pairwise" if kernel == "linear" else "auto")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("kernel,mode", [("rbf", "auto"), ("linear", "auto")])
+def test_sparse_simulated_ranks(world, kernel, mode):
+    csr, _ = datagen.sparse_csr(6000, 5000, 20, seed=2, dtype=np.float64)
+    m = csr[3] - 1
+    x = np.linspace(1, 2, m)
+    full = sparse_svm(csr, kernel, np.float64, mode=mode)
+    full.setup_data_on_device()
+    full.generate_q()
+    want = full.run_device_kernel(None, np.zeros(m), x, 1.0)
+    total = np.zeros(m)
+    for r in range(world):
+        svm = sparse_svm(csr, kernel, np.float64, mode=mode, sim=(r, world))
+        svm.setup_data_on_device()
+        svm.generate_q()
+        total += svm.run_device_kernel(None, np.zeros(m), x, 1.0)
+        svm.close()
+    np.testing.assert_allclose(total, want, rtol=1e-12, atol=1e-12 * np.abs(want).max())
+
+
+@pytest.mark.parametrize("kernel", ["linear", "rbf"])
+def test_sparse_learn_matches_oracle(oracle, kernel):
+    csr, y = datagen.sparse_csr(2000, 2500, 30, seed=8, dtype=np.float64)
+    svm = sparse_svm(csr, kernel, np.float64, y=y, coef0=0.0)
+    svm.learn(imax=60)
+    ref = oracle.learn(kernel, oracle_data(oracle, csr, np.float64), y, imax=60, gamma=1.0 / 2500)
+    assert abs(svm.iters - ref["iters"]) <= 1
+    n = min(len(svm.trace), len(ref["trace"]), 6)
+    np.testing.assert_allclose(svm.trace[:n], ref["trace"][:n], rtol=1e-6)
+    np.testing.assert_allclose(svm.alpha, ref["alpha"], rtol=1e-6, atol=1e-6 * np.abs(ref["alpha"]).max())
