@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """bench.py — CG iterations/s of the MI355X PLSSVM hot path (BASELINE.json metric).
 
-One "step" = one CG iteration of openmp::csvm::solver_CG semantics (one implicit Q~·p over the
-whole problem + the device-resident vector updates + the per-iteration RCCL all-reduce when
-N > 1). Default workload = BASELINE.json configs[1]: dense RBF, 100k points x 256 features,
-fp64, generate_data.py-style blobs (seeded, synthetic). N > 1 splits the same problem's
-lower-triangle tiles over the ranks (strong scaling) with one all-reduce of the m-vector per K·p.
+One "step" = one CG iteration with openmp::csvm::solver_CG semantics: one implicit Q~·p over the
+whole problem + the device-resident vector updates + (N > 1) the per-iteration RCCL all-reduce.
+Default workload = BASELINE.json configs[1]: dense RBF, 100k points x 256 features, fp64,
+generate_data.py-style blobs (seeded, synthetic). N > 1 splits the same problem over the ranks
+(strong scaling). Other configs (--config) are the sparse / fp32 rows of BASELINE.json.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
 (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the environment).
@@ -26,22 +26,57 @@ import numpy as np  # noqa: E402
 import plssvm_sparse_fp22_amd as pm  # noqa: E402  (loads libplssvm_mi355x.so before torch)
 from plssvm_sparse_fp22_amd import datagen  # noqa: E402
 
-PEAKS = {  # MI355X_MICROARCH.md: dense fp64 78.6 TF (vector = matrix), fp32 157.3 TF, HBM 8 TB/s
-    "f64": 78.6e12,
-    "f32": 157.3e12,
-    "hbm": 8.0e12,
-}
+PEAKS = {"f64": 78.6e12, "f32": 157.3e12, "hbm": 8.0e12}  # MI355X_MICROARCH.md (dense MFMA, HBM3E)
+METRIC = "CG iters/sec + implicit K·p HBM GB/s vs roofline, N×d stated, 1/2/4/8 GPU"
 
 CONFIGS = {
-    # name: (kernel, n, d, dtype, layout, description)
-    "dense_rbf_100k": ("rbf", 100_000, 256, np.float64, "dense", "Dense RBF, 100k points x 256 features, fp64"),
-    "dense_linear_500": ("linear", 500, 4, np.float64, "dense", "generate_data.py 500x4 dense, linear, fp64"),
-    "dense_linear_500k": ("linear", 500_000, 1024, np.float32, "dense", "Dense linear, 500k x 1024, fp32 (MFMA)"),
+    # name: kernel, N, d, dtype, layout, nnz/row, description
+    "dense_rbf_100k": ("rbf", 100_000, 256, np.float64, "dense", 0,
+                       "Dense RBF, 100k points x 256 features, fp64 (BASELINE configs[1])"),
+    "dense_linear_500": ("linear", 500, 4, np.float64, "dense", 0,
+                         "generate_data.py 500x4 dense, linear, fp64 (configs[0])"),
+    "dense_linear_500k": ("linear", 500_000, 1024, np.float32, "dense", 0,
+                          "Dense linear, 500k x 1024, fp32, MFMA pairwise (configs[3])"),
+    "csr_linear_1m": ("linear", 1_000_000, 50_000, np.float32, "csr", 50,
+                      "CSR-sparse linear, 1M x 50k @ 0.1% nnz, fp32, factored (configs[2])"),
+    "csr_rbf_1m": ("rbf", 1_000_000, 50_000, np.float32, "csr", 50,
+                   "CSR-sparse RBF, 1M x 50k @ 0.1% nnz, fp32 (configs[2] with RBF: the 70% HBM target)"),
+    "fp22_rbf_2m": ("rbf", 2_000_000, 100_000, np.float32, "fp22", 50,
+                    "COO/CSR RBF with FP22-packed features, 2M x 100k @ 0.05% nnz (configs[4])"),
 }
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def make_problem(cfg, n_override, d_override, rank):
+    kernel, n, d, dtype, layout, k, desc = cfg
+    if n_override:
+        if layout != "dense" and not d_override:  # keep the column occupancy c_f = n k / d fixed
+            d = max(k, int(round(d * n_override / n)))
+        n = n_override
+    if d_override:
+        d = d_override
+    t0 = time.time()
+    p = pm.Parameter(kernel, gamma=1.0 / d, real_type=dtype)
+    if layout == "dense":
+        X, y = datagen.blobs(n, d, seed=2, dtype=dtype)
+        p.data, p.labels = X, y
+        extra = dict(X=X)
+    else:
+        csr, y = datagen.sparse_csr(n, d, k, seed=3 if layout == "csr" else 5, dtype=dtype)
+        if layout == "fp22":
+            from plssvm_sparse_fp22_amd.fp22 import pack
+
+            p.csr = (csr[0], csr[1], pack(csr[2]), n, d)
+            p.val_fmt = pm._abi.VAL_FP22
+        else:
+            p.csr = csr
+        p.labels = y
+        extra = dict(csr=csr)
+    log(f"[rank {rank}] {layout} data {n}x{d} {np.dtype(dtype).name} generated in {time.time() - t0:.1f}s")
+    return p, n, d, y, extra
 
 
 def main():
@@ -51,6 +86,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="dense_rbf_100k", choices=sorted(CONFIGS))
     ap.add_argument("--n", type=int, default=0, help="override number of points")
+    ap.add_argument("--d", type=int, default=0, help="override number of features")
     ap.add_argument("--kp-reps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -60,33 +96,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     dist = None
+    uid = None
     if world > 1:
-        import torch
         import torch.distributed as dist
 
         dist.init_process_group("gloo")
-        uid = [pm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        uid = uid[0]
-    else:
-        uid = None
+        box = [pm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
 
-    kernel, n, d, dtype, layout, desc = CONFIGS[args.config]
-    if args.n:
-        n = args.n
-    t0 = time.time()
-    X, y = datagen.blobs(n, d, seed=2, dtype=dtype)
-    log(f"[rank {rank}] data {n}x{d} {np.dtype(dtype).name} generated in {time.time() - t0:.1f}s")
-
-    p = pm.Parameter(kernel, gamma=1.0 / d, real_type=dtype)
-    p.data, p.labels = X, y
+    cfg = CONFIGS[args.config]
+    kernel, _, _, dtype, layout, _, desc = cfg
+    p, n, d, y, extra = make_problem(cfg, args.n, args.d, rank)
     svm = pm.CSVM(p, device=local_rank, rank=rank, world_size=world, uid=uid)
     t0 = time.time()
     svm.setup_data_on_device()
+    t_setup = time.time() - t0
     q = svm.generate_q()
     b = (y[:-1] - y[-1]).astype(dtype)
     delta0 = svm.cg_begin(b, q, eps=1e-3)
-    log(f"[rank {rank}] setup+q+r0 {time.time() - t0:.2f}s delta0={delta0:.6e}")
+    log(f"[rank {rank}] setup {t_setup:.2f}s, q + r0 {time.time() - t0 - t_setup:.2f}s, delta0={delta0:.6e}")
 
     def barrier():
         if dist is not None:
@@ -96,7 +125,7 @@ def main():
         svm.cg_step(args.warmup, force=True)
     barrier()
     t_start = time.perf_counter()
-    svm.cg_step(args.steps, force=True)  # ends with hipStreamSynchronize
+    svm.cg_step(args.steps, force=True)  # ends with hipStreamSynchronize on the engine stream
     elapsed = time.perf_counter() - t_start
     barrier()
     if dist is not None:
@@ -107,33 +136,17 @@ def main():
         elapsed = float(t.item())
     iters_per_s = args.steps / elapsed
 
-    # ---- roofline of the dominant kernel (hipEvents on the engine stream) ----
     info = svm.info()
     ms_kp, ms_dom = svm.time_kp(args.kp_reps)
-    m = n - 1
-    pairs = m * (m + 1) / 2 * (info["tiles_local"] / max(1, info["tiles_total"]))
-    if info["kp_mode"] == pm._abi.KP_FACTORED:
-        alg = 2.0 * (m // world + 1) * d * np.dtype(dtype).itemsize  # gemv_n pass: XT rows of this rank
-        bound, unit, peak = "hbm", "GB/s", PEAKS["hbm"]
-        achieved = alg / (ms_dom * 1e-3)
-        roof = dict(bound=bound, achieved=achieved / 1e9, peak=peak / 1e9, unit=unit, frac=achieved / peak,
-                    traffic=None)
-    else:
-        alg = 2.0 * d * pairs  # the Gram-block FLOP of the lower triangle (norm-trick form)
-        pk = PEAKS["f64" if dtype == np.float64 else "f32"]
-        achieved = alg / (ms_dom * 1e-3)
-        roof = dict(bound="mfma", achieved=achieved / 1e12, peak=pk / 1e12, unit="TFLOP/s", frac=achieved / pk,
-                    traffic=None, alg_flop_per_launch=alg, alg_flop_per_kp_survey=3.0 * d * m * (m + 1) / 2,
-                    kernel="kp_tile_kernel", launch_ms=ms_dom)
+    roof = roofline(cfg, info, n, d, world, ms_dom, extra)
 
-    # ---- CPU baseline: the oracle (port of the reference OpenMP kernel), rank 0, N = 1 only ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(kernel, X, dtype, d, m, args.cpu_seconds)
+        cpu = cpu_baseline(kernel, dtype, d, n - 1, args.cpu_seconds, extra)
 
     if rank == 0:
         out = {
-            "metric": "CG iters/sec + implicit K·p HBM GB/s vs roofline, N×d stated, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": iters_per_s,
             "unit": "CG iterations/s",
             "n_gpus": world,
@@ -144,9 +157,11 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64" if dtype == np.float64 else "f32",
-            "data": "synthetic (seeded generate_data.py-style blobs)",
+            "data": "synthetic (seeded generate_data.py-style blobs / sparse CSR)",
             "config": {"workload": desc, "N": n, "d": d, "kernel": kernel, "layout": layout,
-                       "parallelism": f"row-block triangle tiles x{world}, RCCL all-reduce"},
+                       "kp_mode": {1: "pairwise", 2: "factored"}[info["kp_mode"]],
+                       "parallelism": f"x{world} GPUs: work split of the implicit matrix, RCCL all-reduce per K·p",
+                       "setup_s": round(t_setup, 3)},
             "roofline": roof,
             "cpu_baseline": cpu,
             "kp_ms": ms_kp,
@@ -157,32 +172,75 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(kernel, X, dtype, d, m, budget_s):
-    """Time the oracle's OpenMP K·p (reference Release flags) on a leading-rows sample; scale by (m/m')^2."""
+def roofline(cfg, info, n, d, world, ms_dom, extra):
+    kernel, _, _, dtype, layout, _, _ = cfg
+    m = n - 1
+    s = ms_dom * 1e-3
+    if layout == "dense" and info["kp_mode"] == pm._abi.KP_PAIRWISE:
+        pairs = m * (m + 1) / 2 * info["tiles_local"] / max(1, info["tiles_total"])
+        alg = 2.0 * d * pairs  # Gram-block FLOP of this rank's lower-triangle tiles (GEMM form)
+        pk = PEAKS["f64" if dtype == np.float64 else "f32"]
+        return dict(bound="mfma", achieved=alg / s / 1e12, peak=pk / 1e12, unit="TFLOP/s", frac=alg / s / pk,
+                    traffic=None, kernel="kp_tile_kernel", launch_ms=ms_dom, alg_flop_per_launch=alg,
+                    alg_flop_per_kp_survey=3.0 * d * m * (m + 1) / 2)
+    es = np.dtype(dtype).itemsize
+    if info["kp_mode"] == pm._abi.KP_FACTORED:
+        if layout == "dense":
+            alg = 2.0 * m * d * es / world
+            kname = "gemv_t_kernel+gemv_n_kernel"
+        else:
+            nnz = info["nnz"]
+            alg = (2 * (nnz * (4 + es) + (m + 1) * 8) + 4 * m * es + 2 * d * es) / world
+            kname = "csc_gemv_kernel+csr_gemv_kernel"
+        return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
+                    frac=alg / s / PEAKS["hbm"], traffic=None, kernel=kname, launch_ms=ms_dom, alg_bytes=alg)
+    # sparse Gram pattern (poly / rbf): SURVEY §8(d) 3-RBF / 5 figure, this rank's share of the pairs
+    col = extra["csr"][1]
+    c = np.bincount(col, minlength=d).astype(np.float64)
+    vb = 2.75 if layout == "fp22" else es
+    co = float((c * (c + 1) / 2).sum())
+    alg = (co * (4 + vb) + col.size * (4 + vb) + 3 * m * es) / world
+    stream = info["pairs"] * (2 + es)
+    return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s", frac=alg / s / PEAKS["hbm"],
+                traffic=None, kernel="gram_kp_kernel", launch_ms=ms_dom, alg_bytes=alg,
+                stream_bytes_per_launch=stream, stream_GBps=stream / s / 1e9, pairs=info["pairs"])
+
+
+def cpu_baseline(kernel, dtype, d, m, budget_s, extra):
+    """The oracle's OpenMP K·p (reference Release flags) on a leading-rows sample, scaled to N."""
     from oracle import pyoracle
 
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     gamma = np.dtype(dtype).type(1.0 / d)
 
+    def sample(n_s):
+        if "X" in extra:
+            return pyoracle.Data(extra["X"][:n_s], dtype=dtype)
+        rowptr, col, val, n, dd = extra["csr"]
+        e = rowptr[n_s]
+        return pyoracle.Data(rowptr=rowptr[: n_s + 1], col=col[:e], val=val[:e], n=n_s, d=dd, dtype=dtype)
+
     def run(n_s):
-        data = pyoracle.Data(X[:n_s], dtype=dtype)
+        data = sample(n_s)
         q = pyoracle.generate_q(kernel, data, gamma=gamma, fast=True)
         pvec = np.ones(n_s - 1, dtype=dtype)
         t = time.perf_counter()
         pyoracle.kp(kernel, data, q, dtype(1.0), dtype(1.0), 1.0, pvec, gamma=gamma, nthreads=threads, fast=True)
         return time.perf_counter() - t
 
-    n_s = min(X.shape[0], 3000)
+    n_all = m + 1
+    n_s = min(n_all, 3000)
     t = run(n_s)
     target = budget_s * 0.8
-    if t < target and n_s < X.shape[0]:
-        n_s = int(min(X.shape[0], 40_000, n_s * math.sqrt(target / max(t, 1e-3))))
+    if t < target and n_s < n_all:
+        n_s = int(min(n_all, 60_000, n_s * math.sqrt(target / max(t, 1e-3))))
         t = run(n_s)
     ms = n_s - 1
-    t_full = t * (m * (m + 1)) / (ms * (ms + 1))
+    t_full = t * (m * (m + 1)) / (ms * (ms + 1))  # the reference kernel visits every lower-triangle pair
     return {"value": 1.0 / t_full, "unit": "CG iterations/s", "cores": threads, "kind": "port",
-            "sample": f"one K·p on the first {n_s} of {m + 1} points ({t:.2f}s), scaled by pair count to N={m + 1}",
-            "pair_feature_per_s": ms * (ms + 1) / 2 * d / t}
+            "sample": f"one K·p of the oracle (reference OpenMP kernel restated, -O3 -ffast-math) on the first "
+                      f"{n_s} of {n_all} points ({t:.2f}s), scaled by the lower-triangle pair count to N={n_all}",
+            "pair_per_s": ms * (ms + 1) / 2 / t}
 
 
 if __name__ == "__main__":

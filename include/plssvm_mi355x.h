@@ -153,6 +153,7 @@ typedef struct {
     int64_t n, d, m, n_pad, d_pad, nnz;
     int64_t tiles_total, tiles_local, tile_rows, tile_cols;
     int64_t device_bytes;
+    int64_t pairs; /* sparse pairwise kernels: stored overlapping pairs (j < i) of this rank */
     int kp_mode, rank, world_size, real_bytes, kernel, is_sparse, val_fmt;
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);

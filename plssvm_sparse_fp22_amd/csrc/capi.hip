@@ -256,6 +256,7 @@ int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
         info->tile_rows = plssvm_mi::KP_TILE;
         info->tile_cols = plssvm_mi::KP_TILE;
         info->device_bytes = e.device_bytes();
+        info->pairs = e.csr.pairs;
         info->kp_mode = e.factored() ? PLSSVM_MI_KP_FACTORED : PLSSVM_MI_KP_PAIRWISE;
         info->rank = e.rank;
         info->world_size = e.world;

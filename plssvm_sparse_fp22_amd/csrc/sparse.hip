@@ -601,7 +601,10 @@ void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status) {
 
 template <typename T>
 void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
-    if (factored()) {
+    if (factored()) {  // both SpMV passes (the factored K·p without its collectives)
+        hipLaunchKernelGGL(csc_gemv_kernel<T>, dim3((unsigned) ceil_div(d, 4)), dim3(256), 0, stream,
+                           csr.col_lo.get(), csr.col_hi.get(), csr.crow.get(), csr.cvals(), d, p, w.get(), status);
+        MI_LAUNCH_CHECK();
         if (r1 > r0)
             hipLaunchKernelGGL(csr_gemv_kernel<T>, dim3((unsigned) ceil_div(r1 - r0, 16)), dim3(256), 0, stream,
                                csr.rowptr.get(), csr.col.get(), csr.rvals(), r0, r1, w.get(), raw.get(), status);

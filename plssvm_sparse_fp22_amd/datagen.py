@@ -49,8 +49,8 @@ def sparse_csr(n, d, nnz_per_row, seed=3, dtype=np.float32):
             dup = (np.diff(c, axis=1) == 0).any(axis=1) if k > 1 else np.zeros(e - a, bool)
             if not dup.any():
                 break
-            idx = np.nonzero(dup)[0]
-            cc = np.stack([rng.choice(d, size=k, replace=False) for _ in idx])
+            idx = np.nonzero(dup)[0]  # redraw rows with a repeated column until all are distinct
+            cc = rng.integers(0, d, size=(idx.size, k))
             cc.sort(axis=1)
             c[idx] = cc
         col[a:e] = c

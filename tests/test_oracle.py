@@ -167,3 +167,13 @@ def test_parser_sparse_fixture():
     (rowptr, col, val, n, d), _ = parse_libsvm(fixture_path("5x4.sparse.libsvm"), sparse=True)
     assert n == 5 and d == 4 and list(rowptr) == [0, 0, 1, 2, 4, 5]
     assert np.array_equal(datagen.densify((rowptr, col, val, n, d)), want)
+
+
+def test_product_fp22_codec_matches_oracle(oracle):
+    from plssvm_sparse_fp22_amd import fp22
+
+    rng = np.random.default_rng(4)
+    v = np.concatenate([rng.normal(size=4099).astype(np.float32) * 10, np.float32([np.inf, -np.inf, 0, -0.0])])
+    assert np.array_equal(fp22.pack(v), oracle.fp22_pack(v))
+    assert np.array_equal(fp22.unpack(fp22.pack(v), v.size), oracle.fp22_unpack(oracle.fp22_pack(v), v.size))
+    assert np.isnan(fp22.unpack(fp22.pack(np.float32([np.nan])), 1)[0])
