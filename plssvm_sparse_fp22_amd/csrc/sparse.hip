@@ -143,7 +143,8 @@ __global__ __launch_bounds__(256) void gram_gen_kernel(const int64_t *__restrict
         const T xi = val[k];
         for (int64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
             const uint64_t j = (uint64_t) crow[t];
-            keys[out + (t - c0)] = ((j / GRAM_CW) << 32) | (il << 16) | (j % GRAM_CW);
+            constexpr uint64_t CW = gram_cw<T>();
+            keys[out + (t - c0)] = ((j / CW) << 32) | (il << 16) | (j % CW);
             vals[out + (t - c0)] = xi * cval[t];
         }
         out += c1 - c0;
@@ -170,64 +171,184 @@ __global__ __launch_bounds__(256) void gram_store_kernel(const uint64_t *__restr
 }
 
 // ---- Gram K·p ---------------------------------------------------------------------------------------------
-template <typename T, int KERNEL>
-__global__ __launch_bounds__(512) void gram_kp_kernel(const gram_cell *__restrict__ cells,
-                                                      const int64_t *__restrict__ rb_base,
-                                                      const int32_t *__restrict__ rowoff,
-                                                      const uint16_t *__restrict__ pj, const T *__restrict__ ps,
-                                                      const T *__restrict__ norms, const T *__restrict__ ev,
-                                                      const T *__restrict__ p, T *__restrict__ slab_row,
-                                                      T *__restrict__ slab_col, int64_t m, int64_t m_pad, kfun<T> kf,
-                                                      T kappa, const cg_scalars<T> *__restrict__ status) {
-    __shared__ T colacc[GRAM_CW];
-    if (status != nullptr && status->converged) return;
-    const gram_cell cell = cells[xcd_remap(blockIdx.x, gridDim.x)];
-    for (int t = threadIdx.x; t < GRAM_CW; t += 512) colacc[t] = T(0);
-    __syncthreads();
-    const int64_t I0 = (int64_t) cell.I * GRAM_RB, W0 = (int64_t) cell.W * GRAM_CW;
-    const int rows = (int) min<int64_t>(GRAM_RB, m - I0);
-    const int64_t base = rb_base[cell.I];
-    const int32_t *ro = rowoff + cell.rowoff;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int il = wave; il < rows; il += 8) {
-        const int64_t i = I0 + il;
-        const int64_t a = base + ro[il], b = base + ro[il + 1];
-        const T pi = p[i];
-        const T ni = norms[i];
-        const T ei = (KERNEL == 2) ? ev[i] : T(0);
-        T acc = 0;
-        for (int64_t e = a + lane; e < b; e += 64) {
-            const int jl = pj[e];
-            const T s = ps[e];
-            const int64_t j = W0 + jl;
-            T c;
-            if (KERNEL == 2) {
-                T dist = ni + norms[j] - T(2) * s;
-                dist = dist > T(0) ? dist : T(0);
-                c = exp(-kf.gamma * dist) - ei * ev[j];
-            } else if (KERNEL == 1) {
-                const T bse = fma(kf.gamma, s, kf.coef0);
-                T kv = T(1);
-                for (int q = 0; q < kf.degree; ++q) kv *= bse;
-                c = kv - kappa;
-            } else {
-                c = s;
-            }
-            acc = fma(c, p[j], acc);
-            atomicAdd(&colacc[jl], c * pi);
-        }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-        if (lane == 0) slab_row[(int64_t) cell.W * m_pad + i] = acc;
-    }
-    __syncthreads();
-    const int wlen = (int) min<int64_t>(GRAM_CW, m - W0);
-    for (int t = threadIdx.x; t < wlen; t += 512) slab_col[(int64_t) cell.I * m_pad + W0 + t] = colacc[t];
+__host__ __device__ inline int64_t gram_nw(int64_t I, int64_t m, int64_t cw) {
+    const int64_t hi = m < (I + 1) * GRAM_RB ? m : (I + 1) * GRAM_RB;  // rows of block I are < hi, so j < hi
+    return (hi + cw - 1) / cw;
 }
 
-__host__ __device__ inline int64_t gram_nw(int64_t I, int64_t m) {
-    const int64_t hi = m < (I + 1) * GRAM_RB ? m : (I + 1) * GRAM_RB;  // rows of block I are < hi, so j < hi
-    return (hi + GRAM_CW - 1) / GRAM_CW;
+template <typename T>
+__device__ __forceinline__ void load8(const T *__restrict__ ps, int64_t e0, T (&s)[8]) {
+    if constexpr (sizeof(T) == 4) {
+        const float4 a = *reinterpret_cast<const float4 *>(ps + e0), b = *reinterpret_cast<const float4 *>(ps + e0 + 4);
+        s[0] = a.x, s[1] = a.y, s[2] = a.z, s[3] = a.w, s[4] = b.x, s[5] = b.y, s[6] = b.z, s[7] = b.w;
+    } else {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const double2 v = *reinterpret_cast<const double2 *>(ps + e0 + 2 * h);
+            s[2 * h] = v.x, s[2 * h + 1] = v.y;
+        }
+    }
+}
+
+// One 1024-thread workgroup per cell (2048 rows x CW-row window). The cell's pairs are one
+// contiguous, row-sorted stream cut into 8-pair chunks; each wave walks a contiguous range of
+// chunks (64 per step, lane = chunk), so a lane's row only moves forward and is tracked
+// incrementally. Per step and lane: 16 B of j + 32/64 B of s (prefetched one step ahead), the
+// window's n_j, e_j, p_j from LDS, mirrored column sums into an LDS accumulator (ds_add), row
+// partials reduced across lanes by a segmented shuffle scan and added by segment heads.
+template <typename T, int KERNEL>
+__global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restrict__ cells,
+                                                       const int64_t *__restrict__ rb_base,
+                                                       const int32_t *__restrict__ rowoff,
+                                                       const uint16_t *__restrict__ pj, const T *__restrict__ ps,
+                                                       const T *__restrict__ norms, const T *__restrict__ ev,
+                                                       const T *__restrict__ p, T *__restrict__ slab_row,
+                                                       T *__restrict__ slab_col, int64_t m, int64_t m_pad, kfun<T> kf,
+                                                       T kappa, const cg_scalars<T> *__restrict__ status,
+                                                       int ablate) {
+    constexpr int CW = gram_cw<T>();
+    __shared__ T wn[CW], we[CW], wp[CW], colacc[CW];
+    __shared__ T rowacc[GRAM_RB];
+    __shared__ int32_t ro[GRAM_RB + 1];
+    if (status != nullptr && status->converged) return;
+    const gram_cell cell = cells[xcd_remap(blockIdx.x, gridDim.x)];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t I0 = (int64_t) cell.I * GRAM_RB, W0 = (int64_t) cell.W * CW;
+    const int rows = (int) min<int64_t>(GRAM_RB, m - I0);
+    const int wlen = (int) min<int64_t>(CW, m - W0);
+    for (int t = tid; t < CW; t += 1024) {
+        const bool ok = t < wlen;
+        wn[t] = ok ? norms[W0 + t] : T(0);
+        we[t] = (KERNEL == 2 && ok) ? ev[W0 + t] : T(0);
+        wp[t] = ok ? p[W0 + t] : T(0);
+        colacc[t] = T(0);
+    }
+    for (int t = tid; t < GRAM_RB; t += 1024) rowacc[t] = T(0);
+    for (int t = tid; t <= rows; t += 1024) ro[t] = rowoff[cell.rowoff + t];
+    __syncthreads();
+
+    const int64_t base = rb_base[cell.I];
+    const int64_t A = base + ro[0], B = base + ro[rows];
+    const int64_t c0 = A >> 3, c1 = (B + 7) >> 3;
+    const int64_t per_wave = ((c1 - c0 + 15) / 16 + 63) / 64 * 64;
+    const int64_t wbeg = c0 + wave * per_wave;
+    const int64_t wend = min<int64_t>(c1, wbeg + per_wave);
+    const T gamma = kf.gamma;
+
+    // lane state: current row, its end (absolute pair index), its p / norm / e
+    int r = 0;
+    int64_t rend = 0;
+    T pi = 0, ni = 0, ei = 0;
+    auto seek = [&](int64_t e) {  // move r forward to the row containing pair e
+        const int32_t rel = (int32_t) (e - base);
+        if (rend <= e) {
+            int steps = 0;
+            while (steps < 8 && ro[r + 1] <= rel) ++r, ++steps;
+            if (ro[r + 1] <= rel) {  // long jump: binary search in [r, rows)
+                int lo = r, hi = rows;
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (ro[mid] <= rel) lo = mid;
+                    else hi = mid;
+                }
+                r = lo;
+            }
+            rend = base + ro[r + 1];
+            pi = p[I0 + r];
+            ni = norms[I0 + r];
+            if (KERNEL == 2) ei = ev[I0 + r];
+        }
+    };
+
+    uint4 jv_n = make_uint4(0, 0, 0, 0);
+    T s_n[8];
+    if (wbeg + lane < wend) {
+        jv_n = *reinterpret_cast<const uint4 *>(pj + ((wbeg + lane) << 3));
+        load8<T>(ps, (wbeg + lane) << 3, s_n);
+    }
+    bool first = true;
+    for (int64_t cb = wbeg; cb < wend; cb += 64) {  // wave-uniform trip count
+        const int64_t c = cb + lane;
+        const bool have = c < wend;
+        const uint4 jv = jv_n;
+        T s[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[k] = s_n[k];
+        if (cb + 64 + lane < wend) {  // prefetch the next step
+            jv_n = *reinterpret_cast<const uint4 *>(pj + ((cb + 64 + lane) << 3));
+            load8<T>(ps, (cb + 64 + lane) << 3, s_n);
+        }
+        int rl = -1;  // row of this lane's last pair (for the cross-lane reduction)
+        T acc = 0;
+        if (have) {
+            const int64_t e0 = c << 3;
+            if (first) {
+                rend = 0;
+                r = 0;
+            }
+            first = false;
+            const uint32_t jw[4] = { jv.x, jv.y, jv.z, jv.w };
+            int jl[8];
+            T gn[8], ge[8], gp[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                jl[k] = (int) ((jw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+                gn[k] = wn[jl[k]];
+                ge[k] = we[jl[k]];
+                gp[k] = wp[jl[k]];
+            }
+            const int64_t ea = e0 > A ? e0 : A;
+            seek(ea);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int64_t e = e0 + k;
+                if (e < A || e >= B) continue;
+                if (e >= rend) {
+                    if (acc != T(0)) atomicAdd(&rowacc[r], acc);
+                    acc = T(0);
+                    seek(e);
+                }
+                T cv;
+                if (KERNEL == 2) {
+                    T dist = ni + gn[k] - T(2) * s[k];
+                    dist = dist > T(0) ? dist : T(0);
+                    cv = (ablate & 2) ? dist - ei * ge[k] : exp(-gamma * dist) - ei * ge[k];
+                } else if (KERNEL == 1) {
+                    const T bse = fma(gamma, s[k], kf.coef0);
+                    T kv = T(1);
+                    for (int q = 0; q < kf.degree; ++q) kv *= bse;
+                    cv = kv - kappa;
+                } else {
+                    cv = s[k];
+                }
+                acc = fma(cv, gp[k], acc);
+                if (ablate & 1) {
+                    acc += cv * pi;  // timing-only ablation: no LDS column atomics
+                } else if (ablate & 4) {
+                    atomicAdd(reinterpret_cast<int *>(&colacc[jl[k]]), (int) (cv * pi * T(1e6)));
+                } else if (ablate & 8) {
+                    atomicAdd(reinterpret_cast<unsigned long long *>(&colacc[jl[k] & ~1]),
+                              (unsigned long long) (long long) (cv * pi * T(1e6)));
+                } else {
+                    atomicAdd(&colacc[jl[k]], cv * pi);
+                }
+            }
+            rl = r;
+        }
+        // segmented reduction of (row, partial) across the wave: rows are non-decreasing in lane order
+        T sacc = acc;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const T so = __shfl_down(sacc, off);
+            const int rr = __shfl_down(rl, off);
+            if (lane + off < 64 && rr == rl) sacc += so;
+        }
+        const int rprev = __shfl_up(rl, 1);
+        if (rl >= 0 && (lane == 0 || rprev != rl)) atomicAdd(&rowacc[rl], sacc);
+    }
+    __syncthreads();
+    for (int t = tid; t < rows; t += 1024) slab_row[(int64_t) cell.W * m_pad + I0 + t] = rowacc[t];
+    for (int t = tid; t < wlen; t += 1024) slab_col[(int64_t) cell.I * m_pad + W0 + t] = colacc[t];
 }
 
 template <typename T>
@@ -235,17 +356,18 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const T *__restrict__ 
                                                           const T *__restrict__ slab_col, int64_t m, int64_t m_pad,
                                                           int64_t rb0, int64_t rb1, T *__restrict__ raw,
                                                           const cg_scalars<T> *__restrict__ status) {
+    constexpr int64_t CW = gram_cw<T>();
     if (status != nullptr && status->converged) return;
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
-    const int64_t I = i / GRAM_RB, W = i / GRAM_CW;
+    const int64_t I = i / GRAM_RB, W = i / CW;
     T s = 0;
     if (I >= rb0 && I < rb1) {
-        const int64_t nw = gram_nw(I, m);
+        const int64_t nw = gram_nw(I, m, CW);
         for (int64_t w = 0; w < nw; ++w) s += slab_row[w * m_pad + i];
     }
     for (int64_t J = max<int64_t>(rb0, I); J < rb1; ++J) {  // blocks with rows > i may pair with j = i
-        if (W < gram_nw(J, m)) s += slab_col[J * m_pad + i];
+        if (W < gram_nw(J, m, CW)) s += slab_col[J * m_pad + i];
     }
     raw[i] = s;
 }
@@ -273,6 +395,16 @@ __global__ __launch_bounds__(256) void gram_base_kernel(int kernel, kfun<T> kf, 
         add = norms[i] * p[i];
     }
     raw[i] += add;
+}
+
+// timing-only ablation switch for profiling the Gram kernel (results are wrong when non-zero):
+// PLSSVM_MI_GRAM_ABLATE bit 0 = drop the LDS column atomics, bit 1 = drop the exp
+int gram_ablate() {
+    static const int v = [] {
+        const char *s = std::getenv("PLSSVM_MI_GRAM_ABLATE");
+        return s ? std::atoi(s) : 0;
+    }();
+    return v;
 }
 
 template <typename T>
@@ -434,7 +566,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             return (int64_t) (std::lower_bound(cum.begin(), cum.end(), (cum[nRB] * r) / eff_world) - cum.begin());
         };
         csr.nRB = nRB;
-        csr.nW = ceil_div(std::max<int64_t>(m, 1), GRAM_CW);
+        csr.nW = ceil_div(std::max<int64_t>(m, 1), (int64_t) gram_cw<T>());
         csr.rb0 = std::min(split(eff_rank), nRB);
         csr.rb1 = std::max(csr.rb0, std::min(split(eff_rank + 1), nRB));
         csr.pair_bound = cum[csr.rb1] - cum[csr.rb0];
@@ -457,8 +589,9 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     std::vector<gram_cell> cells;
     std::vector<int64_t> rowoff_base(csr.nRB, 0);
     int64_t ro_total = 0;
+    const int64_t CW = gram_cw<T>();
     for (int64_t I = csr.rb0; I < csr.rb1; ++I) {
-        const int64_t nw = gram_nw(I, m);
+        const int64_t nw = gram_nw(I, m, CW);
         rowoff_base[I] = ro_total;
         for (int64_t W = 0; W < nw; ++W) cells.push_back(gram_cell{ (int32_t) I, (int32_t) W, ro_total + W * GRAM_RB });
         ro_total += nw * GRAM_RB + 1;
@@ -470,8 +603,10 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
                                     hipMemcpyHostToDevice, stream));
     csr.rowoff.alloc(std::max<int64_t>(ro_total, 1), stream);
     csr.rb_base.alloc(std::max<int64_t>(csr.nRB, 1), stream);
-    csr.pj.alloc(std::max<int64_t>(csr.pair_bound, 1), stream, false);
-    csr.ps.alloc(std::max<int64_t>(csr.pair_bound, 1), stream, false);
+    // each row block's pairs start 8-aligned (the K·p kernel reads 8 pairs per lane with 16-byte loads)
+    const int64_t pcap = csr.pair_bound + 8 * (csr.rb1 - csr.rb0) + 16;
+    csr.pj.alloc(pcap, stream);
+    csr.ps.alloc(pcap, stream);
     csr.slab_row.alloc(std::max<int64_t>(csr.nW, 1) * csr.m_pad, stream);
     csr.slab_col.alloc(std::max<int64_t>(csr.nRB, 1) * csr.m_pad, stream);
     csr.ssc.alloc(2, stream);
@@ -509,7 +644,8 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     const int end_bit = 32 + std::max(1, (int) std::ceil(std::log2((double) csr.nW + 1.0)));
     for (int64_t I = csr.rb0; I < csr.rb1; ++I) {
         const int64_t i0 = I * GRAM_RB, i1 = std::min<int64_t>(m, i0 + GRAM_RB), rows = i1 - i0;
-        const int64_t nw = gram_nw(I, m);
+        const int64_t nw = gram_nw(I, m, CW);
+        pos = round_up(pos, 8);
         rb_base[I] = pos;
         MI_HIP_CHECK(hipMemsetAsync(cnt.get(), 0, sizeof(int64_t) * (GRAM_RB + 1), stream));
         hipLaunchKernelGGL(gram_count_kernel, dim3((unsigned) ceil_div(rows, 256)), dim3(256), 0, stream,
@@ -617,22 +753,22 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
         kappa = 1;
         for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
     }
-    const dim3 grid((unsigned) csr.ncells), block(512);
+    const dim3 grid((unsigned) csr.ncells), block(1024);
     switch (kernel) {
         case 0:
             hipLaunchKernelGGL((gram_kp_kernel<T, 0>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
                                csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
-                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status);
+                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status, gram_ablate());
             break;
         case 1:
             hipLaunchKernelGGL((gram_kp_kernel<T, 1>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
                                csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
-                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status);
+                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status, gram_ablate());
             break;
         default:
             hipLaunchKernelGGL((gram_kp_kernel<T, 2>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
                                csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
-                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status);
+                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status, gram_ablate());
             break;
     }
     MI_LAUNCH_CHECK();

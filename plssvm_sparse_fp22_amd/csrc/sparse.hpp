@@ -55,7 +55,10 @@ struct vals_t {
 // a cell (I, W) holds, row by row (i ascending) then j ascending, every j in window W with
 // s_ij = x_i . x_j structurally non-zero (some shared feature), stored as (uint16 j - W*CW, s).
 constexpr int GRAM_RB = 2048;
-constexpr int GRAM_CW = 8192;
+// window edge: the K·p kernel stages n_j, e_j, p_j of the window plus a column accumulator in LDS
+// (4 x 8192 x 4 B fp32 / 4 x 4096 x 8 B fp64 = 128 KiB) — one 1024-thread workgroup per CU
+template <typename T>
+constexpr int gram_cw() { return sizeof(T) == 8 ? 4096 : 8192; }
 
 struct gram_cell {
     int32_t I, W;
