@@ -1,0 +1,177 @@
+// plssvm-train for the MI355X backend: same flags, defaults and output as the reference executable
+// (src/main_train.cpp:27-91, src/plssvm/parameter_train.cpp:38-142), training through
+// plssvm::mi355x::csvm<T> (host/csvm.hpp) on libplssvm_mi355x.so.
+//
+// Additions (not in the reference): --sparse keeps LIBSVM input as CSR (the reference densifies),
+// --max_iter overrides the CG limit (default: num_features, csvm.cpp:256), --single trains in fp32
+// (the reference selects that at compile time, main_train.cpp:21-25), --device picks the GPU.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "csvm.hpp"
+
+namespace {
+
+const char *kHelp =
+    "LS-SVM with multiple (GPU-)backends\n"
+    "Usage:\n"
+    "  plssvm-train [OPTION...] training_set_file [model_file]\n\n"
+    "  -t, --kernel_type arg      set type of kernel function.\n"
+    "                                  0 -- linear: u'*v\n"
+    "                                  1 -- polynomial: (gamma*u'*v + coef0)^degree\n"
+    "                                  2 -- radial basis function: exp(-gamma*|u-v|^2) (default: 0)\n"
+    "  -d, --degree arg           set degree in kernel function (default: 3)\n"
+    "  -g, --gamma arg            set gamma in kernel function (default: 1 / num_features)\n"
+    "  -r, --coef0 arg            set coef0 in kernel function (default: 0)\n"
+    "  -c, --cost arg             set the parameter C (default: 1)\n"
+    "  -e, --epsilon arg          set the tolerance of termination criterion (default: 0.001)\n"
+    "  -b, --backend arg          choose the backend: automatic|hip (default: automatic)\n"
+    "  -p, --target_platform arg  choose the target platform: automatic|gpu_amd (default: automatic)\n"
+    "  -q, --quiet                quiet mode (no outputs)\n"
+    "  -h, --help                 print this helper message\n"
+    "      --sparse               keep the data as CSR on the device (MI355X backend addition)\n"
+    "      --max_iter arg         maximum CG iterations (default: num_features)\n"
+    "      --single               train in single precision (float)\n"
+    "      --device arg           HIP device ordinal (default: 0)\n";
+
+struct cli {
+    std::map<std::string, std::string> opt;
+    std::vector<std::string> pos;
+};
+
+cli parse(int argc, char **argv) {
+    static const std::map<std::string, std::string> shorts = { { "t", "kernel_type" }, { "d", "degree" },
+                                                               { "g", "gamma" },       { "r", "coef0" },
+                                                               { "c", "cost" },        { "e", "epsilon" },
+                                                               { "b", "backend" },     { "p", "target_platform" },
+                                                               { "q", "quiet" },       { "h", "help" } };
+    static const std::map<std::string, bool> is_flag = { { "quiet", true }, { "help", true }, { "sparse", true },
+                                                        { "single", true } };
+    cli c;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        std::string key, val;
+        bool has_val = false;
+        if (a.rfind("--", 0) == 0) {
+            key = a.substr(2);
+            const auto eq = key.find('=');
+            if (eq != std::string::npos) {
+                val = key.substr(eq + 1);
+                key = key.substr(0, eq);
+                has_val = true;
+            }
+        } else if (a.size() >= 2 && a[0] == '-' && !(a[1] >= '0' && a[1] <= '9')) {
+            const auto it = shorts.find(a.substr(1, 1));
+            if (it == shorts.end()) throw std::invalid_argument("Option '" + a + "' does not exist");
+            key = it->second;
+            if (a.size() > 2) {
+                val = a.substr(2);
+                has_val = true;
+            }
+        } else {
+            c.pos.push_back(a);
+            continue;
+        }
+        if (is_flag.count(key)) {
+            c.opt[key] = "1";
+            continue;
+        }
+        if (!has_val) {
+            if (i + 1 >= argc) throw std::invalid_argument("Option '" + key + "' is missing an argument");
+            val = argv[++i];
+        }
+        c.opt[key] = val;
+    }
+    return c;
+}
+
+template <typename T>
+int train(const cli &c) {
+    using namespace plssvm::mi355x;
+    parameter<T> params;
+    if (c.opt.count("kernel_type")) params.kernel = parse_kernel(c.opt.at("kernel_type"));
+    if (c.opt.count("degree")) params.degree = std::stoi(c.opt.at("degree"));
+    if (c.opt.count("gamma")) {
+        params.gamma = to_real<T>(c.opt.at("gamma"));
+        if (params.gamma == T(0)) {
+            std::fprintf(stderr, "gamma = 0.0 is not allowed, it doesnt make any sense!\n");
+            std::printf("%s", kHelp);
+            return EXIT_FAILURE;
+        }
+    }
+    if (c.opt.count("coef0")) params.coef0 = to_real<T>(c.opt.at("coef0"));
+    if (c.opt.count("cost")) params.cost = to_real<T>(c.opt.at("cost"));
+    if (c.opt.count("epsilon")) params.epsilon = to_real<T>(c.opt.at("epsilon"));
+    const std::string backend = c.opt.count("backend") ? c.opt.at("backend") : "automatic";
+    if (backend != "automatic" && backend != "hip" && backend != "mi355x")
+        throw std::invalid_argument("Unavailable backend: '" + backend + "' (this build provides hip = MI355X)");
+    const std::string target = c.opt.count("target_platform") ? c.opt.at("target_platform") : "automatic";
+    if (target != "automatic" && target != "gpu_amd")
+        throw std::invalid_argument("Invalid target platform '" + target + "' for the HIP backend!");
+    params.print_info = !c.opt.count("quiet");
+    if (c.pos.empty()) {
+        std::fprintf(stderr, "Error missing input file!");
+        std::printf("%s", kHelp);
+        return EXIT_FAILURE;
+    }
+    params.input_filename = c.pos[0];
+    if (c.pos.size() > 1) params.model_filename = c.pos[1];
+    const auto t0 = std::chrono::steady_clock::now();
+    params.parse_train_file(c.pos[0], c.opt.count("sparse") > 0);
+    if (c.pos.size() > 1) params.model_filename = c.pos[1];
+    if (params.print_info) {
+        std::printf("Read %lld data points with %lld features in %lldms using the libsvm parser from file '%s'.\n\n",
+                    (long long) params.num_data_points, (long long) params.num_features,
+                    (long long) std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count(),
+                    params.input_filename.c_str());
+        std::printf("task: training\nkernel type: %s -> ", kernel_name(params.kernel));
+        switch (params.kernel) {
+            case kernel_type::linear: std::printf("u'*v\n"); break;
+            case kernel_type::polynomial:
+                std::printf("(gamma*u'*v + coef0)^degree\ngamma: %s\ncoef0: %s\ndegree: %d\n",
+                            csvm<T>::shortest(params.gamma).c_str(), csvm<T>::shortest(params.coef0).c_str(), params.degree);
+                break;
+            default: std::printf("exp(-gamma*|u-v|^2)\ngamma: %s\n", csvm<T>::shortest(params.gamma).c_str()); break;
+        }
+        std::printf("cost: %s\nepsilon: %s\ninput file (data set): '%s'\noutput file (model): '%s'\n\n",
+                    csvm<T>::shortest(params.cost).c_str(), csvm<T>::shortest(params.epsilon).c_str(),
+                    params.input_filename.c_str(), params.model_filename.c_str());
+        std::printf("Using HIP (MI355X, gfx950) as backend.\n\n");
+    }
+    const int device = c.opt.count("device") ? std::stoi(c.opt.at("device")) : 0;
+    csvm<T> svm(params, device);
+    const auto t1 = std::chrono::steady_clock::now();
+    svm.learn(c.opt.count("max_iter") ? std::stoll(c.opt.at("max_iter")) : -1);
+    const auto t2 = std::chrono::steady_clock::now();
+    if (params.print_info) {
+        std::printf("Solved minimization problem (r = b - Ax) using CG in %lldms (%lld iterations, residuum %s).\n",
+                    (long long) std::chrono::duration_cast<std::chrono::milliseconds>(t2 - t1).count(),
+                    (long long) svm.iterations(),
+                    csvm<T>::shortest((T) svm.residual_trace().back()).c_str());
+    }
+    svm.write_model(params.model_filename);
+    if (params.print_info) std::printf("Wrote model file ('%s').\n", params.model_filename.c_str());
+    return EXIT_SUCCESS;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    try {
+        const cli c = parse(argc, argv);
+        if (c.opt.count("help")) {
+            std::printf("%s", kHelp);
+            return EXIT_SUCCESS;
+        }
+        return c.opt.count("single") ? train<float>(c) : train<double>(c);
+    } catch (const std::exception &e) {
+        std::cerr << e.what() << std::endl;
+        return EXIT_FAILURE;
+    }
+}

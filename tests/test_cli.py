@@ -1,0 +1,49 @@
+"""plssvm-train (C++ host executable over the C ABI): the reference's CLI smoke test
+(`plssvm-train --help`, tests/CMakeLists.txt:115-116) on CPU, and the golden 5x4 model on the GPU."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, fixture_path
+
+EXE = os.path.join(ROOT, "plssvm_sparse_fp22_amd", "bin", "plssvm-train")
+
+
+def test_help():
+    out = subprocess.run([EXE, "--help"], capture_output=True, text=True, check=True).stdout
+    for flag in ("--kernel_type", "--degree", "--gamma", "--coef0", "--cost", "--epsilon", "--backend", "--quiet"):
+        assert flag in out
+
+
+def test_bad_backend_and_missing_input():
+    r = subprocess.run([EXE, "-b", "cuda", fixture_path("5x4.libsvm")], capture_output=True, text=True)
+    assert r.returncode != 0 and "backend" in r.stderr
+    r = subprocess.run([EXE], capture_output=True, text=True)
+    assert r.returncode != 0
+
+
+def read_model(path):
+    from plssvm_sparse_fp22_amd.io import parse_model
+
+    return parse_model(path)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--sparse"]])
+def test_train_reproduces_golden_model(tmp_path, extra):
+    out = tmp_path / "5x4.model"
+    subprocess.run([EXE, "-q", *extra, fixture_path("5x4.libsvm"), str(out)], check=True)
+    got, want = read_model(str(out)), read_model(fixture_path("5x4.libsvm.model"))
+    assert got["kernel"] == "linear" and got["nr_sv"] == [2, 3]
+    assert abs(got["rho"] - want["rho"]) <= 1e-9 * abs(want["rho"])
+    # same support vectors with the same alphas (the reference's order of negatives follows OpenMP threads)
+    key = lambda sv: tuple(np.round(sv, 5))
+    g = {key(sv): a for sv, a in zip(got["SV"], got["alpha"])}
+    w = {key(sv): a for sv, a in zip(want["SV"], want["alpha"])}
+    assert g.keys() == w.keys()
+    for k in w:
+        assert abs(g[k] - w[k]) <= 1e-9 * max(1.0, abs(w[k]))
+    head = open(out).read().splitlines()[:8]
+    assert head[0] == "svm_type c_svc" and head[1] == "kernel_type linear" and head[-1] == "SV"
