@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <numeric>
 
 #include "../../include/plssvm_mi355x.h"
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(256) void gram_gen_kernel(const int64_t *__restrict
         const T xi = val[k];
         for (int64_t t = c0 + threadIdx.x; t < c1; t += blockDim.x) {
             const uint64_t j = (uint64_t) crow[t];
-            constexpr uint64_t CW = gram_cw<T>();
+            constexpr uint64_t CW = GRAM_CW;
             keys[out + (t - c0)] = ((j / CW) << 32) | (il << 16) | (j % CW);
             vals[out + (t - c0)] = xi * cval[t];
         }
@@ -190,12 +191,18 @@ __device__ __forceinline__ void load8(const T *__restrict__ ps, int64_t e0, T (&
     }
 }
 
-// One 1024-thread workgroup per cell (2048 rows x CW-row window). The cell's pairs are one
+// One 1024-thread workgroup per cell (2048 rows x 4096-row window). The cell's pairs are one
 // contiguous, row-sorted stream cut into 8-pair chunks; each wave walks a contiguous range of
 // chunks (64 per step, lane = chunk), so a lane's row only moves forward and is tracked
 // incrementally. Per step and lane: 16 B of j + 32/64 B of s (prefetched one step ahead), the
-// window's n_j, e_j, p_j from LDS, mirrored column sums into an LDS accumulator (ds_add), row
-// partials reduced across lanes by a segmented shuffle scan and added by segment heads.
+// window's n_j, e_j, p_j from LDS, mirrored column sums into an LDS accumulator, row partials
+// reduced across lanes by a segmented shuffle scan and added by segment heads.
+//
+// Both LDS accumulators are int64 fixed point (ds_add_u64): LDS float atomics serialise on gfx950
+// (measured ~190 cycles per wave-wide ds_add_f32 vs ~10 for ds_add_u64), and integer sums are exact
+// and order-independent, so the kernel is bitwise reproducible. The quantum is a per-cell power of
+// two q = 2^e with cvmax * max|p| < 2^(e+50) (cvmax: setup-time bound on |c_ij|), so a sum of up to
+// 4096 terms stays below 2^62 and each term is rounded to 2^-51 of the cell's largest term.
 template <typename T, int KERNEL>
 __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restrict__ cells,
                                                        const int64_t *__restrict__ rb_base,
@@ -204,28 +211,52 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
                                                        const T *__restrict__ norms, const T *__restrict__ ev,
                                                        const T *__restrict__ p, T *__restrict__ slab_row,
                                                        T *__restrict__ slab_col, int64_t m, int64_t m_pad, kfun<T> kf,
-                                                       T kappa, const cg_scalars<T> *__restrict__ status,
+                                                       T kappa, T cvmax, const cg_scalars<T> *__restrict__ status,
                                                        int ablate) {
-    constexpr int CW = gram_cw<T>();
-    __shared__ T wn[CW], we[CW], wp[CW], colacc[CW];
-    __shared__ T rowacc[GRAM_RB];
+    constexpr int CW = GRAM_CW;
+    using acc_t = unsigned long long;
+    __shared__ T wn[CW], we[CW], wp[CW];
+    __shared__ acc_t colacc[CW];
+    __shared__ acc_t rowacc[GRAM_RB];
     __shared__ int32_t ro[GRAM_RB + 1];
+    __shared__ T wmax[16];
     if (status != nullptr && status->converged) return;
     const gram_cell cell = cells[xcd_remap(blockIdx.x, gridDim.x)];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t I0 = (int64_t) cell.I * GRAM_RB, W0 = (int64_t) cell.W * CW;
     const int rows = (int) min<int64_t>(GRAM_RB, m - I0);
     const int wlen = (int) min<int64_t>(CW, m - W0);
+    T pmax = 0;
     for (int t = tid; t < CW; t += 1024) {
         const bool ok = t < wlen;
         wn[t] = ok ? norms[W0 + t] : T(0);
         we[t] = (KERNEL == 2 && ok) ? ev[W0 + t] : T(0);
-        wp[t] = ok ? p[W0 + t] : T(0);
-        colacc[t] = T(0);
+        const T pv = ok ? p[W0 + t] : T(0);
+        wp[t] = pv;
+        pmax = max(pmax, fabs(pv));
+        colacc[t] = 0;
     }
-    for (int t = tid; t < GRAM_RB; t += 1024) rowacc[t] = T(0);
+    for (int t = tid; t < GRAM_RB; t += 1024) {
+        rowacc[t] = 0;
+        if (t < rows) pmax = max(pmax, fabs(p[I0 + t]));
+    }
     for (int t = tid; t <= rows; t += 1024) ro[t] = rowoff[cell.rowoff + t];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) pmax = max(pmax, __shfl_xor(pmax, o));
+    if (lane == 0) wmax[wave] = pmax;
     __syncthreads();
+    pmax = wmax[0];
+#pragma unroll
+    for (int w = 1; w < 16; ++w) pmax = max(pmax, wmax[w]);
+    // quantum 2^qe, clamped to the smallest normal (terms below it are denormal anyway)
+    constexpr int emin = sizeof(T) == 8 ? -1022 : -126;
+    const T bound = cvmax * pmax;
+    const int qe = bound > T(0) && isfinite(bound) ? max(emin, ilogb(bound) + 1 - 50) : emin;
+    const T inv_q = ldexp(T(1), -qe);
+    auto quant = [&](T v) -> acc_t {
+        if constexpr (sizeof(T) == 8) return (acc_t) __double2ll_rn(v * inv_q);
+        else return (acc_t) __float2ll_rn(v * inv_q);
+    };
 
     const int64_t base = rb_base[cell.I];
     const int64_t A = base + ro[0], B = base + ro[rows];
@@ -304,7 +335,7 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
                 const int64_t e = e0 + k;
                 if (e < A || e >= B) continue;
                 if (e >= rend) {
-                    if (acc != T(0)) atomicAdd(&rowacc[r], acc);
+                    if (acc != T(0)) atomicAdd(&rowacc[r], quant(acc));
                     acc = T(0);
                     seek(e);
                 }
@@ -322,16 +353,8 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
                     cv = s[k];
                 }
                 acc = fma(cv, gp[k], acc);
-                if (ablate & 1) {
-                    acc += cv * pi;  // timing-only ablation: no LDS column atomics
-                } else if (ablate & 4) {
-                    atomicAdd(reinterpret_cast<int *>(&colacc[jl[k]]), (int) (cv * pi * T(1e6)));
-                } else if (ablate & 8) {
-                    atomicAdd(reinterpret_cast<unsigned long long *>(&colacc[jl[k] & ~1]),
-                              (unsigned long long) (long long) (cv * pi * T(1e6)));
-                } else {
-                    atomicAdd(&colacc[jl[k]], cv * pi);
-                }
+                if (ablate & 1) acc += cv * pi;  // timing-only ablation: no LDS column atomics
+                else atomicAdd(&colacc[jl[k]], quant(cv * pi));
             }
             rl = r;
         }
@@ -344,11 +367,28 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
             if (lane + off < 64 && rr == rl) sacc += so;
         }
         const int rprev = __shfl_up(rl, 1);
-        if (rl >= 0 && (lane == 0 || rprev != rl)) atomicAdd(&rowacc[rl], sacc);
+        if (rl >= 0 && (lane == 0 || rprev != rl)) atomicAdd(&rowacc[rl], quant(sacc));
     }
     __syncthreads();
-    for (int t = tid; t < rows; t += 1024) slab_row[(int64_t) cell.W * m_pad + I0 + t] = rowacc[t];
-    for (int t = tid; t < wlen; t += 1024) slab_col[(int64_t) cell.I * m_pad + W0 + t] = colacc[t];
+    for (int t = tid; t < rows; t += 1024)
+        slab_row[(int64_t) cell.W * m_pad + I0 + t] = (T) ldexp((double) (long long) rowacc[t], qe);
+    for (int t = tid; t < wlen; t += 1024)
+        slab_col[(int64_t) cell.I * m_pad + W0 + t] = (T) ldexp((double) (long long) colacc[t], qe);
+}
+
+// max |s| over the stored pairs (bit patterns of non-negative floats order like unsigned integers)
+template <typename T>
+__global__ __launch_bounds__(256) void gram_smax_kernel(const T *__restrict__ ps, int64_t n,
+                                                        unsigned long long *__restrict__ out) {
+    T v = 0;
+    for (int64_t k = (int64_t) blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t) gridDim.x * 256)
+        v = max(v, fabs(ps[k]));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0) {
+        if constexpr (sizeof(T) == 8) atomicMax(out, (unsigned long long) __double_as_longlong(v));
+        else atomicMax(out, (unsigned long long) __float_as_uint(v));
+    }
 }
 
 template <typename T>
@@ -356,7 +396,7 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const T *__restrict__ 
                                                           const T *__restrict__ slab_col, int64_t m, int64_t m_pad,
                                                           int64_t rb0, int64_t rb1, T *__restrict__ raw,
                                                           const cg_scalars<T> *__restrict__ status) {
-    constexpr int64_t CW = gram_cw<T>();
+    constexpr int64_t CW = GRAM_CW;
     if (status != nullptr && status->converged) return;
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
@@ -398,7 +438,7 @@ __global__ __launch_bounds__(256) void gram_base_kernel(int kernel, kfun<T> kf, 
 }
 
 // timing-only ablation switch for profiling the Gram kernel (results are wrong when non-zero):
-// PLSSVM_MI_GRAM_ABLATE bit 0 = drop the LDS column atomics, bit 1 = drop the exp
+// PLSSVM_MI_GRAM_ABLATE bit 0 = drop the LDS column accumulation, bit 1 = drop the exp
 int gram_ablate() {
     static const int v = [] {
         const char *s = std::getenv("PLSSVM_MI_GRAM_ABLATE");
@@ -566,7 +606,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             return (int64_t) (std::lower_bound(cum.begin(), cum.end(), (cum[nRB] * r) / eff_world) - cum.begin());
         };
         csr.nRB = nRB;
-        csr.nW = ceil_div(std::max<int64_t>(m, 1), (int64_t) gram_cw<T>());
+        csr.nW = ceil_div(std::max<int64_t>(m, 1), (int64_t) GRAM_CW);
         csr.rb0 = std::min(split(eff_rank), nRB);
         csr.rb1 = std::max(csr.rb0, std::min(split(eff_rank + 1), nRB));
         csr.pair_bound = cum[csr.rb1] - cum[csr.rb0];
@@ -589,7 +629,7 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     std::vector<gram_cell> cells;
     std::vector<int64_t> rowoff_base(csr.nRB, 0);
     int64_t ro_total = 0;
-    const int64_t CW = gram_cw<T>();
+    const int64_t CW = GRAM_CW;
     for (int64_t I = csr.rb0; I < csr.rb1; ++I) {
         const int64_t nw = gram_nw(I, m, CW);
         rowoff_base[I] = ro_total;
@@ -687,7 +727,32 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     csr.pairs = pos;
     MI_HIP_CHECK(hipMemcpyAsync(csr.rb_base.get(), rb_base.data(), sizeof(int64_t) * (size_t) csr.nRB,
                                 hipMemcpyHostToDevice, stream));
+    // |c_ij| bound: rbf |k - e_i e_j| <= 1; poly |(g s + c0)^deg - c0^deg| <= (|g| smax + |c0|)^deg + |c0|^deg;
+    // linear |s| <= smax. Pad slots between row blocks hold zeros (never counted but harmless).
+    dev_buf<unsigned long long> smax_d;
+    smax_d.alloc(1, stream);
+    unsigned long long smax_bits = 0;
+    if (pos > 0) {
+        hipLaunchKernelGGL(gram_smax_kernel<T>, dim3((unsigned) std::min<int64_t>(ceil_div(pos, 256), 4096)), dim3(256),
+                           0, stream, csr.ps.get(), pos, smax_d.get());
+        MI_LAUNCH_CHECK();
+        MI_HIP_CHECK(hipMemcpyAsync(&smax_bits, smax_d.get(), sizeof smax_bits, hipMemcpyDeviceToHost, stream));
+    }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
+    T smax;
+    if constexpr (sizeof(T) == 8) std::memcpy(&smax, &smax_bits, 8);
+    else {
+        const uint32_t b32 = (uint32_t) smax_bits;
+        std::memcpy(&smax, &b32, 4);
+    }
+    if (kernel == 2) {
+        csr.cvmax = T(1);
+    } else if (kernel == 1) {
+        const double bse = std::fabs((double) gamma) * (double) smax + std::fabs((double) coef0);
+        csr.cvmax = (T) (std::pow(bse, degree) + std::pow(std::fabs((double) coef0), degree));
+    } else {
+        csr.cvmax = smax;
+    }
     csr.have_gram = true;
 }
 
@@ -758,17 +823,17 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
         case 0:
             hipLaunchKernelGGL((gram_kp_kernel<T, 0>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
                                csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
-                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status, gram_ablate());
+                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, csr.cvmax, status, gram_ablate());
             break;
         case 1:
             hipLaunchKernelGGL((gram_kp_kernel<T, 1>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
                                csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
-                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status, gram_ablate());
+                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, csr.cvmax, status, gram_ablate());
             break;
         default:
             hipLaunchKernelGGL((gram_kp_kernel<T, 2>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
                                csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
-                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status, gram_ablate());
+                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, csr.cvmax, status, gram_ablate());
             break;
     }
     MI_LAUNCH_CHECK();

@@ -55,10 +55,9 @@ struct vals_t {
 // a cell (I, W) holds, row by row (i ascending) then j ascending, every j in window W with
 // s_ij = x_i . x_j structurally non-zero (some shared feature), stored as (uint16 j - W*CW, s).
 constexpr int GRAM_RB = 2048;
-// window edge: the K·p kernel stages n_j, e_j, p_j of the window plus a column accumulator in LDS
-// (4 x 8192 x 4 B fp32 / 4 x 4096 x 8 B fp64 = 128 KiB) — one 1024-thread workgroup per CU
-template <typename T>
-constexpr int gram_cw() { return sizeof(T) == 8 ? 4096 : 8192; }
+// window edge: the K·p kernel stages n_j, e_j, p_j of the window plus int64 column and row
+// accumulators in LDS (fp64: 3 x 32 + 32 + 16 KiB + row offsets = 152 KiB; fp32: 96 KiB)
+constexpr int GRAM_CW = 4096;
 
 struct gram_cell {
     int32_t I, W;
@@ -83,6 +82,7 @@ struct csr_data {
     // Gram pattern
     bool have_gram = false;
     int64_t pairs = 0, pair_bound = 0;
+    T cvmax = 0;  // bound on |c_ij| over the stored pairs (fixed-point scale of the K·p accumulators)
     int64_t nRB = 0, nW = 0, rb0 = 0, rb1 = 0, m_pad = 0, ncells = 0;
     dev_buf<uint16_t> pj;
     dev_buf<T> ps;
