@@ -67,6 +67,9 @@ extern "C" {
  * share of the implicit matrix with no collective; the rank-1 Q~ terms are added by rank 0 only,
  * so the K·p results of all simulated ranks sum to the full K·p. */
 #define PLSSVM_MI_OPT_SIM_RANK 2
+/* RBF pair evaluation on sparse data: 0 = auto (factored e_i e_j (exp(2 g s) - 1) when g * max |x|^2
+ * keeps it in floating-point range), 1 = always direct exp(-g |x_i - x_j|^2) - e_i e_j. */
+#define PLSSVM_MI_OPT_RBF_FORM 3
 
 typedef struct plssvm_mi_ctx plssvm_mi_ctx;
 
@@ -155,6 +158,7 @@ typedef struct {
     int64_t device_bytes;
     int64_t pairs; /* sparse pairwise kernels: stored overlapping pairs (j < i) of this rank */
     int kp_mode, rank, world_size, real_bytes, kernel, is_sparse, val_fmt;
+    int rbf_factored; /* sparse rbf: 1 = factored pair form in use (PLSSVM_MI_OPT_RBF_FORM) */
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
 

@@ -96,7 +96,7 @@ class CSVM:
     """One MI355X context (one GPU, one HIP stream). ``world_size > 1`` joins a row-block group."""
 
     def __init__(self, params: Parameter, device=0, rank=0, world_size=1, uid=None, kp_mode="auto",
-                 sim_rank=None):
+                 sim_rank=None, rbf_form=0):
         if params.data is None and params.csr is None:
             raise ValueError("No data points provided!")
         if params.data is not None:
@@ -116,6 +116,8 @@ class CSVM:
         mode = {"auto": _abi.KP_AUTO, "pairwise": _abi.KP_PAIRWISE, "factored": _abi.KP_FACTORED}[kp_mode]
         if mode != _abi.KP_AUTO:
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_KP_MODE, mode))
+        if rbf_form:  # 1 = direct RBF pair form on sparse data, see PLSSVM_MI_OPT_RBF_FORM
+            self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_RBF_FORM, rbf_form))
         if sim_rank is not None:  # (rank, world): single-GPU test hook, see PLSSVM_MI_OPT_SIM_RANK
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_SIM_RANK, sim_rank[0] | (sim_rank[1] << 16)))
         if world_size > 1:

@@ -30,13 +30,14 @@ EXPORTS = (
     "plssvm_mi_time_kp", "plssvm_mi_get_info", "plssvm_mi_partition",
 )
 OPT_SIM_RANK = 2
+OPT_RBF_FORM = 3
 
 
 class Info(ctypes.Structure):
     _fields_ = [(k, ctypes.c_int64) for k in ("n", "d", "m", "n_pad", "d_pad", "nnz", "tiles_total", "tiles_local",
                                               "tile_rows", "tile_cols", "device_bytes", "pairs")] + \
                [(k, ctypes.c_int) for k in ("kp_mode", "rank", "world_size", "real_bytes", "kernel", "is_sparse",
-                                            "val_fmt")]
+                                            "val_fmt", "rbf_factored")]
 
 
 class BackendError(RuntimeError):

@@ -101,6 +101,8 @@ int plssvm_mi_set_option(plssvm_mi_ctx *ctx, int key, int64_t value) {
             if (w < 0 || (w > 0 && r >= w) || e.world > 1) throw mi_error(PLSSVM_MI_ERR_ARG, "bad simulated rank");
             e.sim_rank = r;
             e.sim_world = w;
+        } else if (key == PLSSVM_MI_OPT_RBF_FORM && value >= 0 && value <= 1) {
+            e.rbf_form = (int) value;
         } else {
             throw mi_error(PLSSVM_MI_ERR_ARG, "bad option");
         }
@@ -264,6 +266,7 @@ int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
         info->kernel = e.kernel;
         info->is_sparse = e.sparse ? 1 : 0;
         info->val_fmt = e.csr.val_fmt;
+        info->rbf_factored = e.csr.rbf_factored ? 1 : 0;
     });
 }
 

@@ -29,6 +29,7 @@ struct engine : engine_base {
     int device = 0;
     hipStream_t stream = nullptr;
     int kp_mode = 0;  // PLSSVM_MI_KP_*
+    int rbf_form = 0;  // PLSSVM_MI_OPT_RBF_FORM
 
     // ---- multi-GPU row-block group ----
     int rank = 0, world = 1;

@@ -195,14 +195,25 @@ __device__ __forceinline__ void load8(const T *__restrict__ ps, int64_t e0, T (&
 // contiguous, row-sorted stream cut into 8-pair chunks; each wave walks a contiguous range of
 // chunks (64 per step, lane = chunk), so a lane's row only moves forward and is tracked
 // incrementally. Per step and lane: 16 B of j + 32/64 B of s (prefetched one step ahead), the
-// window's n_j, e_j, p_j from LDS, mirrored column sums into an LDS accumulator, row partials
+// window's per-point factors from LDS, mirrored column sums into an LDS accumulator, row partials
 // reduced across lanes by a segmented shuffle scan and added by segment heads.
+//
+// KERNEL: 0 linear, 1 poly, 2 rbf (c_ij = exp(-g max(0, n_i + n_j - 2 s)) - e_i e_j), 3 rbf factored:
+// c_ij = e_i e_j (exp(2 g s) - 1), so the row sum is e_i sum_j g_ij (e_j p_j) and the column sum
+// e_j sum_i g_ij (e_i p_i): one staged factor (e_j p_j) per window point and no per-pair norm. Used
+// when g max(n) keeps e_i and exp(2 g s) inside the floating-point range (checked at setup).
 //
 // Both LDS accumulators are int64 fixed point (ds_add_u64): LDS float atomics serialise on gfx950
 // (measured ~190 cycles per wave-wide ds_add_f32 vs ~10 for ds_add_u64), and integer sums are exact
 // and order-independent, so the kernel is bitwise reproducible. The quantum is a per-cell power of
-// two q = 2^e with cvmax * max|p| < 2^(e+50) (cvmax: setup-time bound on |c_ij|), so a sum of up to
-// 4096 terms stays below 2^62 and each term is rounded to 2^-51 of the cell's largest term.
+// two q = 2^e with (bound on |term|) < 2^(e+50) — from the cell's max |s| (setup) and the max |p|
+// (or |e p|) over its rows and window — so a sum of up to 4096 terms stays below 2^62 and each term
+// is rounded to 2^-51 of the cell's largest possible term. A single term is rounded with the
+// 1.5*2^52 magic add in fp64 (exact for |x| < 2^51); row partials use the full fp64->int64 convert.
+__device__ __forceinline__ unsigned long long fx_round(double x) {
+    return (unsigned long long) (__double_as_longlong(x + 6755399441055744.0) - 0x4338000000000000LL);
+}
+
 template <typename T, int KERNEL>
 __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restrict__ cells,
                                                        const int64_t *__restrict__ rb_base,
@@ -211,11 +222,11 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
                                                        const T *__restrict__ norms, const T *__restrict__ ev,
                                                        const T *__restrict__ p, T *__restrict__ slab_row,
                                                        T *__restrict__ slab_col, int64_t m, int64_t m_pad, kfun<T> kf,
-                                                       T kappa, T cvmax, const cg_scalars<T> *__restrict__ status,
-                                                       int ablate) {
+                                                       T kappa, const cg_scalars<T> *__restrict__ status, int ablate) {
     constexpr int CW = GRAM_CW;
+    constexpr bool NEED_N = KERNEL == 2, NEED_E = KERNEL == 2;
     using acc_t = unsigned long long;
-    __shared__ T wn[CW], we[CW], wp[CW];
+    __shared__ T wn[NEED_N ? CW : 1], we[NEED_E ? CW : 1], wp[CW];
     __shared__ acc_t colacc[CW];
     __shared__ acc_t rowacc[GRAM_RB];
     __shared__ int32_t ro[GRAM_RB + 1];
@@ -226,19 +237,20 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
     const int64_t I0 = (int64_t) cell.I * GRAM_RB, W0 = (int64_t) cell.W * CW;
     const int rows = (int) min<int64_t>(GRAM_RB, m - I0);
     const int wlen = (int) min<int64_t>(CW, m - W0);
+    const T gamma = kf.gamma;
     T pmax = 0;
     for (int t = tid; t < CW; t += 1024) {
         const bool ok = t < wlen;
-        wn[t] = ok ? norms[W0 + t] : T(0);
-        we[t] = (KERNEL == 2 && ok) ? ev[W0 + t] : T(0);
-        const T pv = ok ? p[W0 + t] : T(0);
+        if (NEED_N) wn[t] = ok ? norms[W0 + t] : T(0);
+        if (NEED_E) we[t] = ok ? ev[W0 + t] : T(0);
+        const T pv = ok ? (KERNEL == 3 ? ev[W0 + t] * p[W0 + t] : p[W0 + t]) : T(0);
         wp[t] = pv;
         pmax = max(pmax, fabs(pv));
         colacc[t] = 0;
     }
     for (int t = tid; t < GRAM_RB; t += 1024) {
         rowacc[t] = 0;
-        if (t < rows) pmax = max(pmax, fabs(p[I0 + t]));
+        if (t < rows) pmax = max(pmax, fabs(KERNEL == 3 ? ev[I0 + t] * p[I0 + t] : p[I0 + t]));
     }
     for (int t = tid; t <= rows; t += 1024) ro[t] = rowoff[cell.rowoff + t];
 #pragma unroll
@@ -248,15 +260,28 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
     pmax = wmax[0];
 #pragma unroll
     for (int w = 1; w < 16; ++w) pmax = max(pmax, wmax[w]);
-    // quantum 2^qe, clamped to the smallest normal (terms below it are denormal anyway)
+    // bound on |c| (|g| for the factored rbf) over the cell's pairs
+    double cb;
+    if (KERNEL == 3) {
+        cb = expm1(2.0 * fabs((double) gamma) * cell.smax);
+    } else if (KERNEL == 2) {
+        cb = 1.0;
+    } else if (KERNEL == 1) {
+        const double bse = fabs((double) gamma) * cell.smax + fabs((double) kf.coef0);
+        double a = 1.0, b = 1.0;
+        for (int q = 0; q < kf.degree; ++q) a *= bse, b *= fabs((double) kf.coef0);
+        cb = a + b;
+    } else {
+        cb = cell.smax;
+    }
+    // quantum 2^qe, clamped to the smallest normal of T (terms below it are denormal anyway)
     constexpr int emin = sizeof(T) == 8 ? -1022 : -126;
-    const T bound = cvmax * pmax;
-    const int qe = bound > T(0) && isfinite(bound) ? max(emin, ilogb(bound) + 1 - 50) : emin;
-    const T inv_q = ldexp(T(1), -qe);
-    auto quant = [&](T v) -> acc_t {
-        if constexpr (sizeof(T) == 8) return (acc_t) __double2ll_rn(v * inv_q);
-        else return (acc_t) __float2ll_rn(v * inv_q);
-    };
+    const double bound = cb * (double) pmax * 1.0000001;
+    const int qe = bound > 0.0 && isfinite(bound) ? max(emin, ilogb(bound) + 1 - 50) : emin;
+    const double inv_q = ldexp(1.0, -qe);
+    // one pair's term (|x| < 2^50): magic-add rounding; row partials (up to 512 terms): full conversion
+    auto quant = [&](T v) -> acc_t { return fx_round((double) v * inv_q); };
+    auto quant_sum = [&](T v) -> acc_t { return (acc_t) __double2ll_rn((double) v * inv_q); };
 
     const int64_t base = rb_base[cell.I];
     const int64_t A = base + ro[0], B = base + ro[rows];
@@ -264,9 +289,8 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
     const int64_t per_wave = ((c1 - c0 + 15) / 16 + 63) / 64 * 64;
     const int64_t wbeg = c0 + wave * per_wave;
     const int64_t wend = min<int64_t>(c1, wbeg + per_wave);
-    const T gamma = kf.gamma;
 
-    // lane state: current row, its end (absolute pair index), its p / norm / e
+    // lane state: current row, its end (absolute pair index), its p (e p) / norm / e
     int r = 0;
     int64_t rend = 0;
     T pi = 0, ni = 0, ei = 0;
@@ -285,9 +309,13 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
                 r = lo;
             }
             rend = base + ro[r + 1];
-            pi = p[I0 + r];
-            ni = norms[I0 + r];
-            if (KERNEL == 2) ei = ev[I0 + r];
+            if (KERNEL == 3) {
+                pi = ev[I0 + r] * p[I0 + r];
+            } else {
+                pi = p[I0 + r];
+                if (NEED_N) ni = norms[I0 + r];
+                if (NEED_E) ei = ev[I0 + r];
+            }
         }
     };
 
@@ -298,6 +326,7 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
         load8<T>(ps, (wbeg + lane) << 3, s_n);
     }
     bool first = true;
+    const T g2 = T(2) * gamma;
     for (int64_t cb = wbeg; cb < wend; cb += 64) {  // wave-uniform trip count
         const int64_t c = cb + lane;
         const bool have = c < wend;
@@ -324,8 +353,8 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 jl[k] = (int) ((jw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
-                gn[k] = wn[jl[k]];
-                ge[k] = we[jl[k]];
+                if (NEED_N) gn[k] = wn[jl[k]];
+                if (NEED_E) ge[k] = we[jl[k]];
                 gp[k] = wp[jl[k]];
             }
             const int64_t ea = e0 > A ? e0 : A;
@@ -335,12 +364,14 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
                 const int64_t e = e0 + k;
                 if (e < A || e >= B) continue;
                 if (e >= rend) {
-                    if (acc != T(0)) atomicAdd(&rowacc[r], quant(acc));
+                    if (acc != T(0)) atomicAdd(&rowacc[r], quant_sum(acc));
                     acc = T(0);
                     seek(e);
                 }
                 T cv;
-                if (KERNEL == 2) {
+                if (KERNEL == 3) {
+                    cv = (ablate & 2) ? g2 * s[k] : exp(g2 * s[k]) - T(1);
+                } else if (KERNEL == 2) {
                     T dist = ni + gn[k] - T(2) * s[k];
                     dist = dist > T(0) ? dist : T(0);
                     cv = (ablate & 2) ? dist - ei * ge[k] : exp(-gamma * dist) - ei * ge[k];
@@ -353,7 +384,7 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
                     cv = s[k];
                 }
                 acc = fma(cv, gp[k], acc);
-                if (ablate & 1) acc += cv * pi;  // timing-only ablation: no LDS column atomics
+                if (ablate & 1) acc += cv * pi;  // timing-only ablation: no LDS column accumulation
                 else atomicAdd(&colacc[jl[k]], quant(cv * pi));
             }
             rl = r;
@@ -367,28 +398,54 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
             if (lane + off < 64 && rr == rl) sacc += so;
         }
         const int rprev = __shfl_up(rl, 1);
-        if (rl >= 0 && (lane == 0 || rprev != rl)) atomicAdd(&rowacc[rl], quant(sacc));
+        if (rl >= 0 && (lane == 0 || rprev != rl)) atomicAdd(&rowacc[rl], quant_sum(sacc));
     }
     __syncthreads();
-    for (int t = tid; t < rows; t += 1024)
-        slab_row[(int64_t) cell.W * m_pad + I0 + t] = (T) ldexp((double) (long long) rowacc[t], qe);
-    for (int t = tid; t < wlen; t += 1024)
-        slab_col[(int64_t) cell.I * m_pad + W0 + t] = (T) ldexp((double) (long long) colacc[t], qe);
+    for (int t = tid; t < rows; t += 1024) {
+        T v = (T) ldexp((double) (long long) rowacc[t], qe);
+        if (KERNEL == 3) v *= ev[I0 + t];
+        slab_row[(int64_t) cell.W * m_pad + I0 + t] = v;
+    }
+    for (int t = tid; t < wlen; t += 1024) {
+        T v = (T) ldexp((double) (long long) colacc[t], qe);
+        if (KERNEL == 3) v *= ev[W0 + t];
+        slab_col[(int64_t) cell.I * m_pad + W0 + t] = v;
+    }
 }
 
-// max |s| over the stored pairs (bit patterns of non-negative floats order like unsigned integers)
+// max |v| over an array (bit patterns of non-negative floats order like unsigned integers)
 template <typename T>
-__global__ __launch_bounds__(256) void gram_smax_kernel(const T *__restrict__ ps, int64_t n,
-                                                        unsigned long long *__restrict__ out) {
-    T v = 0;
+__global__ __launch_bounds__(256) void abs_max_kernel(const T *__restrict__ v, int64_t n,
+                                                      unsigned long long *__restrict__ out) {
+    T a = 0;
     for (int64_t k = (int64_t) blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t) gridDim.x * 256)
-        v = max(v, fabs(ps[k]));
+        a = max(a, fabs(v[k]));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) a = max(a, __shfl_xor(a, o));
+    if ((threadIdx.x & 63) == 0) {
+        if constexpr (sizeof(T) == 8) atomicMax(out, (unsigned long long) __double_as_longlong(a));
+        else atomicMax(out, (unsigned long long) __float_as_uint(a));
+    }
+}
+
+// per cell: max |s| over its pairs (the fixed-point bound of the K·p kernel)
+template <typename T>
+__global__ __launch_bounds__(256) void gram_cell_smax_kernel(gram_cell *__restrict__ cells,
+                                                             const int64_t *__restrict__ rb_base,
+                                                             const int32_t *__restrict__ rowoff,
+                                                             const T *__restrict__ ps, int64_t m) {
+    __shared__ T part[4];
+    gram_cell &cell = cells[blockIdx.x];
+    const int rows = (int) min<int64_t>(GRAM_RB, m - (int64_t) cell.I * GRAM_RB);
+    const int64_t base = rb_base[cell.I];
+    const int64_t a = base + rowoff[cell.rowoff], b = base + rowoff[cell.rowoff + rows];
+    T v = 0;
+    for (int64_t k = a + threadIdx.x; k < b; k += 256) v = max(v, fabs(ps[k]));
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
-    if ((threadIdx.x & 63) == 0) {
-        if constexpr (sizeof(T) == 8) atomicMax(out, (unsigned long long) __double_as_longlong(v));
-        else atomicMax(out, (unsigned long long) __float_as_uint(v));
-    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) cell.smax = (double) max(max(part[0], part[1]), max(part[2], part[3]));
 }
 
 template <typename T>
@@ -458,6 +515,26 @@ void host_check_csr(const int64_t *rowptr, const int32_t *col, int64_t n, int64_
             if (k > rowptr[i] && col[k] <= col[k - 1]) throw mi_error(-1, "CSR columns must be strictly ascending");
         }
     }
+}
+
+template <typename T>
+T abs_max(const T *v, int64_t n, hipStream_t stream) {
+    if (n <= 0) return T(0);
+    dev_buf<unsigned long long> out;
+    out.alloc(1, stream);
+    hipLaunchKernelGGL(abs_max_kernel<T>, dim3((unsigned) std::min<int64_t>(ceil_div(n, 256), 4096)), dim3(256), 0, stream,
+                       v, n, out.get());
+    MI_LAUNCH_CHECK();
+    unsigned long long bits = 0;
+    MI_HIP_CHECK(hipMemcpyAsync(&bits, out.get(), sizeof bits, hipMemcpyDeviceToHost, stream));
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    T r;
+    if constexpr (sizeof(T) == 8) std::memcpy(&r, &bits, 8);
+    else {
+        const uint32_t b32 = (uint32_t) bits;
+        std::memcpy(&r, &b32, 4);
+    }
+    return r;
 }
 
 }  // namespace
@@ -633,7 +710,7 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     for (int64_t I = csr.rb0; I < csr.rb1; ++I) {
         const int64_t nw = gram_nw(I, m, CW);
         rowoff_base[I] = ro_total;
-        for (int64_t W = 0; W < nw; ++W) cells.push_back(gram_cell{ (int32_t) I, (int32_t) W, ro_total + W * GRAM_RB });
+        for (int64_t W = 0; W < nw; ++W) cells.push_back(gram_cell{ (int32_t) I, (int32_t) W, ro_total + W * GRAM_RB, 0.0 });
         ro_total += nw * GRAM_RB + 1;
     }
     csr.ncells = (int64_t) cells.size();
@@ -727,32 +804,18 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     csr.pairs = pos;
     MI_HIP_CHECK(hipMemcpyAsync(csr.rb_base.get(), rb_base.data(), sizeof(int64_t) * (size_t) csr.nRB,
                                 hipMemcpyHostToDevice, stream));
-    // |c_ij| bound: rbf |k - e_i e_j| <= 1; poly |(g s + c0)^deg - c0^deg| <= (|g| smax + |c0|)^deg + |c0|^deg;
-    // linear |s| <= smax. Pad slots between row blocks hold zeros (never counted but harmless).
-    dev_buf<unsigned long long> smax_d;
-    smax_d.alloc(1, stream);
-    unsigned long long smax_bits = 0;
-    if (pos > 0) {
-        hipLaunchKernelGGL(gram_smax_kernel<T>, dim3((unsigned) std::min<int64_t>(ceil_div(pos, 256), 4096)), dim3(256),
-                           0, stream, csr.ps.get(), pos, smax_d.get());
+    if (csr.ncells > 0) {
+        hipLaunchKernelGGL(gram_cell_smax_kernel<T>, dim3((unsigned) csr.ncells), dim3(256), 0, stream, csr.cells.get(),
+                           csr.rb_base.get(), csr.rowoff.get(), csr.ps.get(), m);
         MI_LAUNCH_CHECK();
-        MI_HIP_CHECK(hipMemcpyAsync(&smax_bits, smax_d.get(), sizeof smax_bits, hipMemcpyDeviceToHost, stream));
+    }
+    // factored rbf when e_i = exp(-g n_i) and exp(2 g s_ij) <= exp(2 g max n) stay in range
+    csr.rbf_factored = false;
+    if (kernel == 2) {
+        const double gmax = std::fabs((double) gamma) * (double) abs_max(norms.get(), m, stream);
+        csr.rbf_factored = rbf_form != 1 && gmax <= (sizeof(T) == 8 ? 300.0 : 40.0);
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
-    T smax;
-    if constexpr (sizeof(T) == 8) std::memcpy(&smax, &smax_bits, 8);
-    else {
-        const uint32_t b32 = (uint32_t) smax_bits;
-        std::memcpy(&smax, &b32, 4);
-    }
-    if (kernel == 2) {
-        csr.cvmax = T(1);
-    } else if (kernel == 1) {
-        const double bse = std::fabs((double) gamma) * (double) smax + std::fabs((double) coef0);
-        csr.cvmax = (T) (std::pow(bse, degree) + std::pow(std::fabs((double) coef0), degree));
-    } else {
-        csr.cvmax = smax;
-    }
     csr.have_gram = true;
 }
 
@@ -819,23 +882,15 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
         for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
     }
     const dim3 grid((unsigned) csr.ncells), block(1024);
-    switch (kernel) {
-        case 0:
-            hipLaunchKernelGGL((gram_kp_kernel<T, 0>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
-                               csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
-                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, csr.cvmax, status, gram_ablate());
-            break;
-        case 1:
-            hipLaunchKernelGGL((gram_kp_kernel<T, 1>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
-                               csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
-                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, csr.cvmax, status, gram_ablate());
-            break;
-        default:
-            hipLaunchKernelGGL((gram_kp_kernel<T, 2>), grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(),
-                               csr.rowoff.get(), csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p,
-                               csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, kf(), kappa, csr.cvmax, status, gram_ablate());
-            break;
-    }
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(), csr.rowoff.get(),
+                           csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p, csr.slab_row.get(),
+                           csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status, gram_ablate());
+    };
+    if (kernel == 0) launch(gram_kp_kernel<T, 0>);
+    else if (kernel == 1) launch(gram_kp_kernel<T, 1>);
+    else if (csr.rbf_factored) launch(gram_kp_kernel<T, 3>);
+    else launch(gram_kp_kernel<T, 2>);
     MI_LAUNCH_CHECK();
 }
 

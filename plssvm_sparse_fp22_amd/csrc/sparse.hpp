@@ -62,6 +62,7 @@ constexpr int GRAM_CW = 4096;
 struct gram_cell {
     int32_t I, W;
     int64_t rowoff;  // index in rowoff[] of the cell's row 0 (rowoff holds GRAM_RB + 1 entries per cell)
+    double smax;     // max |s_ij| over the cell's pairs (fixed-point bound of the K·p accumulators)
 };
 
 template <typename T>
@@ -82,7 +83,7 @@ struct csr_data {
     // Gram pattern
     bool have_gram = false;
     int64_t pairs = 0, pair_bound = 0;
-    T cvmax = 0;  // bound on |c_ij| over the stored pairs (fixed-point scale of the K·p accumulators)
+    bool rbf_factored = false;  // rbf pairs as e_i e_j (exp(2 g s) - 1), see sparse.hip
     int64_t nRB = 0, nW = 0, rb0 = 0, rb1 = 0, m_pad = 0, ncells = 0;
     dev_buf<uint16_t> pj;
     dev_buf<T> ps;

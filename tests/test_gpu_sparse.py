@@ -17,6 +17,9 @@ TOL = {np.float64: 1e-12, np.float32: 1e-4}
 
 
 def sparse_svm(csr, kernel, dtype, fp22=False, mode="auto", sim=None, gamma=None, coef0=1.0, y=None, cost=1.0):
+    rbf_form = 0
+    if mode == "direct":  # rbf pairs as exp(-g |x_i - x_j|^2) - e_i e_j instead of the factored form
+        mode, rbf_form = "auto", 1
     rowptr, col, val, n, d = csr
     p = pm.Parameter(kernel, gamma=gamma if gamma is not None else 1.0 / d, coef0=coef0, real_type=dtype, cost=cost)
     if fp22:
@@ -27,7 +30,7 @@ def sparse_svm(csr, kernel, dtype, fp22=False, mode="auto", sim=None, gamma=None
     else:
         p.csr = (rowptr, col, val.astype(dtype), n, d)
     p.labels = y
-    return pm.CSVM(p, kp_mode=mode, sim_rank=sim)
+    return pm.CSVM(p, kp_mode=mode, sim_rank=sim, rbf_form=rbf_form)
 
 
 def oracle_data(oracle, csr, dtype, fp22=False):
@@ -37,12 +40,12 @@ def oracle_data(oracle, csr, dtype, fp22=False):
     return oracle.Data(rowptr=rowptr, col=col, val=val.astype(dtype), n=n, d=d, dtype=dtype)
 
 
-def check_sparse_kp(oracle, csr, kernel, dtype, fp22=False, mode="auto", coef0=1.0):
-    svm = sparse_svm(csr, kernel, dtype, fp22=fp22, mode=mode, coef0=coef0)
+def check_sparse_kp(oracle, csr, kernel, dtype, fp22=False, mode="auto", coef0=1.0, gamma=None):
+    svm = sparse_svm(csr, kernel, dtype, fp22=fp22, mode=mode, coef0=coef0, gamma=gamma)
     svm.setup_data_on_device()
     q = svm.generate_q()
     data = oracle_data(oracle, csr, dtype, fp22)
-    g = dtype(1.0 / csr[4])
+    g = dtype(gamma if gamma is not None else 1.0 / csr[4])
     q_ref = oracle.generate_q(kernel, data, gamma=g, coef0=dtype(coef0))
     np.testing.assert_allclose(q, q_ref, rtol=TOL[dtype], atol=TOL[dtype] * np.abs(q_ref).max())
     m = csr[3] - 1
@@ -60,13 +63,40 @@ def check_sparse_kp(oracle, csr, kernel, dtype, fp22=False, mode="auto", coef0=1
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("kernel,mode", [("linear", "auto"), ("linear", "pairwise"), ("polynomial", "auto"),
-                                         ("rbf", "auto")])
+                                         ("rbf", "auto"), ("rbf", "direct")])
 @pytest.mark.parametrize("shape", [(300, 500, 10), (2500, 3000, 20), (9000, 20000, 15)])
 def test_sparse_kp(oracle, kernel, mode, dtype, shape):
     n, d, k = shape
     csr, _ = datagen.sparse_csr(n, d, k, seed=n + d, dtype=dtype)
     info = check_sparse_kp(oracle, csr, kernel, dtype, mode=mode)
     assert info["is_sparse"] == 1
+    assert info["rbf_factored"] == (kernel == "rbf" and mode == "auto")
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_sparse_rbf_large_gamma_falls_back_to_direct(oracle, dtype):
+    """g max|x|^2 far outside the factored form's range (e_i underflows): auto must pick the direct form."""
+    csr, _ = datagen.sparse_csr(2500, 300, 20, seed=11, dtype=dtype)
+    info = check_sparse_kp(oracle, csr, "rbf", dtype, gamma=50.0)
+    assert info["rbf_factored"] == 0
+
+
+@pytest.mark.parametrize("kernel", ["rbf", "polynomial"])
+def test_sparse_gram_bitwise_reproducible(kernel):
+    """integer LDS accumulation: repeated K·p launches give identical bits"""
+    csr, _ = datagen.sparse_csr(9000, 2000, 30, seed=3, dtype=np.float32)
+    svm = sparse_svm(csr, kernel, np.float32)
+    svm.setup_data_on_device()
+    svm.generate_q()
+    m = csr[3] - 1
+    x = np.random.default_rng(1).standard_normal(m).astype(np.float32)
+    outs = []
+    for _ in range(3):
+        ret = np.zeros(m, dtype=np.float32)
+        svm.run_device_kernel(None, ret, x, 1.0)
+        outs.append(ret)
+    svm.close()
+    assert all(np.array_equal(outs[0], o) for o in outs[1:])
 
 
 @pytest.mark.parametrize("kernel", ["linear", "rbf", "polynomial"])
