@@ -200,10 +200,11 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
     vb = 2.75 if layout == "fp22" else es
     co = float((c * (c + 1) / 2).sum())
     alg = (co * (4 + vb) + col.size * (4 + vb) + 3 * m * es) / world
-    stream = info["pairs"] * (2 + es)
+    stream = info["pair_slots"] * (2 + es)  # stored slots (rows padded to 8 per cell)
     return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s", frac=alg / s / PEAKS["hbm"],
                 traffic=None, kernel="gram_kp_kernel", launch_ms=ms_dom, alg_bytes=alg,
-                stream_bytes_per_launch=stream, stream_GBps=stream / s / 1e9, pairs=info["pairs"])
+                stream_bytes_per_launch=stream, stream_GBps=stream / s / 1e9, pairs=info["pairs"],
+                pair_slots=info["pair_slots"])
 
 
 def cpu_baseline(kernel, dtype, d, m, budget_s, extra):

@@ -158,7 +158,8 @@ typedef struct {
     int64_t device_bytes;
     int64_t pairs; /* sparse pairwise kernels: stored overlapping pairs (j < i) of this rank */
     int kp_mode, rank, world_size, real_bytes, kernel, is_sparse, val_fmt;
-    int rbf_factored; /* sparse rbf: 1 = factored pair form in use (PLSSVM_MI_OPT_RBF_FORM) */
+    int rbf_factored;   /* sparse rbf: 1 = factored pair form in use (PLSSVM_MI_OPT_RBF_FORM) */
+    int64_t pair_slots; /* sparse pairwise kernels: stored pair slots incl. padding (K·p stream) */
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
 

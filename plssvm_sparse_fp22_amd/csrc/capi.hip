@@ -267,6 +267,7 @@ int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
         info->is_sparse = e.sparse ? 1 : 0;
         info->val_fmt = e.csr.val_fmt;
         info->rbf_factored = e.csr.rbf_factored ? 1 : 0;
+        info->pair_slots = e.csr.slots;
     });
 }
 

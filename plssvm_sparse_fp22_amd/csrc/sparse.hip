@@ -161,14 +161,27 @@ __global__ __launch_bounds__(256) void gram_rowcount_kernel(const uint64_t *__re
     atomicAdd(&rowcnt[(k >> 32) * GRAM_RB + ((k >> 16) & 0xFFFF)], 1);
 }
 
+// rows are padded to a multiple of 8 pairs per cell (pads: j = 0, s = 0), so an 8-pair chunk never
+// spans two rows; pair u of group g = (W, row) goes to padded[g] + (u - uoff[g])
+__global__ __launch_bounds__(256) void gram_pad_kernel(const int32_t *__restrict__ cnt, int64_t n,
+                                                       int32_t *__restrict__ cnt8) {
+    const int64_t g = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < n) cnt8[g] = (cnt[g] + 7) & ~7;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void gram_store_kernel(const uint64_t *__restrict__ ukeys,
                                                          const T *__restrict__ usum, const int64_t *__restrict__ nruns,
-                                                         uint16_t *__restrict__ pj, T *__restrict__ ps) {
+                                                         const int32_t *__restrict__ uoff,
+                                                         const int32_t *__restrict__ padded, uint16_t *__restrict__ pj,
+                                                         T *__restrict__ ps) {
     const int64_t u = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= *nruns) return;
-    pj[u] = (uint16_t) (ukeys[u] & 0xFFFF);
-    ps[u] = usum[u];
+    const uint64_t k = ukeys[u];
+    const int64_t g = (int64_t) (k >> 32) * GRAM_RB + (int64_t) ((k >> 16) & 0xFFFF);
+    const int64_t dst = (int64_t) padded[g] + (u - (int64_t) uoff[g]);
+    pj[dst] = (uint16_t) (k & 0xFFFF);
+    ps[dst] = usum[u];
 }
 
 // ---- Gram K·p ---------------------------------------------------------------------------------------------
@@ -191,7 +204,8 @@ __device__ __forceinline__ void load8(const T *__restrict__ ps, int64_t e0, T (&
     }
 }
 
-// One 1024-thread workgroup per cell (2048 rows x 4096-row window). The cell's pairs are one
+// One 512-thread workgroup per cell (2048 rows x 4096-row window), two resident per CU so one
+// cell's prologue/epilogue overlaps another's stream. The cell's pairs are one
 // contiguous, row-sorted stream cut into 8-pair chunks; each wave walks a contiguous range of
 // chunks (64 per step, lane = chunk), so a lane's row only moves forward and is tracked
 // incrementally. Per step and lane: 16 B of j + 32/64 B of s (prefetched one step ahead), the
@@ -210,12 +224,18 @@ __device__ __forceinline__ void load8(const T *__restrict__ ps, int64_t e0, T (&
 // (or |e p|) over its rows and window — so a sum of up to 4096 terms stays below 2^62 and each term
 // is rounded to 2^-51 of the cell's largest possible term. A single term is rounded with the
 // 1.5*2^52 magic add in fp64 (exact for |x| < 2^51); row partials use the full fp64->int64 convert.
+template <typename T>
+__device__ __forceinline__ T fast_exp2(T x) {
+    if constexpr (sizeof(T) == 4) return __builtin_amdgcn_exp2f(x);  // v_exp_f32
+    else return exp2(x);
+}
+
 __device__ __forceinline__ unsigned long long fx_round(double x) {
     return (unsigned long long) (__double_as_longlong(x + 6755399441055744.0) - 0x4338000000000000LL);
 }
 
 template <typename T, int KERNEL>
-__global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restrict__ cells,
+__global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__restrict__ cells,
                                                        const int64_t *__restrict__ rb_base,
                                                        const int32_t *__restrict__ rowoff,
                                                        const uint16_t *__restrict__ pj, const T *__restrict__ ps,
@@ -223,14 +243,14 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
                                                        const T *__restrict__ p, T *__restrict__ slab_row,
                                                        T *__restrict__ slab_col, int64_t m, int64_t m_pad, kfun<T> kf,
                                                        T kappa, const cg_scalars<T> *__restrict__ status, int ablate) {
-    constexpr int CW = GRAM_CW;
+    constexpr int CW = GRAM_CW, NWAVE = GRAM_WG / 64;
     constexpr bool NEED_N = KERNEL == 2, NEED_E = KERNEL == 2;
     using acc_t = unsigned long long;
     __shared__ T wn[NEED_N ? CW : 1], we[NEED_E ? CW : 1], wp[CW];
     __shared__ acc_t colacc[CW];
     __shared__ acc_t rowacc[GRAM_RB];
     __shared__ int32_t ro[GRAM_RB + 1];
-    __shared__ T wmax[16];
+    __shared__ T wmax[NWAVE];
     if (status != nullptr && status->converged) return;
     const gram_cell cell = cells[xcd_remap(blockIdx.x, gridDim.x)];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -239,7 +259,7 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
     const int wlen = (int) min<int64_t>(CW, m - W0);
     const T gamma = kf.gamma;
     T pmax = 0;
-    for (int t = tid; t < CW; t += 1024) {
+    for (int t = tid; t < CW; t += GRAM_WG) {
         const bool ok = t < wlen;
         if (NEED_N) wn[t] = ok ? norms[W0 + t] : T(0);
         if (NEED_E) we[t] = ok ? ev[W0 + t] : T(0);
@@ -248,18 +268,18 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
         pmax = max(pmax, fabs(pv));
         colacc[t] = 0;
     }
-    for (int t = tid; t < GRAM_RB; t += 1024) {
+    for (int t = tid; t < GRAM_RB; t += GRAM_WG) {
         rowacc[t] = 0;
         if (t < rows) pmax = max(pmax, fabs(KERNEL == 3 ? ev[I0 + t] * p[I0 + t] : p[I0 + t]));
     }
-    for (int t = tid; t <= rows; t += 1024) ro[t] = rowoff[cell.rowoff + t];
+    for (int t = tid; t <= rows; t += GRAM_WG) ro[t] = rowoff[cell.rowoff + t];
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) pmax = max(pmax, __shfl_xor(pmax, o));
     if (lane == 0) wmax[wave] = pmax;
     __syncthreads();
     pmax = wmax[0];
 #pragma unroll
-    for (int w = 1; w < 16; ++w) pmax = max(pmax, wmax[w]);
+    for (int w = 1; w < NWAVE; ++w) pmax = max(pmax, wmax[w]);
     // bound on |c| (|g| for the factored rbf) over the cell's pairs
     double cb;
     if (KERNEL == 3) {
@@ -283,41 +303,40 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
     auto quant = [&](T v) -> acc_t { return fx_round((double) v * inv_q); };
     auto quant_sum = [&](T v) -> acc_t { return (acc_t) __double2ll_rn((double) v * inv_q); };
 
-    const int64_t base = rb_base[cell.I];
-    const int64_t A = base + ro[0], B = base + ro[rows];
-    const int64_t c0 = A >> 3, c1 = (B + 7) >> 3;
-    const int64_t per_wave = ((c1 - c0 + 15) / 16 + 63) / 64 * 64;
+    const int64_t base = rb_base[cell.I];  // 8-aligned, and every row's pair count is padded to 8
+    const int64_t c0 = (base + ro[0]) >> 3, c1 = (base + ro[rows]) >> 3;
+    const int64_t per_wave = ((c1 - c0 + NWAVE - 1) / NWAVE + 63) / 64 * 64;
     const int64_t wbeg = c0 + wave * per_wave;
     const int64_t wend = min<int64_t>(c1, wbeg + per_wave);
 
     // lane state: current row, its end (absolute pair index), its p (e p) / norm / e
     int r = 0;
-    int64_t rend = 0;
+    int64_t rend = base + ro[0];
     T pi = 0, ni = 0, ei = 0;
-    auto seek = [&](int64_t e) {  // move r forward to the row containing pair e
+    auto seek = [&](int64_t e) {  // move r forward to the row containing pair e (rend <= e)
         const int32_t rel = (int32_t) (e - base);
-        if (rend <= e) {
-            int steps = 0;
-            while (steps < 8 && ro[r + 1] <= rel) ++r, ++steps;
-            if (ro[r + 1] <= rel) {  // long jump: binary search in [r, rows)
-                int lo = r, hi = rows;
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (ro[mid] <= rel) lo = mid;
-                    else hi = mid;
-                }
-                r = lo;
+        int steps = 0;
+        while (steps < 8 && ro[r + 1] <= rel) ++r, ++steps;
+        if (ro[r + 1] <= rel) {  // long jump: binary search in [r, rows)
+            int lo = r, hi = rows;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (ro[mid] <= rel) lo = mid;
+                else hi = mid;
             }
-            rend = base + ro[r + 1];
-            if (KERNEL == 3) {
-                pi = ev[I0 + r] * p[I0 + r];
-            } else {
-                pi = p[I0 + r];
-                if (NEED_N) ni = norms[I0 + r];
-                if (NEED_E) ei = ev[I0 + r];
-            }
+            r = lo;
+        }
+        rend = base + ro[r + 1];
+        if (KERNEL == 3) {
+            pi = ev[I0 + r] * p[I0 + r];
+        } else {
+            pi = p[I0 + r];
+            if (NEED_N) ni = norms[I0 + r];
+            if (NEED_E) ei = ev[I0 + r];
         }
     };
+    // exp(-g dist) = exp2(-g log2(e) dist); exp(2 g s) = exp2(2 g log2(e) s)
+    const T lg = gamma * T(1.4426950408889634);
 
     uint4 jv_n = make_uint4(0, 0, 0, 0);
     T s_n[8];
@@ -325,8 +344,6 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
         jv_n = *reinterpret_cast<const uint4 *>(pj + ((wbeg + lane) << 3));
         load8<T>(ps, (wbeg + lane) << 3, s_n);
     }
-    bool first = true;
-    const T g2 = T(2) * gamma;
     for (int64_t cb = wbeg; cb < wend; cb += 64) {  // wave-uniform trip count
         const int64_t c = cb + lane;
         const bool have = c < wend;
@@ -338,54 +355,34 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
             jv_n = *reinterpret_cast<const uint4 *>(pj + ((cb + 64 + lane) << 3));
             load8<T>(ps, (cb + 64 + lane) << 3, s_n);
         }
-        int rl = -1;  // row of this lane's last pair (for the cross-lane reduction)
+        int rl = -1;  // row of this lane's chunk (for the cross-lane reduction)
         T acc = 0;
         if (have) {
             const int64_t e0 = c << 3;
-            if (first) {
-                rend = 0;
-                r = 0;
-            }
-            first = false;
+            if (e0 >= rend) seek(e0);
             const uint32_t jw[4] = { jv.x, jv.y, jv.z, jv.w };
-            int jl[8];
-            T gn[8], ge[8], gp[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                jl[k] = (int) ((jw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
-                if (NEED_N) gn[k] = wn[jl[k]];
-                if (NEED_E) ge[k] = we[jl[k]];
-                gp[k] = wp[jl[k]];
-            }
-            const int64_t ea = e0 > A ? e0 : A;
-            seek(ea);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int64_t e = e0 + k;
-                if (e < A || e >= B) continue;
-                if (e >= rend) {
-                    if (acc != T(0)) atomicAdd(&rowacc[r], quant_sum(acc));
-                    acc = T(0);
-                    seek(e);
-                }
+                const int jl = (int) ((jw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
                 T cv;
                 if (KERNEL == 3) {
-                    cv = (ablate & 2) ? g2 * s[k] : exp(g2 * s[k]) - T(1);
+                    cv = (ablate & 2) ? lg * s[k] : fast_exp2(T(2) * lg * s[k]) - T(1);  // pads: s = 0 -> 0
                 } else if (KERNEL == 2) {
-                    T dist = ni + gn[k] - T(2) * s[k];
+                    T dist = ni + wn[jl] - T(2) * s[k];
                     dist = dist > T(0) ? dist : T(0);
-                    cv = (ablate & 2) ? dist - ei * ge[k] : exp(-gamma * dist) - ei * ge[k];
+                    cv = (ablate & 2) ? dist - ei * we[jl] : fast_exp2(-lg * dist) - ei * we[jl];
+                    cv = s[k] == T(0) ? T(0) : cv;  // pads (and exact-zero pairs, whose c is 0)
                 } else if (KERNEL == 1) {
                     const T bse = fma(gamma, s[k], kf.coef0);
                     T kv = T(1);
                     for (int q = 0; q < kf.degree; ++q) kv *= bse;
-                    cv = kv - kappa;
+                    cv = kv - kappa;  // pads: bse = c0 -> kv == kappa bitwise
                 } else {
                     cv = s[k];
                 }
-                acc = fma(cv, gp[k], acc);
+                acc = fma(cv, wp[jl], acc);
                 if (ablate & 1) acc += cv * pi;  // timing-only ablation: no LDS column accumulation
-                else atomicAdd(&colacc[jl[k]], quant(cv * pi));
+                else atomicAdd(&colacc[jl], quant(cv * pi));
             }
             rl = r;
         }
@@ -401,12 +398,12 @@ __global__ __launch_bounds__(1024) void gram_kp_kernel(const gram_cell *__restri
         if (rl >= 0 && (lane == 0 || rprev != rl)) atomicAdd(&rowacc[rl], quant_sum(sacc));
     }
     __syncthreads();
-    for (int t = tid; t < rows; t += 1024) {
+    for (int t = tid; t < rows; t += GRAM_WG) {
         T v = (T) ldexp((double) (long long) rowacc[t], qe);
         if (KERNEL == 3) v *= ev[I0 + t];
         slab_row[(int64_t) cell.W * m_pad + I0 + t] = v;
     }
-    for (int t = tid; t < wlen; t += 1024) {
+    for (int t = tid; t < wlen; t += GRAM_WG) {
         T v = (T) ldexp((double) (long long) colacc[t], qe);
         if (KERNEL == 3) v *= ev[W0 + t];
         slab_col[(int64_t) cell.I * m_pad + W0 + t] = v;
@@ -721,7 +718,11 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     csr.rowoff.alloc(std::max<int64_t>(ro_total, 1), stream);
     csr.rb_base.alloc(std::max<int64_t>(csr.nRB, 1), stream);
     // each row block's pairs start 8-aligned (the K·p kernel reads 8 pairs per lane with 16-byte loads)
-    const int64_t pcap = csr.pair_bound + 8 * (csr.rb1 - csr.rb0) + 16;
+    // unique pairs <= incidences (pair_bound); padding adds < 8 per non-empty (row, window) group
+    int64_t groups = 0;
+    for (int64_t I = csr.rb0; I < csr.rb1; ++I)
+        groups += (std::min<int64_t>(m, (I + 1) * GRAM_RB) - I * GRAM_RB) * gram_nw(I, m, CW);
+    const int64_t pcap = csr.pair_bound + 7 * std::min(csr.pair_bound, groups) + 16;
     csr.pj.alloc(pcap, stream);
     csr.ps.alloc(pcap, stream);
     csr.slab_row.alloc(std::max<int64_t>(csr.nW, 1) * csr.m_pad, stream);
@@ -733,7 +734,7 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     dev_buf<uint64_t> keys, keys_s;
     dev_buf<T> vals, vals_s;
     dev_buf<int64_t> cnt, off, nruns;
-    dev_buf<int32_t> rowcnt;
+    dev_buf<int32_t> rowcnt, uoff, cnt8;
     keys.alloc(cap, stream, false);
     keys_s.alloc(cap, stream, false);
     vals.alloc(cap, stream, false);
@@ -742,6 +743,8 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     off.alloc(GRAM_RB + 1, stream);
     nruns.alloc(1, stream);
     rowcnt.alloc(csr.nW * GRAM_RB + 1, stream);
+    uoff.alloc(csr.nW * GRAM_RB + 1, stream);
+    cnt8.alloc(csr.nW * GRAM_RB + 1, stream);
     size_t tmp_sort = 0, tmp_scan = 0, tmp_red = 0, tmp_scan32 = 0;
     MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, keys.get(), keys_s.get(), vals.get(),
                                                     vals_s.get(), (int) std::min<int64_t>(cap, INT32_MAX), 0, 64,
@@ -758,6 +761,7 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
 
     std::vector<int64_t> rb_base(csr.nRB, 0);
     int64_t pos = 0;
+    csr.pairs = 0;
     const int end_bit = 32 + std::max(1, (int) std::ceil(std::log2((double) csr.nW + 1.0)));
     for (int64_t I = csr.rb0; I < csr.rb1; ++I) {
         const int64_t i0 = I * GRAM_RB, i1 = std::min<int64_t>(m, i0 + GRAM_RB), rows = i1 - i0;
@@ -792,16 +796,30 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
             hipLaunchKernelGGL(gram_rowcount_kernel, dim3((unsigned) ceil_div(nu, 256)), dim3(256), 0, stream,
                                keys.get(), nruns.get(), rowcnt.get());
             MI_LAUNCH_CHECK();
+        }
+        const int ng = (int) (nw * GRAM_RB + 1);
+        int32_t *padded = csr.rowoff.get() + rowoff_base[I];
+        size_t t3s = tmp_scan32;
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.get(), t3s, rowcnt.get(), uoff.get(), ng, stream));
+        hipLaunchKernelGGL(gram_pad_kernel, dim3((unsigned) ceil_div(ng, 256)), dim3(256), 0, stream, rowcnt.get(),
+                           (int64_t) ng, cnt8.get());
+        MI_LAUNCH_CHECK();
+        t3s = tmp_scan32;
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.get(), t3s, cnt8.get(), padded, ng, stream));
+        int32_t slots = 0;
+        MI_HIP_CHECK(hipMemcpyAsync(&slots, padded + ng - 1, sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        if (slots < 0 || pos + slots > pcap) throw mi_error(-5, "Gram pattern exceeds its capacity bound");
+        if (nu > 0) {
             hipLaunchKernelGGL(gram_store_kernel<T>, dim3((unsigned) ceil_div(nu, 256)), dim3(256), 0, stream,
-                               keys.get(), vals.get(), nruns.get(), csr.pj.get() + pos, csr.ps.get() + pos);
+                               keys.get(), vals.get(), nruns.get(), uoff.get(), padded, csr.pj.get() + pos,
+                               csr.ps.get() + pos);
             MI_LAUNCH_CHECK();
         }
-        size_t t3s = tmp_scan32;
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.get(), t3s, rowcnt.get(), csr.rowoff.get() + rowoff_base[I],
-                                                      (int) (nw * GRAM_RB + 1), stream));
-        pos += nu;
+        csr.pairs += nu;
+        pos += slots;
     }
-    csr.pairs = pos;
+    csr.slots = pos;
     MI_HIP_CHECK(hipMemcpyAsync(csr.rb_base.get(), rb_base.data(), sizeof(int64_t) * (size_t) csr.nRB,
                                 hipMemcpyHostToDevice, stream));
     if (csr.ncells > 0) {
@@ -881,7 +899,7 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
         kappa = 1;
         for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
     }
-    const dim3 grid((unsigned) csr.ncells), block(1024);
+    const dim3 grid((unsigned) csr.ncells), block(GRAM_WG);
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(), csr.rowoff.get(),
                            csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p, csr.slab_row.get(),

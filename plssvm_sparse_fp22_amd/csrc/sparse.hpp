@@ -58,6 +58,7 @@ constexpr int GRAM_RB = 2048;
 // window edge: the K·p kernel stages n_j, e_j, p_j of the window plus int64 column and row
 // accumulators in LDS (fp64: 3 x 32 + 32 + 16 KiB + row offsets = 152 KiB; fp32: 96 KiB)
 constexpr int GRAM_CW = 4096;
+constexpr int GRAM_WG = 512;  // K·p workgroup size
 
 struct gram_cell {
     int32_t I, W;
@@ -82,7 +83,8 @@ struct csr_data {
 
     // Gram pattern
     bool have_gram = false;
-    int64_t pairs = 0, pair_bound = 0;
+    int64_t pairs = 0, pair_bound = 0;  // unique overlapping pairs; incidence bound
+    int64_t slots = 0;                   // stored pair slots (rows padded to 8 per cell)
     bool rbf_factored = false;  // rbf pairs as e_i e_j (exp(2 g s) - 1), see sparse.hip
     int64_t nRB = 0, nW = 0, rb0 = 0, rb1 = 0, m_pad = 0, ncells = 0;
     dev_buf<uint16_t> pj;
