@@ -139,6 +139,7 @@ def main():
     info = svm.info()
     ms_kp, ms_dom = svm.time_kp(args.kp_reps)
     roof = roofline(cfg, info, n, d, world, ms_dom, extra)
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(args.config, n, d, world, roof["kernel"])
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -205,6 +206,18 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
                 traffic=None, kernel="gram_kp_kernel", launch_ms=ms_dom, alg_bytes=alg,
                 stream_bytes_per_launch=stream, stream_GBps=stream / s / 1e9, pairs=info["pairs"],
                 pair_slots=info["pair_slots"])
+
+
+def pmc_traffic(config, n, d, world, kernel):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC pass of this exact
+    workload (profiles/*_<config>_traffic.json, written by tools/pmc_traffic.py), else None."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_traffic.json")), reverse=True):
+        t = json.load(open(path))
+        if t["N"] == n and t["d"] == d and t["n_gpus"] == world and kernel == t["kernel"]:
+            return t["hbm_read_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def cpu_baseline(kernel, dtype, d, m, budget_s, extra):
