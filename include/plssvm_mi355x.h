@@ -4,7 +4,7 @@
  * The reference exposes this path only as C++ virtuals of plssvm::csvm<T> /
  * plssvm::detail::gpu_csvm<T, device_ptr_t, queue_t>; every entry point below names the
  * reference member it replaces (paths relative to the reference repository root). The C++
- * adapter plssvm::mi355x::csvm<T> (plssvm_sparse_fp22_amd/csrc/csvm.hpp) maps those virtuals
+ * adapter plssvm::mi355x::csvm<T> (plssvm_sparse_fp22_amd/host/csvm.hpp) maps those virtuals
  * onto these calls; ctypes/cgo/JNI bindings can call them directly.
  *
  * Conventions
@@ -160,6 +160,8 @@ typedef struct {
     int kp_mode, rank, world_size, real_bytes, kernel, is_sparse, val_fmt;
     int rbf_factored;   /* sparse rbf: 1 = factored pair form in use (PLSSVM_MI_OPT_RBF_FORM) */
     int64_t pair_slots; /* sparse pairwise kernels: stored pair slots incl. padding (K·p stream) */
+    int64_t spmv_bytes; /* sparse factored linear: HBM bytes both SpMV passes move per K·p (padded SELL
+                           stream, slot maps, panel partials) */
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
 

@@ -92,6 +92,8 @@ struct engine : engine_base {
     void build_gram_blocks(const int64_t *cpos, int64_t max_inc);  // sparse Gram pattern (pairwise kernels)
     void sparse_kp_raw(const T *p, const cg_scalars<T> *status);  // raw[i] = sum_j k_ij p_j, i < m
     void sparse_dominant(const T *p, const cg_scalars<T> *status);  // the dominant sparse kernel
+    void spmv_pass_csc(const T *p, const cg_scalars<T> *status);    // factored linear: w = X^T p
+    void spmv_pass_csr(const cg_scalars<T> *status);                // factored linear: raw = X w
     int64_t csr_bytes() const { return csr.bytes(); }
 
     void allreduce(T *buf, int64_t count);

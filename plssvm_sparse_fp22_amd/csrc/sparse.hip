@@ -73,46 +73,6 @@ __global__ __launch_bounds__(256) void csr_q_kernel(kfun<T> kf, const int64_t *_
     }
 }
 
-// ---- factored linear ---------------------------------------------------------------------------------
-// w[f] = sum_{i in rows of this rank} x_if p_i : one wave per column (CSC)
-template <typename T>
-__global__ __launch_bounds__(256) void csc_gemv_kernel(const int64_t *__restrict__ lo, const int64_t *__restrict__ hi,
-                                                       const int32_t *__restrict__ crow, vals_t<T> cval, int64_t d,
-                                                       const T *__restrict__ p, T *__restrict__ w,
-                                                       const cg_scalars<T> *__restrict__ status) {
-    if (status != nullptr && status->converged) return;
-    const int64_t f = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (f >= d) return;
-    T s = 0;
-    const int64_t b = hi[f];
-    for (int64_t k = lo[f] + lane; k < b; k += 64) s = fma(cval[k], p[crow[k]], s);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
-    if (lane == 0) w[f] = s;
-}
-
-// raw[i] = sum_f x_if w_f for r0 <= i < r1 : 16 lanes per row
-template <typename T>
-__global__ __launch_bounds__(256) void csr_gemv_kernel(const int64_t *__restrict__ rowptr,
-                                                       const int32_t *__restrict__ col, vals_t<T> val, int64_t r0,
-                                                       int64_t r1, const T *__restrict__ w, T *__restrict__ raw,
-                                                       const cg_scalars<T> *__restrict__ status) {
-    if (status != nullptr && status->converged) return;
-    const int64_t row = r0 + (int64_t) blockIdx.x * 16 + (threadIdx.x >> 4);
-    const int sl = threadIdx.x & 15;
-    T s = 0;
-    if (row < r1) {
-        const int64_t b = rowptr[row + 1];
-        for (int64_t k = rowptr[row] + sl; k < b; k += 16) s = fma(val[k], w[col[k]], s);
-    }
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    s += __shfl_xor(s, 4);
-    s += __shfl_xor(s, 8);
-    if (row < r1 && sl == 0) raw[row] = s;
-}
-
 // ---- Gram pattern build ---------------------------------------------------------------------------------
 // incidences of row i: sum over its entries e of #{ j < i in column col[e] } = cpos[e] - colptr[col[e]]
 __global__ __launch_bounds__(256) void gram_count_kernel(const int64_t *__restrict__ rowptr,
@@ -583,8 +543,44 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         if (nnz) MI_HIP_CHECK(hipMemcpyAsync(csr.val.get(), val, sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice, stream));
     }
 
-    // CSC of rows 0..m-1 (counting sort: rows ascending inside each column) and, per CSR entry, its
-    // CSC position (the column-join needs "rows < i in this column" = cpos - colptr)
+    norms.alloc(std::max<int64_t>(n_pad, 1), stream);
+    csr.e.alloc(std::max<int64_t>(n_pad, 1), stream);
+    if (m > 0)
+        hipLaunchKernelGGL(csr_norms_kernel<T>, dim3((unsigned) ceil_div(m, 16)), dim3(256), 0, stream,
+                           csr.rowptr.get(), csr.rvals(), m, gamma, norms.get(), csr.e.get());
+    MI_LAUNCH_CHECK();
+    finish_setup();  // row split r0, r1
+
+    if (factored()) {
+        // factored linear: w = X_rows^T p over rows [csc_r0, csc_r1) — all rows for
+        // a single or simulated rank, this rank's rows in a real group (w is then all-reduced) — and
+        // raw[r0, r1) = X w, both as panelled SELL-64 SpMVs (spmv.hpp)
+        const bool local = world > 1 && sim_world == 0;
+        csr.csc_r0 = local ? r0 : 0;
+        csr.csc_r1 = local ? r1 : m;
+        const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
+        constexpr int64_t blocks = 512;  // two 1024-thread workgroups per CU
+        build_spmv_plan<T>(
+            csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22,
+            [&](auto emit) {
+                for (int64_t i = csr.csc_r0; i < csr.csc_r1; ++i)
+                    for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit((int64_t) col[k], i - csr.csc_r0, (double) hval(k));
+            },
+            blocks, stream);
+        build_spmv_plan<T>(
+            csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22,
+            [&](auto emit) {
+                for (int64_t i = r0; i < r1; ++i)
+                    for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit(i - r0, (int64_t) col[k], (double) hval(k));
+            },
+            blocks, stream);
+        return;
+    }
+
+    // CSC of rows 0..m-1 for the Gram pattern (counting sort: rows ascending inside each column) and,
+    // per CSR entry, its CSC position (the column join needs "rows < i in this column" = cpos - colptr)
+    csr.csc_r0 = 0;
+    csr.csc_r1 = m;
     std::vector<int64_t> colptr(d + 1, 0), cpos(std::max<int64_t>(nnz, 1));
     for (int64_t k = 0; k < nnz; ++k) ++colptr[col[k] + 1];
     for (int64_t f = 0; f < d; ++f) colptr[f + 1] += colptr[f];
@@ -617,9 +613,9 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             const int64_t g = t >> 4;
             const int bit = 22 * (int) (t & 15);
             const int64_t wi = g * 11 + (bit >> 5);
-            const int s = bit & 31;
-            w[wi] |= (uint32_t) (code << s);
-            if (s > 10) w[wi + 1] |= (uint32_t) (code >> (32 - s));
+            const int sh = bit & 31;
+            w[wi] |= (uint32_t) (code << sh);
+            if (sh > 10) w[wi + 1] |= (uint32_t) (code >> (32 - sh));
         }
         csr.cval22.alloc((int64_t) w.size(), stream);
         MI_HIP_CHECK(hipMemcpyAsync(csr.cval22.get(), w.data(), sizeof(uint32_t) * w.size(), hipMemcpyHostToDevice,
@@ -633,39 +629,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         MI_HIP_CHECK(hipStreamSynchronize(stream));
     }
 
-    norms.alloc(std::max<int64_t>(n_pad, 1), stream);
-    csr.e.alloc(std::max<int64_t>(n_pad, 1), stream);
-    if (m > 0)
-        hipLaunchKernelGGL(csr_norms_kernel<T>, dim3((unsigned) ceil_div(m, 16)), dim3(256), 0, stream,
-                           csr.rowptr.get(), csr.rvals(), m, gamma, norms.get(), csr.e.get());
-    MI_LAUNCH_CHECK();
-    finish_setup();
-
-    // per-column CSC range of this rank's rows (factored multi-rank); all rows in simulated mode
     {
-        std::vector<int64_t> lo(d), hi(d);
-        const bool all_rows = (world == 1) || sim_world > 0;
-        for (int64_t f = 0; f < d; ++f) {
-            if (all_rows) {
-                lo[f] = colptr[f];
-                hi[f] = colptr[f + 1];
-            } else {
-                lo[f] = std::lower_bound(crow.begin() + colptr[f], crow.begin() + colptr[f + 1], (int32_t) r0) -
-                        crow.begin();
-                hi[f] = std::lower_bound(crow.begin() + colptr[f], crow.begin() + colptr[f + 1], (int32_t) r1) -
-                        crow.begin();
-            }
-        }
-        csr.col_lo.alloc(d, stream);
-        csr.col_hi.alloc(d, stream);
-        MI_HIP_CHECK(hipMemcpyAsync(csr.col_lo.get(), lo.data(), sizeof(int64_t) * (size_t) d, hipMemcpyHostToDevice,
-                                    stream));
-        MI_HIP_CHECK(hipMemcpyAsync(csr.col_hi.get(), hi.data(), sizeof(int64_t) * (size_t) d, hipMemcpyHostToDevice,
-                                    stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-    }
-
-    if (!factored()) {
         // Gram pattern: row blocks owned by this rank, balanced by column-join incidences
         const int64_t nRB = ceil_div(std::max<int64_t>(m, 1), GRAM_RB);
         std::vector<int64_t> inc_rb(nRB, 0);
@@ -837,6 +801,17 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     csr.have_gram = true;
 }
 
+// factored linear passes: w = X_rows^T p, raw[r0..r1) = X w (panelled SELL SpMVs, spmv.hpp)
+template <typename T>
+void engine<T>::spmv_pass_csc(const T *p, const cg_scalars<T> *status) {
+    launch_panel_spmv<T>(csr.spmv_csc, p + csr.csc_r0, csr.csc_r1 - csr.csc_r0, w.get(), status, stream);
+}
+
+template <typename T>
+void engine<T>::spmv_pass_csr(const cg_scalars<T> *status) {
+    launch_panel_spmv<T>(csr.spmv_csr, w.get(), d, raw.get() + r0, status, stream);
+}
+
 template <typename T>
 void engine<T>::sparse_q() {
     if (m <= 0) return;
@@ -850,14 +825,9 @@ void engine<T>::sparse_q() {
 template <typename T>
 void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status) {
     if (factored()) {
-        hipLaunchKernelGGL(csc_gemv_kernel<T>, dim3((unsigned) ceil_div(d, 4)), dim3(256), 0, stream,
-                           csr.col_lo.get(), csr.col_hi.get(), csr.crow.get(), csr.cvals(), d, p, w.get(), status);
-        MI_LAUNCH_CHECK();
+        spmv_pass_csc(p, status);
         allreduce(w.get(), d);
-        if (r1 > r0)
-            hipLaunchKernelGGL(csr_gemv_kernel<T>, dim3((unsigned) ceil_div(r1 - r0, 16)), dim3(256), 0, stream,
-                               csr.rowptr.get(), csr.col.get(), csr.rvals(), r0, r1, w.get(), raw.get(), status);
-        MI_LAUNCH_CHECK();
+        spmv_pass_csr(status);
         allgather_rows(raw.get());
         return;
     }
@@ -884,13 +854,8 @@ void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status) {
 template <typename T>
 void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
     if (factored()) {  // both SpMV passes (the factored K·p without its collectives)
-        hipLaunchKernelGGL(csc_gemv_kernel<T>, dim3((unsigned) ceil_div(d, 4)), dim3(256), 0, stream,
-                           csr.col_lo.get(), csr.col_hi.get(), csr.crow.get(), csr.cvals(), d, p, w.get(), status);
-        MI_LAUNCH_CHECK();
-        if (r1 > r0)
-            hipLaunchKernelGGL(csr_gemv_kernel<T>, dim3((unsigned) ceil_div(r1 - r0, 16)), dim3(256), 0, stream,
-                               csr.rowptr.get(), csr.col.get(), csr.rvals(), r0, r1, w.get(), raw.get(), status);
-        MI_LAUNCH_CHECK();
+        spmv_pass_csc(p, status);
+        spmv_pass_csr(status);
         return;
     }
     if (csr.ncells == 0) return;
@@ -917,7 +882,9 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
     template void engine<T>::build_gram_blocks(const int64_t *, int64_t);                                     \
     template void engine<T>::sparse_q();                                                                      \
     template void engine<T>::sparse_kp_raw(const T *, const cg_scalars<T> *);                                 \
-    template void engine<T>::sparse_dominant(const T *, const cg_scalars<T> *);
+    template void engine<T>::sparse_dominant(const T *, const cg_scalars<T> *);                               \
+    template void engine<T>::spmv_pass_csc(const T *, const cg_scalars<T> *);                                 \
+    template void engine<T>::spmv_pass_csr(const cg_scalars<T> *);
 INST(float)
 INST(double)
 #undef INST

@@ -5,50 +5,11 @@
 #pragma once
 
 #include "buffer.hpp"
+#include "fp22.hpp"
 #include "kernels.hpp"
+#include "spmv.hpp"
 
 namespace plssvm_mi {
-
-// ---- packed FP22: binary32 truncated to its top 22 bits (RNE), 16 values per 11 uint32 words ----
-__host__ __device__ inline float fp22_decode(uint32_t code) {
-    union {
-        uint32_t u;
-        float f;
-    } v;
-    v.u = (code & 0x3FFFFFu) << 10;
-    return v.f;
-}
-
-inline uint32_t fp22_encode_host(float x) {
-    union {
-        float f;
-        uint32_t u;
-    } v;
-    v.f = x;
-    const uint32_t u = v.u;
-    if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x007FFFFFu)) return ((u >> 10) | 0x1000u) & 0x3FFFFFu;
-    return ((u + 0x1FFu + ((u >> 10) & 1u)) >> 10) & 0x3FFFFFu;
-}
-
-inline int64_t fp22_words(int64_t n) { return ((n + 15) / 16) * 11; }
-
-__host__ __device__ inline float fp22_get(const uint32_t *words, int64_t e) {
-    const int64_t g = e >> 4;
-    const int bit = 22 * (int) (e & 15);
-    const uint32_t *w = words + g * 11 + (bit >> 5);
-    const int s = bit & 31;
-    uint64_t x = (uint64_t) w[0] >> s;
-    if (s > 10) x |= (uint64_t) w[1] << (32 - s);
-    return fp22_decode((uint32_t) x);
-}
-
-// value accessor: real array or packed FP22 words
-template <typename T>
-struct vals_t {
-    const T *v;
-    const uint32_t *v22;
-    __device__ __forceinline__ T operator[](int64_t e) const { return v22 ? (T) fp22_get(v22, e) : v[e]; }
-};
 
 // ---- sparse Gram pattern (pairwise kernels on sparse data), see DESIGN.md §4 ------------------------
 // rows are grouped in row blocks of GRAM_RB rows, candidate partners j < i in windows of GRAM_CW rows;
@@ -78,7 +39,10 @@ struct csr_data {
     dev_buf<int32_t> crow;
     dev_buf<T> cval;
     dev_buf<uint32_t> cval22;
-    dev_buf<int64_t> col_lo, col_hi;  // per column: CSC range of this rank's rows (factored multi-rank)
+    // factored linear: w = X_rows^T p (rows [csc_r0, csc_r1): all rows for one / simulated ranks,
+    // this rank's rows in a real group) and raw[r0, r1) = X w, both as panelled SELL SpMVs
+    int64_t csc_r0 = 0, csc_r1 = 0;
+    spmv_plan<T> spmv_csc, spmv_csr;
     dev_buf<T> e;                     // rbf separable factor exp(-gamma n_i)
 
     // Gram pattern
@@ -100,7 +64,7 @@ struct csr_data {
     vals_t<T> cvals() const { return vals_t<T>{ cval.get(), cval22.get() }; }
     int64_t bytes() const {
         return rowptr.bytes() + col.bytes() + val.bytes() + val22.bytes() + colptr.bytes() + crow.bytes() +
-               cval.bytes() + cval22.bytes() + col_lo.bytes() + col_hi.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
+               cval.bytes() + cval22.bytes() + spmv_csc.bytes() + spmv_csr.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
                rb_base.bytes() + rowoff.bytes() + cells.bytes() + slab_row.bytes() + slab_col.bytes();
     }
 };

@@ -1,0 +1,329 @@
+// Panelled SELL-64-σ SpMV for the factored sparse-linear K·p.
+//
+//   out[s] = sum_{entries e of segment s} val[e] * x[index(e)]
+//
+// used twice per K·p: CSC pass w = X^T p (segments = columns, gathered vector = p) and CSR pass
+// raw = X w (segments = rows, gathered vector = w).
+//
+// Why this layout (measured, tools/spmv_microbench.hip, config 3 = 1M x 50k @ 50 nnz/row, fp32):
+//  * a dword gather from global memory costs about one cache-line request per lane: a CSR-vector
+//    kernel gathering w / p from global memory runs at 1.2-1.5 TB/s whatever the stream layout, so
+//    the gathered vector is cut into panels of W elements (64 KiB) held in LDS. The matrix is stored
+//    panel-major and every entry carries a 16-bit panel-local index (6 B per fp32 entry, not 8);
+//  * segments of a panel are dealt to lanes: 64 segments form a chunk whose entries are stored
+//    lane-interleaved (entry j of the chunk's slot l at chunk_off + 64 j + l), so every load of a
+//    wave is one contiguous, coalesced 128 / 256 B line and each lane accumulates its own segment
+//    in a register, in entry order — no product buffer, no segment reduction, no atomics.
+//    Chunks are padded to their longest segment with (index 0, value 0) entries; segments are
+//    sorted by length (descending, stable) inside windows of SELL_SIGMA segments so that padding
+//    stays small and a chunk's output stays inside one window (slot -> segment map `perm`);
+//  * a workgroup takes a contiguous chunk range of one panel, loads the panel of x into LDS once,
+//    and its 16 waves walk the chunks; panel results are partial sums partial[q][s], reduced in
+//    panel order (deterministic).
+// When the panels would cost more than the stream (P * nseg > nnz / 2: very wide, very sparse
+// matrices) the plan uses one panel with 32-bit global indices gathered from global memory.
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+#include <vector>
+
+#include "buffer.hpp"
+#include "fp22.hpp"
+#include "kernels.hpp"
+
+namespace plssvm_mi {
+
+constexpr int SELL_NT = 1024;  // 16 waves per workgroup
+constexpr int SELL_WAVES = SELL_NT / 64;
+constexpr int SELL_XBYTES = 65536;  // LDS panel of the gathered vector
+constexpr int SELL_SIGMA = 4096;    // sorting window (segments)
+#ifndef PLSSVM_MI_SELL_UNROLL
+#define PLSSVM_MI_SELL_UNROLL 8
+#endif
+constexpr int SELL_UNROLL = PLSSVM_MI_SELL_UNROLL;  // entries per lane in flight per step
+template <typename T>
+constexpr int sell_width() { return SELL_XBYTES / (int) sizeof(T); }
+
+struct sell_chunk {
+    int64_t off;    // first entry (entry j of slot l at off + 64 j + l)
+    int32_t width;  // entries per slot (longest segment of the chunk)
+    int32_t q;      // panel
+};
+
+template <bool LDSX>
+struct sell_idx {
+    using type = int32_t;
+};
+template <>
+struct sell_idx<true> {
+    using type = uint16_t;
+};
+
+template <typename T>
+struct spmv_plan {
+    bool ldsx = false;
+    int64_t P = 0, nseg = 0, W = 0, nnz = 0, slots_total = 0, entries = 0, nchunks = 0, nblocks = 0;
+    dev_buf<sell_chunk> chunks;
+    dev_buf<int32_t> perm;    // [nchunks * 64] slot -> segment (-1: padding slot)
+    dev_buf<uint16_t> idx16;  // ldsx: panel-local index
+    dev_buf<int32_t> idx32;   // !ldsx: global index
+    dev_buf<T> val;
+    dev_buf<uint32_t> val22;
+    dev_buf<int32_t> bchunk;  // [nblocks + 1]: chunk range of block b (all of one panel)
+    dev_buf<T> partial;       // [P][nseg] (P > 1)
+
+    vals_t<T> vals() const { return vals_t<T>{ val.get(), val22.get() }; }
+    int64_t bytes() const {
+        return chunks.bytes() + perm.bytes() + idx16.bytes() + idx32.bytes() + val.bytes() + val22.bytes() +
+               bchunk.bytes() + partial.bytes();
+    }
+    // bytes one pass moves through HBM: padded index/value stream, slot map, partial slab write + read
+    int64_t stream_bytes() const {
+        const int64_t vb = val22.get() ? fp22_words(entries) * 4 : entries * (int64_t) sizeof(T);
+        return entries * (ldsx ? 2 : 4) + vb + perm.bytes() + chunks.bytes() + (P > 1 ? 2 * partial.bytes() : 0);
+    }
+};
+
+// FP22: both words are loaded unconditionally (the packed array carries one word of padding)
+template <typename T, bool F22>
+__device__ __forceinline__ T sell_val(const vals_t<T> &val, int64_t k) {
+    if constexpr (F22) {
+        const int64_t g = k >> 4;
+        const int bit = 22 * (int) (k & 15);
+        const uint32_t *w = val.v22 + g * 11 + (bit >> 5);
+        const int sh = bit & 31;
+        const uint64_t lo = __builtin_nontemporal_load(w), hi = __builtin_nontemporal_load(w + 1);
+        return (T) fp22_decode((uint32_t) (((hi << 32) | lo) >> sh));
+    } else {
+        return __builtin_nontemporal_load(val.v + k);
+    }
+}
+
+template <typename T, bool LDSX, bool F22>
+__global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__restrict__ chunks,
+                                                            const int32_t *__restrict__ perm,
+                                                            const typename sell_idx<LDSX>::type *__restrict__ idx,
+                                                            vals_t<T> val, const int32_t *__restrict__ bchunk,
+                                                            const T *__restrict__ x, int64_t xn, int64_t W,
+                                                            int64_t nseg, T *__restrict__ out,
+                                                            const cg_scalars<T> *__restrict__ status) {
+    constexpr int XW = LDSX ? sell_width<T>() : 1;
+    __shared__ T xs[XW];
+    if (status != nullptr && status->converged) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int c0 = bchunk[blockIdx.x], c1 = bchunk[blockIdx.x + 1];
+    if (c0 >= c1) return;
+    const int q = chunks[c0].q;
+    T *o = out + (int64_t) q * nseg;
+    const T *xg = x + (int64_t) q * W;  // LDSX: panel q gathers x[q W + local]; otherwise W = 0
+    if constexpr (LDSX) {
+        const int xl = (int) min((int64_t) W, xn - (int64_t) q * W);
+        constexpr int XPER = XW / SELL_NT;
+        T t[XPER];
+#pragma unroll
+        for (int u = 0; u < XPER; ++u) {
+            const int k = tid + u * SELL_NT;
+            t[u] = k < xl ? xg[k] : T(0);
+        }
+#pragma unroll
+        for (int u = 0; u < XPER; ++u) xs[tid + u * SELL_NT] = t[u];
+        __syncthreads();
+    }
+    auto gx = [&](int c) -> T {
+        if constexpr (LDSX) return xs[c];
+        else return xg[c];
+    };
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int c = c0 + wave; c < c1; c += SELL_WAVES) {
+        const sell_chunk ch = chunks[c];
+        const int slot_seg = perm[(int64_t) c * 64 + lane];
+        const int64_t base = ch.off + lane;
+        // steps of SELL_UNROLL entries; a step past the width re-reads the slot's last entry (same
+        // cache line) and masks it, so every step issues all of its loads at once
+        const int last = max(ch.width - 1, 0);
+        T acc = 0;
+        for (int j = 0; j < ch.width; j += SELL_UNROLL) {
+            typename sell_idx<LDSX>::type ci[SELL_UNROLL];
+            T vi[SELL_UNROLL];
+#pragma unroll
+            for (int u = 0; u < SELL_UNROLL; ++u) {
+                const int64_t k = base + (int64_t) min(j + u, last) * 64;
+                ci[u] = __builtin_nontemporal_load(idx + k);
+                vi[u] = sell_val<T, F22>(val, k);
+            }
+#pragma unroll
+            for (int u = 0; u < SELL_UNROLL; ++u) {
+                const T v = j + u < ch.width ? vi[u] : T(0);
+                acc = fma(v, gx((int) ci[u]), acc);
+            }
+        }
+        if (slot_seg >= 0) o[slot_seg] = acc;
+    }
+}
+
+// out[s] = sum_q partial[q][s] in panel order
+template <typename T>
+__global__ __launch_bounds__(256) void panel_reduce_kernel(const T *__restrict__ partial, int64_t P, int64_t nseg,
+                                                           T *__restrict__ out, const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    const int64_t s = (int64_t) blockIdx.x * 256 + threadIdx.x;
+    if (s >= nseg) return;
+    T a = 0;
+    for (int64_t q = 0; q < P; ++q) a += partial[q * nseg + s];
+    out[s] = a;
+}
+
+// out[0..nseg) = the pass result (partial slabs + reduction when P > 1)
+template <typename T>
+inline void launch_panel_spmv(const spmv_plan<T> &pl, const T *x, int64_t xn, T *out, const cg_scalars<T> *status,
+                              hipStream_t stream) {
+    if (pl.nseg <= 0 || pl.nblocks <= 0) return;
+    T *dst = pl.P > 1 ? pl.partial.get() : out;
+    const bool f22 = pl.val22.get() != nullptr;
+    const dim3 grid((unsigned) pl.nblocks), block(SELL_NT);
+    if (pl.ldsx) {
+        auto k = f22 ? sell_spmv_kernel<T, true, true> : sell_spmv_kernel<T, true, false>;
+        hipLaunchKernelGGL(k, grid, block, 0, stream, pl.chunks.get(), pl.perm.get(), pl.idx16.get(), pl.vals(),
+                           pl.bchunk.get(), x, xn, pl.W, pl.nseg, dst, status);
+    } else {
+        auto k = f22 ? sell_spmv_kernel<T, false, true> : sell_spmv_kernel<T, false, false>;
+        hipLaunchKernelGGL(k, grid, block, 0, stream, pl.chunks.get(), pl.perm.get(), pl.idx32.get(), pl.vals(),
+                           pl.bchunk.get(), x, xn, (int64_t) 0, pl.nseg, dst, status);
+    }
+    MI_LAUNCH_CHECK();
+    if (pl.P > 1) {
+        hipLaunchKernelGGL(panel_reduce_kernel<T>, dim3((unsigned) ceil_div(pl.nseg, 256)), dim3(256), 0, stream,
+                           pl.partial.get(), pl.P, pl.nseg, out, status);
+        MI_LAUNCH_CHECK();
+    }
+}
+
+// Host construction. gen(emit) must call emit(s, global_index, value) for every entry, the entries
+// of one segment in their summation order (for each panel). xn = length of the gathered vector.
+// target_blocks: workgroups per pass (each loads its panel of x once). force_mode: 0 auto,
+// 1 LDS panels, 2 one panel gathered from global memory.
+template <typename T, typename Gen>
+void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bool fp22, Gen gen, int64_t target_blocks,
+                     hipStream_t stream, int force_mode = 0) {
+    pl = spmv_plan<T>{};
+    pl.nseg = nseg;
+    pl.nnz = nnz;
+    if (nseg <= 0) return;
+    const int64_t Wmax = sell_width<T>();
+    const int64_t P_lds = std::max<int64_t>(1, ceil_div(std::max<int64_t>(xn, 1), Wmax));
+    bool ldsx = P_lds * (nseg + 1) * 2 <= std::max<int64_t>(nnz, 1);
+    if (force_mode == 1) ldsx = true;
+    if (force_mode == 2) ldsx = false;
+    pl.ldsx = ldsx;
+    pl.P = ldsx ? P_lds : 1;
+    pl.W = ldsx ? Wmax : std::max<int64_t>(xn, 1);
+    const int64_t P = pl.P, W = pl.W;
+    // segment lengths per panel
+    std::vector<int32_t> len((size_t) (P * nseg), 0);
+    gen([&](int64_t s, int64_t g, double) { ++len[(size_t) ((g / W) * nseg + s)]; });
+    // per panel: sort windows by length (descending, stable), deal 64 slots per chunk
+    const int64_t slots_per_panel = round_up(nseg, 64);
+    const int64_t nch_per_panel = slots_per_panel / 64;
+    std::vector<sell_chunk> chunks((size_t) (P * nch_per_panel));
+    std::vector<int32_t> perm((size_t) (P * slots_per_panel), -1);
+    std::vector<int64_t> pos((size_t) (P * nseg));  // next storage position of segment (q, s)
+    std::vector<int32_t> order;
+    int64_t off = 0;
+    for (int64_t q = 0; q < P; ++q) {
+        const int32_t *lq = len.data() + q * nseg;
+        for (int64_t w0 = 0; w0 < nseg; w0 += SELL_SIGMA) {
+            const int64_t w1 = std::min(nseg, w0 + (int64_t) SELL_SIGMA);
+            order.resize((size_t) (w1 - w0));
+            std::iota(order.begin(), order.end(), (int32_t) w0);
+            std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return lq[a] > lq[b]; });
+            // the slots of this window are [w0, w1) (SELL_SIGMA is a multiple of 64)
+            for (int64_t k = 0; k < (int64_t) order.size(); ++k) perm[(size_t) (q * slots_per_panel + w0 + k)] = order[k];
+        }
+        for (int64_t c = 0; c < nch_per_panel; ++c) {
+            int32_t width = 0;
+            for (int l = 0; l < 64; ++l) {
+                const int32_t sgm = perm[(size_t) (q * slots_per_panel + c * 64 + l)];
+                if (sgm >= 0) width = std::max(width, lq[sgm]);
+            }
+            chunks[(size_t) (q * nch_per_panel + c)] = sell_chunk{ off, width, (int32_t) q };
+            for (int l = 0; l < 64; ++l) {
+                const int32_t sgm = perm[(size_t) (q * slots_per_panel + c * 64 + l)];
+                if (sgm >= 0) pos[(size_t) (q * nseg + sgm)] = off + l;
+            }
+            off += (int64_t) width * 64;
+        }
+    }
+    pl.entries = off;
+    pl.nchunks = (int64_t) chunks.size();
+    pl.slots_total = P * slots_per_panel;
+    // fill (zero padding: index 0, value 0 contributes exactly 0) plus a 64-entry zero tail
+    const int64_t cap = off + 64;
+    std::vector<uint16_t> i16(ldsx ? cap : 0, 0);
+    std::vector<int32_t> i32(ldsx ? 0 : cap, 0);
+    std::vector<T> vr(fp22 ? 0 : cap, T(0));
+    std::vector<uint32_t> v22(fp22 ? fp22_words(cap) + 1 : 0, 0u);
+    gen([&](int64_t s, int64_t g, double v) {
+        const int64_t q = g / W;
+        int64_t &p = pos[(size_t) (q * nseg + s)];
+        const int64_t t = p;
+        p += 64;
+        if (ldsx) i16[t] = (uint16_t) (g - q * W);
+        else i32[t] = (int32_t) g;
+        if (fp22) {
+            const uint64_t code = fp22_encode_host((float) v);
+            const int64_t gg = t >> 4;
+            const int bit = 22 * (int) (t & 15);
+            const int64_t wi = gg * 11 + (bit >> 5);
+            const int sh = bit & 31;
+            v22[wi] |= (uint32_t) (code << sh);
+            if (sh > 10) v22[wi + 1] |= (uint32_t) (code >> (32 - sh));
+        } else {
+            vr[t] = (T) v;
+        }
+    });
+    // blocks: ~target_blocks, each a contiguous chunk range of one panel, balanced by cost
+    // (entries + a per-chunk charge for its descriptor, slot map and output)
+    constexpr int64_t CHUNK_COST = 8 * 64;
+    auto cost = [&](const sell_chunk &c) { return (int64_t) c.width * 64 + CHUNK_COST; };
+    int64_t total_cost = 0;
+    for (const auto &c : chunks) total_cost += cost(c);
+    std::vector<int32_t> bchunk{ 0 };
+    for (int64_t q = 0; q < P; ++q) {
+        const int64_t i0 = q * nch_per_panel, i1 = i0 + nch_per_panel;
+        if (i1 == i0) continue;
+        int64_t cq = 0;
+        for (int64_t i = i0; i < i1; ++i) cq += cost(chunks[(size_t) i]);
+        int64_t nbq = std::max<int64_t>(1, (int64_t) std::llround((double) target_blocks * (double) cq /
+                                                                  (double) std::max<int64_t>(total_cost, 1)));
+        nbq = std::min(nbq, i1 - i0);
+        int64_t acc = 0, k = 1;
+        for (int64_t i = i0; i < i1; ++i) {
+            acc += cost(chunks[(size_t) i]);
+            if (i + 1 < i1 && k < nbq && acc * nbq >= k * cq) {
+                bchunk.push_back((int32_t) (i + 1));
+                ++k;
+            }
+        }
+        bchunk.push_back((int32_t) i1);
+    }
+    pl.nblocks = (int64_t) bchunk.size() - 1;
+    auto up = [&](auto &buf, const auto &vec) {
+        using E = typename std::decay_t<decltype(vec)>::value_type;
+        if (vec.empty()) return;
+        buf.alloc((int64_t) vec.size(), stream, false);
+        MI_HIP_CHECK(hipMemcpyAsync(buf.get(), vec.data(), sizeof(E) * vec.size(), hipMemcpyHostToDevice, stream));
+    };
+    up(pl.chunks, chunks);
+    up(pl.perm, perm);
+    up(pl.idx16, i16);
+    up(pl.idx32, i32);
+    up(pl.val, vr);
+    up(pl.val22, v22);
+    up(pl.bchunk, bchunk);
+    if (P > 1) pl.partial.alloc(P * nseg, stream, false);
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+}  // namespace plssvm_mi
