@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--config", default="dense_rbf_100k", choices=sorted(CONFIGS))
     ap.add_argument("--n", type=int, default=0, help="override number of points")
     ap.add_argument("--d", type=int, default=0, help="override number of features")
+    ap.add_argument("--kernel", choices=["linear", "polynomial", "rbf"], default=None,
+                    help="override the configuration's kernel function (ablations)")
     ap.add_argument("--kp-reps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -106,6 +108,8 @@ def main():
         uid = box[0]
 
     cfg = CONFIGS[args.config]
+    if args.kernel:
+        cfg = (args.kernel,) + tuple(cfg[1:])
     kernel, _, _, dtype, layout, _, desc = cfg
     p, n, d, y, extra = make_problem(cfg, args.n, args.d, rank)
     svm = pm.CSVM(p, device=local_rank, rank=rank, world_size=world, uid=uid)
@@ -183,7 +187,7 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
         pk = PEAKS["f64" if dtype == np.float64 else "f32"]
         return dict(bound="mfma", achieved=alg / s / 1e12, peak=pk / 1e12, unit="TFLOP/s", frac=alg / s / pk,
                     traffic=None, kernel="kp_tile_kernel", launch_ms=ms_dom, alg_flop_per_launch=alg,
-                    alg_flop_per_kp_survey=3.0 * d * m * (m + 1) / 2)
+                    alg_flop_per_kp_survey=(3.0 if kernel == "rbf" else 2.0) * d * m * (m + 1) / 2)
     es = np.dtype(dtype).itemsize
     if info["kp_mode"] == pm._abi.KP_FACTORED:
         if layout == "dense":
