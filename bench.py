@@ -91,6 +91,9 @@ def main():
                     help="override the configuration's kernel function (ablations)")
     ap.add_argument("--kp-reps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--sim-rank", default=None, metavar="R/W",
+                    help="one GPU computes rank R's share of a W-GPU job (no collective): measures one rank of a "
+                         "multi-GPU configuration that does not fit one GPU (e.g. configs[4])")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -112,7 +115,13 @@ def main():
         cfg = (args.kernel,) + tuple(cfg[1:])
     kernel, _, _, dtype, layout, _, desc = cfg
     p, n, d, y, extra = make_problem(cfg, args.n, args.d, rank)
-    svm = pm.CSVM(p, device=local_rank, rank=rank, world_size=world, uid=uid)
+    sim = None
+    if args.sim_rank:
+        if world > 1:
+            raise SystemExit("--sim-rank is a single-process option")
+        sim = tuple(int(v) for v in args.sim_rank.split("/"))
+    svm = pm.CSVM(p, device=local_rank, rank=rank, world_size=world, uid=uid, sim_rank=sim)
+    share = sim[1] if sim else world  # the work split divides the implicit matrix by this
     t0 = time.time()
     svm.setup_data_on_device()
     t_setup = time.time() - t0
@@ -142,8 +151,9 @@ def main():
 
     info = svm.info()
     ms_kp, ms_dom = svm.time_kp(args.kp_reps)
-    roof = roofline(cfg, info, n, d, world, ms_dom, extra)
-    roof["traffic"], roof["traffic_source"] = pmc_traffic(args.config, n, d, world, roof["kernel"])
+    roof = roofline(cfg, info, n, d, share, ms_dom, extra)
+    tkey = args.config + (f"_sim{sim[0]}of{sim[1]}" if sim else "")
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(tkey, n, d, world, roof["kernel"])
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -171,6 +181,10 @@ def main():
             "cpu_baseline": cpu,
             "kp_ms": ms_kp,
         }
+        if sim:
+            out["config"]["simulated_rank"] = f"{sim[0]}/{sim[1]}"
+            out["config"]["parallelism"] = (f"one MI355X computing rank {sim[0]}'s share of a {sim[1]}-GPU job "
+                                            "(no collective); value = CG iterations/s of that share")
         print(json.dumps(out), flush=True)
     svm.close()
     if dist is not None:

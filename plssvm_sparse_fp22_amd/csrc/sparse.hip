@@ -532,17 +532,18 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                                 stream));
     csr.col.alloc(std::max<int64_t>(nnz, 1), stream);
     if (nnz) MI_HIP_CHECK(hipMemcpyAsync(csr.col.get(), col, sizeof(int32_t) * (size_t) nnz, hipMemcpyHostToDevice, stream));
-    if (val_fmt == PLSSVM_MI_VAL_FP22) {
-        const int64_t nw = fp22_words(std::max<int64_t>(nnz, 1));
-        csr.val22.alloc(nw + 1, stream);
-        if (nnz)
-            MI_HIP_CHECK(hipMemcpyAsync(csr.val22.get(), val, sizeof(uint32_t) * (size_t) fp22_words(nnz),
-                                        hipMemcpyHostToDevice, stream));
-    } else {
-        csr.val.alloc(std::max<int64_t>(nnz, 1), stream);
-        if (nnz) MI_HIP_CHECK(hipMemcpyAsync(csr.val.get(), val, sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice, stream));
+    // device CSR values in the context's real type: q, norms and the Gram-pattern build read them at
+    // setup only (the Gram K·p streams the products s_ij); packed FP22 input is decoded here once and
+    // stays packed only where the K·p streams feature values (the factored-linear SELL stream)
+    csr.val.alloc(std::max<int64_t>(nnz, 1), stream);
+    if (nnz && val_fmt == PLSSVM_MI_VAL_FP22) {
+        std::vector<T> dec((size_t) nnz);
+        for (int64_t k = 0; k < nnz; ++k) dec[(size_t) k] = hval(k);
+        MI_HIP_CHECK(hipMemcpyAsync(csr.val.get(), dec.data(), sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+    } else if (nnz) {
+        MI_HIP_CHECK(hipMemcpyAsync(csr.val.get(), val, sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice, stream));
     }
-
     norms.alloc(std::max<int64_t>(n_pad, 1), stream);
     csr.e.alloc(std::max<int64_t>(n_pad, 1), stream);
     if (m > 0)
@@ -586,17 +587,15 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     for (int64_t f = 0; f < d; ++f) colptr[f + 1] += colptr[f];
     std::vector<int64_t> fill(colptr.begin(), colptr.end() - 1);
     std::vector<int32_t> crow(std::max<int64_t>(nnz, 1));
-    std::vector<T> cval_real;
-    std::vector<float> cval_f;
-    if (val_fmt == PLSSVM_MI_VAL_FP22) cval_f.resize(std::max<int64_t>(nnz, 1));
-    else cval_real.resize(std::max<int64_t>(nnz, 1));
+    // values in CSC order, decoded (FP22 input included: the Gram build multiplies them once at setup,
+    // the K·p stream holds the products s_ij, so FP22 changes only the input format)
+    std::vector<T> cval_real(std::max<int64_t>(nnz, 1));
     for (int64_t i = 0; i < m; ++i) {
         for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
             const int64_t t = fill[col[k]]++;
             crow[t] = (int32_t) i;
             cpos[k] = t;
-            if (val_fmt == PLSSVM_MI_VAL_FP22) cval_f[t] = (float) hval(k);
-            else cval_real[t] = hval(k);
+            cval_real[t] = hval(k);
         }
     }
     csr.colptr.alloc(d + 1, stream);
@@ -606,28 +605,11 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     if (nnz)
         MI_HIP_CHECK(hipMemcpyAsync(csr.crow.get(), crow.data(), sizeof(int32_t) * (size_t) nnz, hipMemcpyHostToDevice,
                                     stream));
-    if (val_fmt == PLSSVM_MI_VAL_FP22) {
-        std::vector<uint32_t> w(fp22_words(std::max<int64_t>(nnz, 1)) + 1, 0u);
-        for (int64_t t = 0; t < nnz; ++t) {  // re-pack in CSC order (decode(encode(decoded)) is exact)
-            const uint64_t code = fp22_encode_host(cval_f[t]);
-            const int64_t g = t >> 4;
-            const int bit = 22 * (int) (t & 15);
-            const int64_t wi = g * 11 + (bit >> 5);
-            const int sh = bit & 31;
-            w[wi] |= (uint32_t) (code << sh);
-            if (sh > 10) w[wi + 1] |= (uint32_t) (code >> (32 - sh));
-        }
-        csr.cval22.alloc((int64_t) w.size(), stream);
-        MI_HIP_CHECK(hipMemcpyAsync(csr.cval22.get(), w.data(), sizeof(uint32_t) * w.size(), hipMemcpyHostToDevice,
+    csr.cval.alloc(std::max<int64_t>(nnz, 1), stream);
+    if (nnz)
+        MI_HIP_CHECK(hipMemcpyAsync(csr.cval.get(), cval_real.data(), sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice,
                                     stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-    } else {
-        csr.cval.alloc(std::max<int64_t>(nnz, 1), stream);
-        if (nnz)
-            MI_HIP_CHECK(hipMemcpyAsync(csr.cval.get(), cval_real.data(), sizeof(T) * (size_t) nnz,
-                                        hipMemcpyHostToDevice, stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-    }
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
 
     {
         // Gram pattern: row blocks owned by this rank, balanced by column-join incidences

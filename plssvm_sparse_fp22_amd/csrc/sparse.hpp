@@ -33,12 +33,10 @@ struct csr_data {
     int val_fmt = 0;  // PLSSVM_MI_VAL_REAL | PLSSVM_MI_VAL_FP22
     dev_buf<int64_t> rowptr;
     dev_buf<int32_t> col;
-    dev_buf<T> val;
-    dev_buf<uint32_t> val22;
+    dev_buf<T> val;  // decoded values (setup-time kernels: q, norms, Gram build)
     dev_buf<int64_t> colptr;  // CSC of rows 0..m-1
     dev_buf<int32_t> crow;
-    dev_buf<T> cval;
-    dev_buf<uint32_t> cval22;
+    dev_buf<T> cval;  // CSC values (decoded; Gram pattern build only)
     // factored linear: w = X_rows^T p (rows [csc_r0, csc_r1): all rows for one / simulated ranks,
     // this rank's rows in a real group) and raw[r0, r1) = X w, both as panelled SELL SpMVs
     int64_t csc_r0 = 0, csc_r1 = 0;
@@ -60,11 +58,11 @@ struct csr_data {
     dev_buf<T> slab_col;  // [nRB][m_pad]
     dev_buf<T> ssc;       // device scalars: [0] = sum(e p) or sum(p)
 
-    vals_t<T> rvals() const { return vals_t<T>{ val.get(), val22.get() }; }
-    vals_t<T> cvals() const { return vals_t<T>{ cval.get(), cval22.get() }; }
+    vals_t<T> rvals() const { return vals_t<T>{ val.get(), nullptr }; }
+    vals_t<T> cvals() const { return vals_t<T>{ cval.get(), nullptr }; }
     int64_t bytes() const {
-        return rowptr.bytes() + col.bytes() + val.bytes() + val22.bytes() + colptr.bytes() + crow.bytes() +
-               cval.bytes() + cval22.bytes() + spmv_csc.bytes() + spmv_csr.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
+        return rowptr.bytes() + col.bytes() + val.bytes() + colptr.bytes() + crow.bytes() +
+               cval.bytes() + spmv_csc.bytes() + spmv_csr.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
                rb_base.bytes() + rowoff.bytes() + cells.bytes() + slab_row.bytes() + slab_col.bytes();
     }
 };

@@ -154,3 +154,28 @@ def test_sparse_learn_matches_oracle(oracle, kernel):
     n = min(len(svm.trace), len(ref["trace"]), 6)
     np.testing.assert_allclose(svm.trace[:n], ref["trace"][:n], rtol=1e-6)
     np.testing.assert_allclose(svm.alpha, ref["alpha"], rtol=1e-6, atol=1e-6 * np.abs(ref["alpha"]).max())
+
+
+@pytest.mark.parametrize("kernel,mode", [("rbf", "auto"), ("rbf", "direct"), ("polynomial", "auto"),
+                                         ("linear", "pairwise"), ("linear", "auto")])
+def test_sparse_fp22_equals_decoded_input(kernel, mode):
+    """FP22 input == the same matrix given as decoded fp32, bit for bit, at a size with several Gram row
+    blocks and windows (rows >= 4096; a device-side FP22 decode in the Gram build once broke exactly there)."""
+    from plssvm_sparse_fp22_amd.fp22 import pack, unpack
+
+    n, d, k = 20000, 4000, 50
+    csr, _ = datagen.sparse_csr(n, d, k, seed=5, dtype=np.float32)
+    dec = unpack(pack(csr[2]), csr[2].size)
+    x = np.random.default_rng(4).uniform(1, 2, n - 1).astype(np.float32)
+    outs = []
+    for fp22 in (True, False):
+        c = (csr[0], csr[1], csr[2] if fp22 else dec, n, d)
+        svm = sparse_svm(c, kernel, np.float32, fp22=fp22, mode=mode)
+        svm.setup_data_on_device()
+        q = svm.generate_q()
+        ret = svm.run_device_kernel(None, np.zeros(n - 1, np.float32), x, 1.0)
+        outs.append((q, ret))
+        svm.close()
+    assert np.all(np.isfinite(outs[0][1]))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
