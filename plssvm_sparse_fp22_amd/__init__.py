@@ -120,7 +120,9 @@ class CSVM:
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_RBF_FORM, rbf_form))
         if sim_rank is not None:  # (rank, world): single-GPU test hook, see PLSSVM_MI_OPT_SIM_RANK
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_SIM_RANK, sim_rank[0] | (sim_rank[1] << 16)))
-        if world_size > 1:
+        if world_size > 1 or uid is not None:  # a single-rank group (uid given) also runs its collectives on RCCL
+            if uid is None:
+                raise ValueError("world_size > 1 needs the group's unique id (rank 0: plssvm_sparse_fp22_amd.unique_id())")
             self._uid = ctypes.create_string_buffer(uid, _abi.UNIQUE_ID_BYTES)
             self._check(L.plssvm_mi_comm_init(self._ctx, rank, world_size, self._uid))
         self.world_size = world_size

@@ -121,22 +121,26 @@ void engine<T>::comm_init(int rank_, int world_, const void *uid) {
     }
     rank = rank_;
     world = world_;
-    if (world > 1) {
-        ncclUniqueId id;
-        std::memcpy(&id, uid, sizeof(id));
-        MI_NCCL_CHECK(ncclCommInitRank(&comm, world, id, rank));
+    // a single-rank group still gets a communicator (every collective then runs through RCCL on
+    // one GPU: the test path for the collective code on a one-GPU box)
+    if (uid == nullptr) {
+        if (world > 1) throw mi_error(-1, "a multi-rank group needs a unique id");
+        return;
     }
+    ncclUniqueId id;
+    std::memcpy(&id, uid, sizeof(id));
+    MI_NCCL_CHECK(ncclCommInitRank(&comm, world, id, rank));
 }
 
 template <typename T>
 void engine<T>::allreduce(T *buf, int64_t count) {
-    if (world == 1 || count <= 0) return;
+    if (comm == nullptr || count <= 0) return;
     MI_NCCL_CHECK(ncclAllReduce(buf, buf, (size_t) count, nccl_type<T>(), ncclSum, comm, stream));
 }
 
 template <typename T>
 void engine<T>::allgather_rows(T *buf) {
-    if (world == 1) return;
+    if (comm == nullptr) return;
     MI_NCCL_CHECK(ncclAllGather(buf + (int64_t) rank * chunk, buf, (size_t) chunk, nccl_type<T>(), comm, stream));
 }
 

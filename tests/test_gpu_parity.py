@@ -214,3 +214,34 @@ def test_single_point_degenerate():
     svm = make_svm(X, np.array([1.0]), "rbf", np.float64)
     svm.learn()
     assert svm.alpha.shape == (1,) and svm.alpha[0] == 0.0
+
+
+@pytest.mark.parametrize("layout,kernel,kp_mode", [("dense", "rbf", "auto"), ("dense", "linear", "factored"),
+                                                   ("csr", "linear", "auto"), ("csr", "rbf", "auto")])
+def test_single_rank_rccl_group(layout, kernel, kp_mode):
+    """A one-rank RCCL group (uid given) runs every per-K·p collective through RCCL on this GPU
+    (all-reduce of the raw K·p / of w, all-gather of the factored rows): the K·p and a CG solve must
+    equal the context without a communicator bit for bit — the collective code path on hardware."""
+    n, d = 3000, 64
+    if layout == "dense":
+        X, y = datagen.blobs(n, d, seed=3)
+    else:
+        csr, y = datagen.sparse_csr(n, 5000, 20, seed=3, dtype=np.float64)
+    outs = []
+    for uid in (None, pm.unique_id()):
+        p = pm.Parameter(kernel, gamma=1.0 / d, real_type=np.float64)
+        if layout == "dense":
+            p.data = X
+        else:
+            p.csr = csr
+        p.labels = y
+        svm = pm.CSVM(p, kp_mode=kp_mode, uid=uid)
+        svm.setup_data_on_device()
+        svm.generate_q()
+        x = np.linspace(1, 2, n - 1)
+        ret = svm.run_device_kernel(None, np.zeros(n - 1), x, 1.0)
+        svm.learn(imax=40)
+        outs.append((ret, np.array(svm.trace), svm.alpha.copy()))
+        svm.close()
+    for a, b in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, b)
