@@ -145,6 +145,22 @@ PLSSVM_MI_API int plssvm_mi_cg_result(plssvm_mi_ctx *ctx, void *x_out, double *d
 PLSSVM_MI_API int plssvm_mi_learn(plssvm_mi_ctx *ctx, const void *y, int64_t imax, double eps, void *alpha_out, double *bias_out,
                     double *delta_trace, int64_t *iters);
 
+/* gpu_csvm::update_w (src/plssvm/backends/gpu_csvm.cpp:327-350; OpenMP csvm.cpp:174-190):
+ * w_out[d] = sum_i alpha_i x_i over all n points of the context's data (alpha[n], e.g. from
+ * plssvm_mi_learn, alpha[m] included). Linear kernel model vector. */
+PLSSVM_MI_API int plssvm_mi_update_w(plssvm_mi_ctx *ctx, const void *alpha, void *w_out);
+
+/* gpu_csvm::predict (src/plssvm/backends/gpu_csvm.cpp:52-120; OpenMP csvm.cpp:193-240):
+ * out[p] = bias + sum_i alpha_i k(x_i, z_p) for np points with d features (linear: w . z_p + bias),
+ * the context's data being the model's support vectors. Dense points: Z row-major [np][d] of the
+ * real type. Sparse points (_csr): int64 rowptr[np+1], int32 col, values in val_fmt. np == 0 is a
+ * no-op; a feature-count mismatch fails with the reference's message. bias = -rho. */
+PLSSVM_MI_API int plssvm_mi_predict_dense(plssvm_mi_ctx *ctx, const void *alpha, double bias, const void *Z, int64_t np,
+                                          int64_t d, void *out);
+PLSSVM_MI_API int plssvm_mi_predict_csr(plssvm_mi_ctx *ctx, const void *alpha, double bias, const int64_t *rowptr,
+                                        const int32_t *col, const void *val, int val_fmt, int64_t np, int64_t d,
+                                        void *out);
+
 /* Timing hook (bench.py): runs `reps` K·p launches (+ reduction/collective) on resident device
  * buffers (p = a fixed device vector) and reports the average device time per K·p and per
  * dominant-kernel launch, measured with hipEvents on the context's stream. */

@@ -128,6 +128,7 @@ class CSVM:
         self.world_size = world_size
         self.rank = rank
         self.QA_cost = None
+        self.w = None
         self.alpha = None
         self.bias = None
         self.trace = None
@@ -228,6 +229,66 @@ class CSVM:
         self.iters = it.value
         self.trace = trace[: it.value + 1]
         return self
+
+    # ---- model use: update_w / predict / accuracy (csvm.hpp:123-178, gpu_csvm.cpp:52-127,327-350) ----
+    def _model(self, alpha, bias):
+        alpha = self.alpha if alpha is None else alpha
+        bias = self.bias if bias is None else bias
+        if alpha is None:
+            raise ValueError("No alphas provided for prediction!")
+        alpha = np.ascontiguousarray(alpha, dtype=self.dtype)
+        if alpha.shape != (self.num_data_points,):
+            raise ValueError(f"alpha must have {self.num_data_points} entries")
+        if not self._on_device:
+            self.setup_data_on_device()
+        return alpha, float(0.0 if bias is None else bias)
+
+    def update_w(self, alpha=None):
+        """w = sum_i alpha_i x_i over all points (the linear kernel's model vector)."""
+        alpha, _ = self._model(alpha, 0.0)
+        w = np.zeros(max(self.num_features, 1), dtype=self.dtype)
+        self._check(_abi.lib().plssvm_mi_update_w(self._ctx, _ptr(alpha), _ptr(w)))
+        self.w = w[: self.num_features]
+        return self.w
+
+    def predict_values(self, points, alpha=None, bias=None, val_fmt=None):
+        """Decision values bias + sum_i alpha_i k(x_i, z) for dense points [np][d] or a CSR tuple
+        (rowptr, col, val, np, d); defaults to the learned alpha and bias."""
+        alpha, b = self._model(alpha, bias)
+        L = _abi.lib()
+        if isinstance(points, tuple):
+            rowptr, col, val, npts, d = points
+            fmt = _abi.VAL_REAL if val_fmt is None else val_fmt
+            rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+            col = np.ascontiguousarray(col, dtype=np.int32)
+            val = np.ascontiguousarray(val, dtype=np.uint32 if fmt == _abi.VAL_FP22 else self.dtype)
+            out = np.zeros(max(npts, 1), dtype=self.dtype)
+            self._check(L.plssvm_mi_predict_csr(self._ctx, _ptr(alpha), b, _ptr(rowptr), _ptr(col), _ptr(val), fmt,
+                                                npts, d, _ptr(out)))
+            return out[:npts]
+        Z = np.ascontiguousarray(points, dtype=self.dtype)
+        if Z.ndim != 2:
+            raise ValueError("points must be a 2-D array [np][d]")
+        out = np.zeros(max(Z.shape[0], 1), dtype=self.dtype)
+        self._check(L.plssvm_mi_predict_dense(self._ctx, _ptr(alpha), b, _ptr(Z), Z.shape[0], Z.shape[1], _ptr(out)))
+        return out[: Z.shape[0]]
+
+    def predict(self, points, alpha=None, bias=None, val_fmt=None):
+        """Predicted labels (+-1): plssvm::operators::sign of the decision values (operators.hpp:174-177)."""
+        v = self.predict_values(points, alpha, bias, val_fmt)
+        return np.where(v > 0, self.dtype.type(1), self.dtype.type(-1))
+
+    def accuracy(self, points=None, labels=None):
+        """csvm::accuracy: fraction of correctly predicted labels (defaults: the training data)."""
+        if points is None:
+            points = self.params.data if self.params.data is not None else self.params.csr
+            labels = self.params.labels
+        if labels is None:
+            raise ValueError("No labels given for the accuracy calculation!")
+        pred = self.predict(points)
+        if pred.shape[0] != len(labels):
+            raise ValueError("the number of points to predict and correct labels mismatch")
+        return float(np.mean(pred == np.asarray(labels, dtype=self.dtype)))
 
     # ---- stepwise CG + timing (bench.py) ----
     def cg_begin(self, b, q=None, eps=None):

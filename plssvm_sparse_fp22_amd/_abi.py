@@ -28,6 +28,7 @@ EXPORTS = (
     "plssvm_mi_comm_init", "plssvm_mi_setup_dense", "plssvm_mi_setup_csr", "plssvm_mi_generate_q", "plssvm_mi_kp",
     "plssvm_mi_solve_cg", "plssvm_mi_cg_begin", "plssvm_mi_cg_step", "plssvm_mi_cg_result", "plssvm_mi_learn",
     "plssvm_mi_time_kp", "plssvm_mi_get_info", "plssvm_mi_partition",
+    "plssvm_mi_update_w", "plssvm_mi_predict_dense", "plssvm_mi_predict_csr",
 )
 OPT_SIM_RANK = 2
 OPT_RBF_FORM = 3
@@ -86,6 +87,9 @@ def _declare(L):
         "plssvm_mi_cg_step": ([P, I64, I, PI64, PI], I),
         "plssvm_mi_cg_result": ([P, P, P, I64, PI64], I),
         "plssvm_mi_learn": ([P, P, I64, D, P, PD, P, PI64], I),
+        "plssvm_mi_update_w": ([P, P, P], I),
+        "plssvm_mi_predict_dense": ([P, P, D, P, I64, I64, P], I),
+        "plssvm_mi_predict_csr": ([P, P, D, P, P, P, I, I64, I64, P], I),
         "plssvm_mi_time_kp": ([P, I, PD, PD], I),
         "plssvm_mi_get_info": ([P, ctypes.POINTER(Info)], I),
         "plssvm_mi_partition": ([I64, I, I, PI64], I),

@@ -242,6 +242,37 @@ int plssvm_mi_time_kp(plssvm_mi_ctx *ctx, int reps, double *ms_per_kp, double *m
     return ctx->call([&](auto &e) { e.time_kp(reps, ms_per_kp, ms_dominant_kernel); });
 }
 
+int plssvm_mi_update_w(plssvm_mi_ctx *ctx, const void *alpha, void *w_out) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        e.update_w(static_cast<const T *>(alpha), static_cast<T *>(w_out));
+    });
+}
+
+int plssvm_mi_predict_dense(plssvm_mi_ctx *ctx, const void *alpha, double bias, const void *Z, int64_t np, int64_t d,
+                            void *out) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        if (np > 0 && Z == nullptr) throw plssvm_mi::mi_error(PLSSVM_MI_ERR_ARG, "no points to predict");
+        e.predict(static_cast<const T *>(alpha), (T) bias, static_cast<const T *>(Z), nullptr, nullptr, nullptr,
+                  PLSSVM_MI_VAL_REAL, np, d, static_cast<T *>(out));
+    });
+}
+
+int plssvm_mi_predict_csr(plssvm_mi_ctx *ctx, const void *alpha, double bias, const int64_t *rowptr, const int32_t *col,
+                          const void *val, int val_fmt, int64_t np, int64_t d, void *out) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        if (np > 0 && (rowptr == nullptr || col == nullptr || (val == nullptr && rowptr[np] > 0)))
+            throw plssvm_mi::mi_error(PLSSVM_MI_ERR_ARG, "no points to predict");
+        e.predict(static_cast<const T *>(alpha), (T) bias, nullptr, rowptr, col, val, val_fmt, np, d,
+                  static_cast<T *>(out));
+    });
+}
+
 int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
     if (!cctx || !info) return PLSSVM_MI_ERR_ARG;
     auto *ctx = const_cast<plssvm_mi_ctx *>(cctx);

@@ -87,6 +87,7 @@ engine<T>::~engine() {
     (void) hipSetDevice(device);
     if (stream) (void) hipStreamSynchronize(stream);
     if (comm) (void) ncclCommDestroy(comm);
+    if (blas) (void) rocblas_destroy_handle(blas);
     XT.reset();
     partial.reset();
     if (stream) (void) hipStreamDestroy(stream);

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <rccl/rccl.h>
+#include <rocblas/rocblas.h>
 
 #include <memory>
 #include <string>
@@ -95,6 +96,13 @@ struct engine : engine_base {
     void spmv_pass_csc(const T *p, const cg_scalars<T> *status);    // factored linear: w = X^T p
     void spmv_pass_csr(const cg_scalars<T> *status);                // factored linear: raw = X w
     int64_t csr_bytes() const { return csr.bytes(); }
+
+    // model use (predict.hip): gpu_csvm::update_w / predict
+    rocblas_handle blas = nullptr;
+    void update_w_device(const T *alpha_dev);  // w = sum_i alpha_i x_i (device alpha[n])
+    void update_w(const T *alpha_host, T *w_host);
+    void predict(const T *alpha_host, T bias, const T *Z, const int64_t *zrowptr, const int32_t *zcol, const void *zval,
+                 int zfmt, int64_t np, int64_t dz, T *out);
 
     void allreduce(T *buf, int64_t count);
     void allgather_rows(T *buf);
