@@ -87,6 +87,7 @@ class csvm {
         if ((int64_t) y.size() != params_.num_data_points)
             throw std::invalid_argument("Number of labels must match the number of data points!");
         setup_data_on_device();
+        on_device_ = true;
         const std::vector<T> q = generate_q();
         const std::size_t m = (std::size_t) params_.num_data_points - 1;
         std::vector<T> b(y.begin(), y.begin() + (std::ptrdiff_t) m);
@@ -141,6 +142,53 @@ class csvm {
         std::fclose(fp);
     }
 
+    // model use (csvm.hpp:123-178; gpu_csvm::update_w / predict, gpu_csvm.cpp:52-127,327-350). Without a
+    // preceding learn(), set_model() supplies the alphas and rho of a model file.
+    void set_model(std::vector<T> alpha, T rho) {
+        if ((int64_t) alpha.size() != params_.num_data_points)
+            throw std::invalid_argument("Number of alphas must match the number of support vectors!");
+        alpha_ = std::move(alpha);
+        bias_ = -rho;
+        on_device_ = false;
+    }
+    std::vector<T> update_w() {
+        need_model();
+        std::vector<T> w((std::size_t) std::max<int64_t>(params_.num_features, 1));
+        check(plssvm_mi_update_w(ctx_, alpha_.data(), w.data()));
+        w.resize((std::size_t) params_.num_features);
+        return w;
+    }
+    // decision values bias + sum_i alpha_i k(sv_i, z) of the points held by `points`
+    std::vector<T> predict(const parameter<T> &points) {
+        need_model();
+        std::vector<T> out((std::size_t) std::max<int64_t>(points.num_data_points, 1));
+        if (points.sparse)
+            check(plssvm_mi_predict_csr(ctx_, alpha_.data(), (double) bias_, points.rowptr.data(), points.col.data(),
+                                        points.val.data(), PLSSVM_MI_VAL_REAL, points.num_data_points,
+                                        points.num_features, out.data()));
+        else
+            check(plssvm_mi_predict_dense(ctx_, alpha_.data(), (double) bias_, points.dense.data(), points.num_data_points,
+                                          points.num_features, out.data()));
+        out.resize((std::size_t) points.num_data_points);
+        return out;
+    }
+    // csvm::predict_label: sign of the decision values (operators.hpp:174-177)
+    std::vector<T> predict_label(const parameter<T> &points) {
+        std::vector<T> v = predict(points);
+        for (T &x : v) x = x > T(0) ? T(1) : T(-1);
+        return v;
+    }
+    // csvm::accuracy(points, correct_labels)
+    T accuracy(const parameter<T> &points) {
+        if (points.labels.empty()) throw std::invalid_argument("No labels given for the accuracy calculation!");
+        const std::vector<T> l = predict_label(points);
+        if (l.size() != points.labels.size())
+            throw std::invalid_argument("Number of data points to predict and correct labels mismatch!");
+        std::size_t ok = 0;
+        for (std::size_t i = 0; i < l.size(); ++i) ok += l[i] * points.labels[i] > T(0);
+        return (T) ok / (T) l.size();
+    }
+
     const std::vector<T> &alpha() const { return alpha_; }
     T bias() const { return bias_; }
     T rho() const { return -bias_; }
@@ -155,6 +203,13 @@ class csvm {
     }
 
   private:
+    void need_model() {
+        if (alpha_.empty()) throw std::invalid_argument("No alphas provided for prediction!");
+        if (!on_device_) {
+            setup_data_on_device();
+            on_device_ = true;
+        }
+    }
     void check(int rc) const {
         if (rc != PLSSVM_MI_OK) throw backend_exception(rc, plssvm_mi_last_error(ctx_));
     }
@@ -164,6 +219,7 @@ class csvm {
     std::vector<T> alpha_;
     std::vector<double> trace_;
     int64_t iterations_ = 0;
+    bool on_device_ = false;
 };
 
 }  // namespace plssvm::mi355x

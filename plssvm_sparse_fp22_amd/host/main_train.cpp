@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "cli.hpp"
 #include "csvm.hpp"
 
 namespace {
@@ -39,57 +40,6 @@ const char *kHelp =
     "      --max_iter arg         maximum CG iterations (default: num_features)\n"
     "      --single               train in single precision (float)\n"
     "      --device arg           HIP device ordinal (default: 0)\n";
-
-struct cli {
-    std::map<std::string, std::string> opt;
-    std::vector<std::string> pos;
-};
-
-cli parse(int argc, char **argv) {
-    static const std::map<std::string, std::string> shorts = { { "t", "kernel_type" }, { "d", "degree" },
-                                                               { "g", "gamma" },       { "r", "coef0" },
-                                                               { "c", "cost" },        { "e", "epsilon" },
-                                                               { "b", "backend" },     { "p", "target_platform" },
-                                                               { "q", "quiet" },       { "h", "help" } };
-    static const std::map<std::string, bool> is_flag = { { "quiet", true }, { "help", true }, { "sparse", true },
-                                                        { "single", true } };
-    cli c;
-    for (int i = 1; i < argc; ++i) {
-        std::string a = argv[i];
-        std::string key, val;
-        bool has_val = false;
-        if (a.rfind("--", 0) == 0) {
-            key = a.substr(2);
-            const auto eq = key.find('=');
-            if (eq != std::string::npos) {
-                val = key.substr(eq + 1);
-                key = key.substr(0, eq);
-                has_val = true;
-            }
-        } else if (a.size() >= 2 && a[0] == '-' && !(a[1] >= '0' && a[1] <= '9')) {
-            const auto it = shorts.find(a.substr(1, 1));
-            if (it == shorts.end()) throw std::invalid_argument("Option '" + a + "' does not exist");
-            key = it->second;
-            if (a.size() > 2) {
-                val = a.substr(2);
-                has_val = true;
-            }
-        } else {
-            c.pos.push_back(a);
-            continue;
-        }
-        if (is_flag.count(key)) {
-            c.opt[key] = "1";
-            continue;
-        }
-        if (!has_val) {
-            if (i + 1 >= argc) throw std::invalid_argument("Option '" + key + "' is missing an argument");
-            val = argv[++i];
-        }
-        c.opt[key] = val;
-    }
-    return c;
-}
 
 template <typename T>
 int train(const cli &c) {
@@ -164,7 +114,10 @@ int train(const cli &c) {
 
 int main(int argc, char **argv) {
     try {
-        const cli c = parse(argc, argv);
+        const cli c = parse_cli(argc, argv, { { "t", "kernel_type" }, { "d", "degree" }, { "g", "gamma" }, { "r", "coef0" },
+                                              { "c", "cost" }, { "e", "epsilon" }, { "b", "backend" },
+                                              { "p", "target_platform" }, { "q", "quiet" }, { "h", "help" } },
+                                { "quiet", "help", "sparse", "single" });
         if (c.opt.count("help")) {
             std::printf("%s", kHelp);
             return EXIT_SUCCESS;

@@ -6,7 +6,9 @@
 //     sign (x > 0 ? +1 : -1, parameter.cpp:160-163);
 //   * indices 0-based as written (parameter.cpp:75-83); num_features = max index + 1;
 //   * gamma = 1 / num_features in the real type when not given (parameter.cpp:150-152);
-//   * model file name = basename(input) + ".model" (parameter.cpp:575-578).
+//   * model file name = basename(input) + ".model", prediction file basename(input) + ".predict"
+//     (parameter.cpp:575-584);
+//   * model files as written by csvm::write_model (parameter.cpp:366-520).
 // Unlike the reference, which always densifies, the data can be kept as CSR (`sparse = true`).
 #pragma once
 
@@ -79,28 +81,24 @@ struct parameter {
     std::vector<real_type> val;
     std::vector<real_type> labels;  // +-1
 
+    std::string predict_name_from_input() const {
+        const auto pos = input_filename.find_last_of("/\\");
+        return input_filename.substr(pos == std::string::npos ? 0 : pos + 1) + ".predict";
+    }
     std::string model_name_from_input() const {
         const auto pos = input_filename.find_last_of("/\\");
         return input_filename.substr(pos == std::string::npos ? 0 : pos + 1) + ".model";
     }
 
-    // parse_train_file -> parse_libsvm_file (src/plssvm/parameter.cpp:132-176)
-    void parse_train_file(const std::string &filename, bool keep_sparse = false) {
-        if (model_filename.empty() || model_filename == model_name_from_input()) {
-            input_filename = filename;
-            model_filename = model_name_from_input();
-        }
-        input_filename = filename;
-        std::ifstream f(filename, std::ios::binary);
-        if (!f) throw std::runtime_error("Couldn't find file: '" + filename + "'!");
-        std::stringstream ss;
-        ss << f.rdbuf();
-        const std::string content = ss.str();
-
+    // LIBSVM rows "[label] idx:val ..." of content[start..] (parameter.cpp:40-176): left-trimmed, empty
+    // and '#' lines skipped, a leading token without ':' is the label / alpha, indices 0-based
+    struct rows_t {
         std::vector<std::vector<std::pair<int64_t, real_type>>> rows;
-        std::vector<real_type> vals;
-        bool has_label = true;
-        std::size_t pos = 0;
+        std::vector<real_type> first;  // label (train / test) or alpha (model SV section)
+        bool has_first = true;
+    };
+    static rows_t parse_rows(const std::string &content, std::size_t pos) {
+        rows_t out;
         while (pos <= content.size()) {
             std::size_t nl = content.find('\n', pos);
             if (nl == std::string::npos) nl = content.size();
@@ -113,10 +111,10 @@ struct parameter {
             std::size_t p = 0;
             if (sp == std::string_view::npos) sp = line.size();
             if (colon == std::string_view::npos || colon >= sp) {
-                vals.push_back(to_real<real_type>(line.substr(0, sp)));
+                out.first.push_back(to_real<real_type>(line.substr(0, sp)));
                 p = sp;
             } else {
-                has_label = false;
+                out.has_first = false;
             }
             std::vector<std::pair<int64_t, real_type>> r;
             while (true) {
@@ -135,19 +133,29 @@ struct parameter {
                 p = e;
             }
             std::sort(r.begin(), r.end());
-            rows.push_back(std::move(r));
+            out.rows.push_back(std::move(r));
         }
+        return out;
+    }
+
+    static std::string read_file(const std::string &filename) {
+        std::ifstream f(filename, std::ios::binary);
+        if (!f) throw std::runtime_error("Couldn't find file: '" + filename + "'!");
+        std::stringstream ss;
+        ss << f.rdbuf();
+        return ss.str();
+    }
+
+    // the data of this parameter object from parsed rows (dense or CSR), d = max(min_features, max index + 1)
+    void set_rows(const rows_t &pr, bool keep_sparse, int64_t min_features = 0) {
+        const auto &rows = pr.rows;
         if (rows.empty()) throw invalid_file_format_exception("Can't parse file: no data points are given!");
-        int64_t d = 0;
+        int64_t d = min_features;
         for (const auto &r : rows)
             if (!r.empty()) d = std::max<int64_t>(d, r.back().first + 1);
         if (d == 0) throw invalid_file_format_exception("Can't parse file: no data points are given!");
         num_data_points = (int64_t) rows.size();
         num_features = d;
-        if (gamma == real_type{ 0 }) gamma = real_type{ 1 } / static_cast<real_type>(d);
-        labels.clear();
-        if (has_label && (int64_t) vals.size() == num_data_points)
-            for (const real_type v : vals) labels.push_back(v > real_type{ 0 } ? real_type{ 1 } : real_type{ -1 });
         sparse = keep_sparse;
         rowptr.assign(1, 0);
         col.clear();
@@ -164,8 +172,87 @@ struct parameter {
         } else {
             dense.assign((std::size_t) (num_data_points * d), real_type{ 0 });
             for (int64_t i = 0; i < num_data_points; ++i)
-                for (const auto &[c, v] : rows[i]) dense[(std::size_t) (i * d + c)] = v;
+                for (const auto &[c, v] : rows[(std::size_t) i]) dense[(std::size_t) (i * d + c)] = v;
         }
+    }
+
+    // parse_train_file -> parse_libsvm_file (src/plssvm/parameter.cpp:132-176)
+    void parse_train_file(const std::string &filename, bool keep_sparse = false) {
+        if (model_filename.empty() || model_filename == model_name_from_input()) {
+            input_filename = filename;
+            model_filename = model_name_from_input();
+        }
+        input_filename = filename;
+        const rows_t pr = parse_rows(read_file(filename), 0);
+        set_rows(pr, keep_sparse);
+        if (gamma == real_type{ 0 }) gamma = real_type{ 1 } / static_cast<real_type>(num_features);
+        labels.clear();
+        if (pr.has_first && (int64_t) pr.first.size() == num_data_points)
+            for (const real_type v : pr.first) labels.push_back(v > real_type{ 0 } ? real_type{ 1 } : real_type{ -1 });
+    }
+
+    // parse_test_file (parameter.cpp:132-176 on the test set): points + optional labels
+    void parse_test_file(const std::string &filename, bool keep_sparse = false, int64_t min_features = 0) {
+        const rows_t pr = parse_rows(read_file(filename), 0);
+        set_rows(pr, keep_sparse, min_features);
+        labels.clear();
+        if (pr.has_first && (int64_t) pr.first.size() == num_data_points)
+            for (const real_type v : pr.first) labels.push_back(v > real_type{ 0 } ? real_type{ 1 } : real_type{ -1 });
+    }
+
+    // parse_model_file (src/plssvm/parameter.cpp:366-520): header (kernel_type, degree, gamma, coef0,
+    // rho, ...) until "SV", then one "alpha idx:val ..." line per support vector; the support vectors
+    // become this object's data, their alphas `alpha`, -rho the bias
+    real_type rho = 0;
+    std::vector<real_type> alpha;
+    void parse_model_file(const std::string &filename, bool keep_sparse = false, int64_t min_features = 0) {
+        const std::string content = read_file(filename);
+        std::size_t pos = 0;
+        bool have_kernel = false, have_rho = false;
+        while (true) {
+            if (pos >= content.size()) throw invalid_file_format_exception("Can't parse file: no support vectors are given!");
+            std::size_t nl = content.find('\n', pos);
+            if (nl == std::string::npos) nl = content.size();
+            std::string line(content.data() + pos, nl - pos);
+            pos = nl + 1;
+            while (!line.empty() && std::isspace((unsigned char) line.back())) line.pop_back();
+            std::size_t b = 0;
+            while (b < line.size() && std::isspace((unsigned char) line[b])) ++b;
+            line = line.substr(b);
+            if (line.empty()) continue;
+            if (line == "SV") break;
+            const std::size_t sp = line.find(' ');
+            const std::string key = line.substr(0, sp), value = sp == std::string::npos ? "" : line.substr(sp + 1);
+            if (key == "svm_type") {
+                if (value != "c_svc") throw invalid_file_format_exception("Can only use c_svc as svm_type, but '" + value + "' was given!");
+            } else if (key == "kernel_type") {
+                kernel = parse_kernel(value);
+                have_kernel = true;
+            } else if (key == "degree") {
+                degree = std::stoi(value);
+            } else if (key == "gamma") {
+                gamma = to_real<real_type>(value);
+            } else if (key == "coef0") {
+                coef0 = to_real<real_type>(value);
+            } else if (key == "rho") {
+                rho = to_real<real_type>(value);
+                have_rho = true;
+            } else if (key == "nr_class") {
+                if (std::stoi(value) != 2) throw invalid_file_format_exception("Can only use 2 classes, but " + value + " were given!");
+            } else if (key == "total_sv" || key == "label" || key == "nr_sv") {
+                // informational (the SV section defines the support vectors)
+            } else {
+                throw invalid_file_format_exception("Unrecognized header entry '" + key + "'! Maybe SV is missing?");
+            }
+        }
+        if (!have_kernel) throw invalid_file_format_exception("Missing kernel_type!");
+        if (!have_rho) throw invalid_file_format_exception("Missing rho value!");
+        const rows_t pr = parse_rows(content, pos);
+        if (!pr.has_first || pr.first.size() != pr.rows.size())
+            throw invalid_file_format_exception("Every support vector needs an alpha value!");
+        set_rows(pr, keep_sparse, min_features);
+        alpha = pr.first;
+        if (gamma == real_type{ 0 }) gamma = real_type{ 1 } / static_cast<real_type>(num_features);
     }
 
     real_type value(int64_t i, int64_t f) const {  // feature f of point i (dense or CSR)

@@ -47,3 +47,44 @@ def test_train_reproduces_golden_model(tmp_path, extra):
         assert abs(g[k] - w[k]) <= 1e-9 * max(1.0, abs(w[k]))
     head = open(out).read().splitlines()[:8]
     assert head[0] == "svm_type c_svc" and head[1] == "kernel_type linear" and head[-1] == "SV"
+
+
+PRED = os.path.join(ROOT, "plssvm_sparse_fp22_amd", "bin", "plssvm-predict")
+
+
+def test_predict_help_and_missing_files():
+    out = subprocess.run([PRED, "--help"], capture_output=True, text=True, check=True).stdout
+    assert "test_file model_file [output_file]" in out
+    for flag in ("--backend", "--target_platform", "--quiet"):
+        assert flag in out
+    r = subprocess.run([PRED, fixture_path("500x200.libsvm.test")], capture_output=True, text=True)
+    assert r.returncode != 0 and "missing model file" in r.stderr
+    r = subprocess.run([PRED, "-b", "cuda", fixture_path("500x200.libsvm.test"), fixture_path("500x200.libsvm.rbf.model")],
+                       capture_output=True, text=True)
+    assert r.returncode != 0 and "backend" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--sparse"]])
+@pytest.mark.parametrize("kernel", ["linear", "polynomial", "rbf"])
+def test_predict_reproduces_reference_prediction_file(tmp_path, kernel, extra):
+    """tests/data/models/500x200.libsvm.<kernel>.model on tests/data/libsvm/500x200.libsvm.test gives the
+    reference's tests/data/predict/500x200.libsvm.predict line for line (main_predict.cpp:80 writes
+    fmt::join(labels, "\n") without a final newline; the fixture file has one)."""
+    out = tmp_path / "p.predict"
+    r = subprocess.run([PRED, *extra, fixture_path("500x200.libsvm.test"), fixture_path(f"500x200.libsvm.{kernel}.model"),
+                        str(out)], capture_output=True, text=True, check=True)
+    got = open(out).read()
+    assert not got.endswith("\n")
+    assert got.split("\n") == open(fixture_path("500x200.libsvm.predict")).read().rstrip("\n").split("\n")
+    assert "Accuracy = " in r.stdout and "(classification)" in r.stdout
+
+
+@pytest.mark.gpu
+def test_train_then_predict_round_trip(tmp_path):
+    model = tmp_path / "m.model"
+    subprocess.run([EXE, "-q", "-t", "2", fixture_path("500x200.libsvm"), str(model)], check=True)
+    r = subprocess.run([PRED, fixture_path("500x200.libsvm"), str(model), str(tmp_path / "p")], capture_output=True,
+                       text=True, check=True)
+    acc = float(r.stdout.split("Accuracy = ")[1].split("%")[0])
+    assert acc > 90.0
