@@ -114,6 +114,13 @@ PLSSVM_MI_API int plssvm_mi_setup_dense(plssvm_mi_ctx *ctx, const void *X, int64
 PLSSVM_MI_API int plssvm_mi_setup_csr(plssvm_mi_ctx *ctx, const int64_t *rowptr, const int32_t *col, const void *val,
                         int val_fmt, int64_t n, int64_t d);
 
+/* Sparse setup from COO triplets (build-defined interchange format, e.g. BASELINE configs[4]):
+ * int64 row[nnz], int32 col[nnz] in any order, values in val_fmt (FP22: packed in triplet order).
+ * Converted on the host to CSR (rows, then columns ascending; a duplicate (row, col) is an error) and
+ * then exactly plssvm_mi_setup_csr. */
+PLSSVM_MI_API int plssvm_mi_setup_coo(plssvm_mi_ctx *ctx, const int64_t *row, const int32_t *col, const void *val,
+                                      int val_fmt, int64_t nnz, int64_t n, int64_t d);
+
 /* gpu_csvm::generate_q (src/plssvm/backends/gpu_csvm.cpp:160-183) + the QA_cost line of
  * csvm::learn (src/plssvm/csvm.cpp:243): q_out[m] = k(x_i, x_last); *qa_cost_out =
  * k(x_last, x_last) + 1/C. Also stores q and QA_cost in the context for plssvm_mi_kp. */

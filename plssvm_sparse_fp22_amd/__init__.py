@@ -21,10 +21,11 @@ import numpy as np
 
 from . import _abi
 from ._abi import BackendError, KERNELS
-from .io import parse_libsvm, parse_model
+from . import io as _io
+from .io import parse_libsvm, parse_model, read_binary, write_binary
 
-__all__ = ["Parameter", "CSVM", "BackendError", "parse_libsvm", "parse_model", "device_count", "unique_id",
-           "partition"]
+__all__ = ["Parameter", "CSVM", "BackendError", "parse_libsvm", "parse_model", "read_binary", "write_binary",
+           "device_count", "unique_id", "partition"]
 
 
 def device_count() -> int:
@@ -67,10 +68,20 @@ class Parameter:
         self.print_info = print_info
         self.data = None  # dense [n][d]
         self.csr = None  # (rowptr, col, val, n, d); val real or packed FP22 words
+        self.coo = None  # (row, col, val, n, d) triplets in any order; val real or packed FP22 words
         self.val_fmt = _abi.VAL_REAL
         self.labels = None
 
     def parse_train_file(self, path, sparse=False):
+        with open(path, "rb") as f:
+            binary = f.read(8) == _io.BIN_MAGIC
+        if binary:  # PLSSVMB1 binary CSR / FP22 file (io.write_binary): always sparse
+            csr, y, fmt = _io.read_binary(path, dtype=self.real_type)
+            self.csr, self.data, self.labels = csr, None, y
+            self.val_fmt = _abi.VAL_FP22 if fmt == _io.BIN_FP22 else _abi.VAL_REAL
+            if self.gamma == 0:
+                self.gamma = float(self.real_type.type(1) / self.real_type.type(csr[4]))
+            return self
         X, y = parse_libsvm(path, dtype=self.real_type, sparse=sparse)
         if sparse:
             self.csr, self.data = X, None
@@ -85,11 +96,15 @@ class Parameter:
 
     @property
     def num_features(self):
-        return self.data.shape[1] if self.data is not None else int(self.csr[4])
+        if self.data is not None:
+            return self.data.shape[1]
+        return int((self.csr if self.csr is not None else self.coo)[4])
 
     @property
     def num_data_points(self):
-        return self.data.shape[0] if self.data is not None else int(self.csr[3])
+        if self.data is not None:
+            return self.data.shape[0]
+        return int((self.csr if self.csr is not None else self.coo)[3])
 
 
 class CSVM:
@@ -97,7 +112,7 @@ class CSVM:
 
     def __init__(self, params: Parameter, device=0, rank=0, world_size=1, uid=None, kp_mode="auto",
                  sim_rank=None, rbf_form=0):
-        if params.data is None and params.csr is None:
+        if params.data is None and params.csr is None and params.coo is None:
             raise ValueError("No data points provided!")
         if params.data is not None:
             if params.data.ndim != 2 or params.data.shape[0] == 0:
@@ -167,12 +182,18 @@ class CSVM:
         if p.data is not None:
             X = np.ascontiguousarray(p.data, dtype=self.dtype)
             self._check(L.plssvm_mi_setup_dense(self._ctx, _ptr(X), X.shape[0], X.shape[1]))
-        else:
+        elif p.csr is not None:
             rowptr, col, val, n, d = p.csr
             rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
             col = np.ascontiguousarray(col, dtype=np.int32)
             val = np.ascontiguousarray(val, dtype=np.uint32 if p.val_fmt == _abi.VAL_FP22 else self.dtype)
             self._check(L.plssvm_mi_setup_csr(self._ctx, _ptr(rowptr), _ptr(col), _ptr(val), p.val_fmt, n, d))
+        else:
+            row, col, val, n, d = p.coo
+            row = np.ascontiguousarray(row, dtype=np.int64)
+            col = np.ascontiguousarray(col, dtype=np.int32)
+            val = np.ascontiguousarray(val, dtype=np.uint32 if p.val_fmt == _abi.VAL_FP22 else self.dtype)
+            self._check(L.plssvm_mi_setup_coo(self._ctx, _ptr(row), _ptr(col), _ptr(val), p.val_fmt, row.size, n, d))
         self._on_device = True
 
     def generate_q(self):

@@ -28,7 +28,7 @@ EXPORTS = (
     "plssvm_mi_comm_init", "plssvm_mi_setup_dense", "plssvm_mi_setup_csr", "plssvm_mi_generate_q", "plssvm_mi_kp",
     "plssvm_mi_solve_cg", "plssvm_mi_cg_begin", "plssvm_mi_cg_step", "plssvm_mi_cg_result", "plssvm_mi_learn",
     "plssvm_mi_time_kp", "plssvm_mi_get_info", "plssvm_mi_partition",
-    "plssvm_mi_update_w", "plssvm_mi_predict_dense", "plssvm_mi_predict_csr",
+    "plssvm_mi_update_w", "plssvm_mi_predict_dense", "plssvm_mi_predict_csr", "plssvm_mi_setup_coo",
 )
 OPT_SIM_RANK = 2
 OPT_RBF_FORM = 3
@@ -80,6 +80,7 @@ def _declare(L):
         "plssvm_mi_comm_init": ([P, I, I, P], I),
         "plssvm_mi_setup_dense": ([P, P, I64, I64], I),
         "plssvm_mi_setup_csr": ([P, P, P, P, I, I64, I64], I),
+        "plssvm_mi_setup_coo": ([P, P, P, P, I, I64, I64, I64], I),
         "plssvm_mi_generate_q": ([P, P, PD], I),
         "plssvm_mi_kp": ([P, P, P, P, D], I),
         "plssvm_mi_solve_cg": ([P, P, P, I64, D, P, P, PI64], I),

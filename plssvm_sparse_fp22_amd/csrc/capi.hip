@@ -1,4 +1,5 @@
 // C ABI (include/plssvm_mi355x.h): exception-free wrappers around engine<float|double>.
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -160,6 +161,58 @@ int plssvm_mi_setup_csr(plssvm_mi_ctx *ctx, const int64_t *rowptr, const int32_t
                         int64_t n, int64_t d) {
     if (!ctx) return PLSSVM_MI_ERR_ARG;
     return ctx->call([&](auto &e) { e.setup_csr(rowptr, col, val, val_fmt, n, d); });
+}
+
+int plssvm_mi_setup_coo(plssvm_mi_ctx *ctx, const int64_t *row, const int32_t *col, const void *val, int val_fmt,
+                        int64_t nnz, int64_t n, int64_t d) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        using plssvm_mi::mi_error;
+        if (n < 1 || d < 1) throw mi_error(PLSSVM_MI_ERR_ARG, "Data set is empty!");
+        if (nnz < 0 || (nnz > 0 && (!row || !col || !val))) throw mi_error(PLSSVM_MI_ERR_ARG, "COO arrays missing");
+        if (val_fmt != PLSSVM_MI_VAL_REAL && val_fmt != PLSSVM_MI_VAL_FP22) throw mi_error(PLSSVM_MI_ERR_ARG, "unknown value format");
+        // counting sort by row (stable), then columns ascending inside each row
+        std::vector<int64_t> rowptr((size_t) n + 1, 0);
+        for (int64_t k = 0; k < nnz; ++k) {
+            if (row[k] < 0 || row[k] >= n) throw mi_error(PLSSVM_MI_ERR_ARG, "COO row index out of range");
+            if (col[k] < 0 || col[k] >= d) throw mi_error(PLSSVM_MI_ERR_ARG, "COO column index out of range");
+            ++rowptr[(size_t) row[k] + 1];
+        }
+        for (int64_t i = 0; i < n; ++i) rowptr[(size_t) i + 1] += rowptr[(size_t) i];
+        std::vector<int64_t> perm((size_t) std::max<int64_t>(nnz, 1)), fill(rowptr.begin(), rowptr.end() - 1);
+        for (int64_t k = 0; k < nnz; ++k) perm[(size_t) fill[(size_t) row[k]]++] = k;
+        std::vector<int32_t> ccol((size_t) std::max<int64_t>(nnz, 1));
+        for (int64_t i = 0; i < n; ++i) {
+            auto b = perm.begin() + rowptr[(size_t) i], en = perm.begin() + rowptr[(size_t) i + 1];
+            std::sort(b, en, [&](int64_t a, int64_t c) { return col[a] < col[c]; });
+            for (auto it = b; it != en; ++it) {
+                if (it != b && col[*it] == col[*(it - 1)])
+                    throw mi_error(PLSSVM_MI_ERR_ARG, "duplicate COO entry (row " + std::to_string(i) + ", column " +
+                                                          std::to_string(col[*it]) + ")");
+                ccol[(size_t) (it - perm.begin())] = col[*it];
+            }
+        }
+        if (val_fmt == PLSSVM_MI_VAL_FP22) {  // re-pack the words in CSR order (decode(encode(x)) is exact)
+            const auto *w = static_cast<const uint32_t *>(val);
+            std::vector<uint32_t> words((size_t) plssvm_mi::fp22_words(std::max<int64_t>(nnz, 1)) + 1, 0u);
+            for (int64_t t = 0; t < nnz; ++t) {
+                const uint64_t code = plssvm_mi::fp22_encode_host(plssvm_mi::fp22_get(w, perm[(size_t) t]));
+                const int64_t g = t >> 4;
+                const int bit = 22 * (int) (t & 15);
+                const int64_t wi = g * 11 + (bit >> 5);
+                const int sh = bit & 31;
+                words[(size_t) wi] |= (uint32_t) (code << sh);
+                if (sh > 10) words[(size_t) wi + 1] |= (uint32_t) (code >> (32 - sh));
+            }
+            e.setup_csr(rowptr.data(), ccol.data(), words.data(), val_fmt, n, d);
+        } else {
+            const auto *v = static_cast<const T *>(val);
+            std::vector<T> cval((size_t) std::max<int64_t>(nnz, 1));
+            for (int64_t t = 0; t < nnz; ++t) cval[(size_t) t] = v[perm[(size_t) t]];
+            e.setup_csr(rowptr.data(), ccol.data(), cval.data(), val_fmt, n, d);
+        }
+    });
 }
 
 int plssvm_mi_generate_q(plssvm_mi_ctx *ctx, void *q_out, double *qa_cost_out) {

@@ -47,8 +47,9 @@ class csvm {
     void setup_data_on_device() {
         const auto &p = params_;
         if (p.sparse) {
-            check(plssvm_mi_setup_csr(ctx_, p.rowptr.data(), p.col.data(), p.val.data(), PLSSVM_MI_VAL_REAL,
-                                      p.num_data_points, p.num_features));
+            const bool f22 = !p.val22.empty() && sizeof(T) == 4;  // packed FP22 input stays packed
+            check(plssvm_mi_setup_csr(ctx_, p.rowptr.data(), p.col.data(), f22 ? (const void *) p.val22.data() : p.val.data(),
+                                      f22 ? PLSSVM_MI_VAL_FP22 : PLSSVM_MI_VAL_REAL, p.num_data_points, p.num_features));
         } else {
             check(plssvm_mi_setup_dense(ctx_, p.dense.data(), p.num_data_points, p.num_features));
         }

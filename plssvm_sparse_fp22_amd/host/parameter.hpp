@@ -17,6 +17,7 @@
 #include <charconv>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <sstream>
 #include <stdexcept>
@@ -79,6 +80,7 @@ struct parameter {
     std::vector<int64_t> rowptr;
     std::vector<int32_t> col;
     std::vector<real_type> val;
+    std::vector<uint32_t> val22;    // packed FP22 words of `val` (binary FP22 input; kept packed for the device)
     std::vector<real_type> labels;  // +-1
 
     std::string predict_name_from_input() const {
@@ -160,6 +162,7 @@ struct parameter {
         rowptr.assign(1, 0);
         col.clear();
         val.clear();
+        val22.clear();
         dense.clear();
         if (sparse) {
             for (const auto &r : rows) {
@@ -176,14 +179,87 @@ struct parameter {
         }
     }
 
-    // parse_train_file -> parse_libsvm_file (src/plssvm/parameter.cpp:132-176)
+    // PLSSVMB1 binary CSR / FP22 data file (layout: plssvm_sparse_fp22_amd/io.py); always kept sparse
+    static bool is_binary(const std::string &content) { return content.size() >= 48 && content.compare(0, 8, "PLSSVMB1") == 0; }
+    void parse_binary(const std::string &c) {
+        auto rd = [&](std::size_t off, void *dst, std::size_t nb) {
+            if (off + nb > c.size()) throw invalid_file_format_exception("truncated PLSSVMB1 file");
+            std::memcpy(dst, c.data() + off, nb);
+        };
+        uint32_t vf[2];
+        int64_t hdr[3];
+        int32_t fmt[2];
+        rd(8, vf, 8);
+        rd(16, hdr, 24);
+        rd(40, fmt, 8);
+        if (vf[0] != 1) throw invalid_file_format_exception("unsupported PLSSVMB1 version");
+        const int64_t n = hdr[0], d = hdr[1], nnz = hdr[2];
+        if (n < 1 || d < 1 || nnz < 0) throw invalid_file_format_exception("Can't parse file: no data points are given!");
+        auto pad8 = [](std::size_t b) { return (8 - b % 8) % 8; };
+        std::size_t off = 48;
+        rowptr.resize((std::size_t) n + 1);
+        rd(off, rowptr.data(), 8 * ((std::size_t) n + 1));
+        off += 8 * ((std::size_t) n + 1);
+        col.resize((std::size_t) nnz);
+        rd(off, col.data(), 4 * (std::size_t) nnz);
+        off += 4 * (std::size_t) nnz + pad8(4 * (std::size_t) nnz);
+        val.resize((std::size_t) nnz);
+        val22.clear();
+        std::size_t nb;
+        if (fmt[0] == 2) {
+            nb = 4 * 11 * (((std::size_t) nnz + 15) / 16);
+            val22.resize(nb / 4 + 1, 0u);
+            rd(off, val22.data(), nb);
+            for (int64_t k = 0; k < nnz; ++k) {
+                const int bit = 22 * (int) (k & 15);
+                const uint32_t *w = val22.data() + (k >> 4) * 11 + (bit >> 5);
+                const int sh = bit & 31;
+                uint64_t x = (uint64_t) w[0] >> sh;
+                if (sh > 10) x |= (uint64_t) w[1] << (32 - sh);
+                const uint32_t u = (uint32_t) (x & 0x3FFFFFu) << 10;
+                float f;
+                std::memcpy(&f, &u, 4);
+                val[(std::size_t) k] = (real_type) f;
+            }
+        } else if (fmt[0] == 1) {
+            nb = 8 * (std::size_t) nnz;
+            std::vector<double> tmp((std::size_t) nnz);
+            rd(off, tmp.data(), nb);
+            for (int64_t k = 0; k < nnz; ++k) val[(std::size_t) k] = (real_type) tmp[(std::size_t) k];
+        } else {
+            nb = 4 * (std::size_t) nnz;
+            std::vector<float> tmp((std::size_t) nnz);
+            rd(off, tmp.data(), nb);
+            for (int64_t k = 0; k < nnz; ++k) val[(std::size_t) k] = (real_type) tmp[(std::size_t) k];
+        }
+        off += nb + pad8(nb);
+        labels.clear();
+        if (vf[1] & 1u) {
+            std::vector<double> y((std::size_t) n);
+            rd(off, y.data(), 8 * (std::size_t) n);
+            for (const double v : y) labels.push_back(v > 0 ? real_type{ 1 } : real_type{ -1 });
+        }
+        if (rowptr[0] != 0 || rowptr.back() != nnz) throw invalid_file_format_exception("corrupt PLSSVMB1 row pointers");
+        sparse = true;
+        num_data_points = n;
+        num_features = d;
+        dense.clear();
+    }
+
+    // parse_train_file -> parse_libsvm_file (src/plssvm/parameter.cpp:132-176); PLSSVMB1 binary files too
     void parse_train_file(const std::string &filename, bool keep_sparse = false) {
         if (model_filename.empty() || model_filename == model_name_from_input()) {
             input_filename = filename;
             model_filename = model_name_from_input();
         }
         input_filename = filename;
-        const rows_t pr = parse_rows(read_file(filename), 0);
+        const std::string content = read_file(filename);
+        if (is_binary(content)) {
+            parse_binary(content);
+            if (gamma == real_type{ 0 }) gamma = real_type{ 1 } / static_cast<real_type>(num_features);
+            return;
+        }
+        const rows_t pr = parse_rows(content, 0);
         set_rows(pr, keep_sparse);
         if (gamma == real_type{ 0 }) gamma = real_type{ 1 } / static_cast<real_type>(num_features);
         labels.clear();

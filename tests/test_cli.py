@@ -88,3 +88,17 @@ def test_train_then_predict_round_trip(tmp_path):
                        text=True, check=True)
     acc = float(r.stdout.split("Accuracy = ")[1].split("%")[0])
     assert acc > 90.0
+
+
+@pytest.mark.gpu
+def test_train_binary_input_equals_libsvm(tmp_path):
+    """plssvm-train on the PLSSVMB1 binary form of 5x4.libsvm writes the same model as on the text file."""
+    from plssvm_sparse_fp22_amd import io
+
+    X, y = io.parse_libsvm(fixture_path("5x4.libsvm"), sparse=True)
+    b = tmp_path / "5x4.bin"
+    io.write_binary(b, X, y, io.BIN_F64)
+    m1, m2 = tmp_path / "a.model", tmp_path / "b.model"
+    subprocess.run([EXE, "-q", "--sparse", fixture_path("5x4.libsvm"), str(m1)], check=True)
+    subprocess.run([EXE, "-q", str(b), str(m2)], check=True)
+    assert open(m1).read() == open(m2).read()

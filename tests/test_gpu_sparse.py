@@ -179,3 +179,45 @@ def test_sparse_fp22_equals_decoded_input(kernel, mode):
     assert np.all(np.isfinite(outs[0][1]))
     np.testing.assert_array_equal(outs[0][0], outs[1][0])
     np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("kernel,fp22", [("rbf", False), ("linear", False), ("rbf", True), ("linear", True)])
+def test_coo_setup_equals_csr(kernel, fp22):
+    """COO triplets in random order (plssvm_mi_setup_coo) == the same matrix as CSR, bit for bit."""
+    n, d = 5000, 3000
+    csr, _ = datagen.sparse_csr(n, d, 15, seed=9, dtype=np.float32)
+    rowptr, col, val = csr[0], csr[1], csr[2]
+    row = np.repeat(np.arange(n, dtype=np.int64), np.diff(rowptr))
+    perm = np.random.default_rng(2).permutation(col.size)
+    x = np.random.default_rng(3).uniform(1, 2, n - 1).astype(np.float32)
+    outs = []
+    for layout in ("csr", "coo"):
+        p = pm.Parameter(kernel, gamma=1.0 / d, real_type=np.float32)
+        if layout == "csr":
+            p.csr = (rowptr, col, pack_fp22(val) if fp22 else val, n, d)
+        else:
+            p.coo = (row[perm], col[perm], pack_fp22(val[perm]) if fp22 else val[perm], n, d)
+        if fp22:
+            p.val_fmt = pm._abi.VAL_FP22
+        with pm.CSVM(p) as svm:
+            svm.setup_data_on_device()
+            q = svm.generate_q()
+            outs.append((q, svm.run_device_kernel(None, np.zeros(n - 1, np.float32), x, 1.0)))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
+def pack_fp22(v):
+    from plssvm_sparse_fp22_amd.fp22 import pack
+
+    return pack(v)
+
+
+def test_coo_rejects_duplicates_and_bad_indices():
+    p = pm.Parameter("rbf", real_type=np.float64)
+    p.coo = (np.array([0, 1, 1], np.int64), np.array([2, 0, 0], np.int32), np.ones(3), 3, 4)
+    with pm.CSVM(p) as svm, pytest.raises(pm.BackendError, match="duplicate COO entry"):
+        svm.setup_data_on_device()
+    p.coo = (np.array([0, 5], np.int64), np.array([1, 1], np.int32), np.ones(2), 3, 4)
+    with pm.CSVM(p) as svm, pytest.raises(pm.BackendError, match="row index out of range"):
+        svm.setup_data_on_device()
