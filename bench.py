@@ -210,7 +210,7 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
         else:
             nnz = info["nnz"]
             alg = (2 * (nnz * (4 + es) + (m + 1) * 8) + 4 * m * es + 2 * d * es) / world
-            kname = "sell_spmv_kernel+panel_reduce_kernel"
+            kname = "sell_spmv_kernel*2+panel_reduce_kernel*2"  # CSC pass + CSR pass
             moved = info["spmv_bytes"]  # what the two SELL passes actually stream (16-bit panel indices)
             return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
                         frac=alg / s / PEAKS["hbm"], traffic=None, kernel=kname, launch_ms=ms_dom, alg_bytes=alg,

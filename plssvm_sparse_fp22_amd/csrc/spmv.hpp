@@ -37,7 +37,10 @@ namespace plssvm_mi {
 
 constexpr int SELL_NT = 1024;  // 16 waves per workgroup
 constexpr int SELL_WAVES = SELL_NT / 64;
-constexpr int SELL_XBYTES = 65536;  // LDS panel of the gathered vector
+#ifndef PLSSVM_MI_SELL_XBYTES
+#define PLSSVM_MI_SELL_XBYTES 65536
+#endif
+constexpr int SELL_XBYTES = PLSSVM_MI_SELL_XBYTES;  // LDS panel of the gathered vector (2 workgroups / CU)
 constexpr int SELL_SIGMA = 4096;    // sorting window (segments)
 #ifndef PLSSVM_MI_SELL_UNROLL
 #define PLSSVM_MI_SELL_UNROLL 8
@@ -163,7 +166,8 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
     }
 }
 
-// out[s] = sum_q partial[q][s] in panel order
+// out[s] = sum_q partial[q][s] in panel order (8 panel loads in flight per step; the CSC pass has few
+// segments and many panels, so per-thread memory parallelism, not thread count, sets its speed)
 template <typename T>
 __global__ __launch_bounds__(256) void panel_reduce_kernel(const T *__restrict__ partial, int64_t P, int64_t nseg,
                                                            T *__restrict__ out, const cg_scalars<T> *__restrict__ status) {
@@ -171,7 +175,15 @@ __global__ __launch_bounds__(256) void panel_reduce_kernel(const T *__restrict__
     const int64_t s = (int64_t) blockIdx.x * 256 + threadIdx.x;
     if (s >= nseg) return;
     T a = 0;
-    for (int64_t q = 0; q < P; ++q) a += partial[q * nseg + s];
+    int64_t q = 0;
+    for (; q + 8 <= P; q += 8) {
+        T v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = partial[(q + u) * nseg + s];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += v[u];
+    }
+    for (; q < P; ++q) a += partial[q * nseg + s];
     out[s] = a;
 }
 

@@ -33,7 +33,10 @@ def main():
     tag, config, rnd = sys.argv[1:4]
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     bench = json.loads(open(os.path.join(src, "bench_trace.json")).read().strip().splitlines()[-1])
-    kernels = bench["roofline"]["kernel"].split("+")  # the dominant launch may be two kernels
+    # the dominant launch may be several kernels; "name*k" = k dispatches of that kernel per launch
+    parts = [k.split("*") for k in bench["roofline"]["kernel"].split("+")]
+    kernels = [p[0] for p in parts]
+    mult = {p[0]: int(p[1]) if len(p) > 1 else 1 for p in parts}
     stats = find(os.path.join(src, "trace", "**", "*kernel_stats.csv"))
     prof = os.path.join(ROOT, "profiles")
     shutil.copy(stats, os.path.join(prof, f"{rnd}_{config}_kernel_stats.csv"))
@@ -44,7 +47,7 @@ def main():
         for k in kernels:
             if k in row["Name"] and k not in avg:
                 avg[k] = float(row["AverageNs"])
-    avg_ns = sum(avg.values()) if len(avg) == len(kernels) else None
+    avg_ns = sum(avg[k] * mult[k] for k in avg) if len(avg) == len(kernels) else None
     vals = {k: [] for k in kernels}
     pmc = find(os.path.join(src, "pmc", "**", "*counter_collection.csv*"))
     with (gzip.open(pmc, "rt") if pmc.endswith(".gz") else open(pmc)) as f:
@@ -54,10 +57,10 @@ def main():
                     vals[k].append(float(row["Counter_Value"]))
     if not all(vals.values()):
         raise SystemExit(f"no FETCH_SIZE rows for {kernels}")
-    fetch_kib = sum(statistics.mean(v) for v in vals.values())
+    fetch_kib = sum(statistics.mean(v) * mult[k] for k, v in vals.items())
     out = {
         "config": config, "N": bench["config"]["N"], "d": bench["config"]["d"], "n_gpus": bench["n_gpus"],
-        "kernel": "+".join(kernels), "dispatches": min(len(v) for v in vals.values()), "fetch_size_kib_mean": fetch_kib,
+        "kernel": bench["roofline"]["kernel"], "dispatches": min(len(v) for v in vals.values()), "fetch_size_kib_mean": fetch_kib,
         "hbm_read_bytes_per_launch": fetch_kib * 1024 * 2,
         "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 counts half of wide streaming reads)",
         "rocprof_avg_ms": None if avg_ns is None else avg_ns * 1e-6,
