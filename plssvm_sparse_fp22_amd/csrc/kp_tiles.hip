@@ -35,6 +35,94 @@ __device__ __forceinline__ T kernel_apply(int kernel, int degree, T gamma, T coe
     return exp(-gamma * dist);
 }
 
+// exp for the fp64 RBF epilogue, in the scaled domain y = x * 256 / ln2 (x = -gamma * dist <= 0):
+// exp(x) = 2^(j >> 8) * 2^((j & 255) / 256) * e^(r ln2 / 256), j = rint(y), r = y - j in [-1/2, 1/2];
+// 2^(i/256) from a 256-entry LDS table (correctly rounded), e^(r ln2/256) by a degree-4 polynomial
+// (truncation < 4e-17 relative). 11 fp64 VALU + 3 integer + 1 LDS read per element instead of ~26
+// for dist + libm exp: on gfx950 every VALU cycle of the epilogue is a cycle of the fp64 MFMA pipe
+// (DESIGN.md §3.1), so the instruction count is what matters. No clamp of y at 0: the norm trick can
+// round dist to -1e-16 relative, giving exp of a tiny positive number (as harmless as the clamp).
+// The rounding of y (|y| < ~1500 on the BASELINE data) adds < 2e-15 relative error.
+__constant__ double c_exp2_256[256] = {
+    1.0, 1.0027112750502025, 1.0054299011128027, 1.0081558981184175,
+    1.0108892860517005, 1.0136300849514894, 1.016378314910953, 1.019133996077738,
+    1.0218971486541166, 1.0246677928971357, 1.0274459491187637, 1.030231637686041,
+    1.0330248790212284, 1.0358256936019572, 1.0386341019613787, 1.041450124688316,
+    1.0442737824274138, 1.0471050958792898, 1.0499440858006872, 1.0527907730046264,
+    1.0556451783605572, 1.0585073227945128, 1.061377227289262, 1.0642549128844645,
+    1.0671404006768237, 1.0700337118202419, 1.0729348675259756, 1.075843889062791,
+    1.0787607977571199, 1.0816856149932152, 1.0846183622133092, 1.0875590609177697,
+    1.0905077326652577, 1.0934643990728858, 1.0964290818163769, 1.099401802630222,
+    1.102382583307841, 1.1053714457017412, 1.1083684117236787, 1.1113735033448175,
+    1.1143867425958924, 1.1174081515673693, 1.1204377524096067, 1.12347556733302,
+    1.1265216186082418, 1.129575928566288, 1.1326385195987192, 1.1357094141578055,
+    1.1387886347566916, 1.1418762039695616, 1.1449721444318042, 1.148076478840179,
+    1.1511892299529827, 1.154310420590216, 1.1574400736337511, 1.1605782120274988,
+    1.1637248587775775, 1.1668800369524817, 1.1700437696832502, 1.1732160801636373,
+    1.1763969916502812, 1.1795865274628758, 1.182784710984341, 1.1859915656609938,
+    1.189207115002721, 1.1924313825831512, 1.1956643920398273, 1.1989061670743806,
+    1.202156731452703, 1.2054161090051239, 1.2086843236265816, 1.2119613992768012,
+    1.215247359980469, 1.2185422298274085, 1.2218460329727576, 1.2251587936371455,
+    1.22848053610687, 1.2318112847340759, 1.2351510639369334, 1.2384998981998165,
+    1.241857812073484, 1.245224830175258, 1.2486009771892048, 1.2519862778663162,
+    1.255380757024691, 1.2587844395497165, 1.2621973503942507, 1.2656195145788063,
+    1.2690509571917332, 1.2724917033894028, 1.275941778396392, 1.2794012075056693,
+    1.2828700160787783, 1.2863482295460256, 1.2898358734066657, 1.2933329732290895,
+    1.2968395546510096, 1.3003556433796506, 1.3038812651919358, 1.3074164459346773,
+    1.3109612115247644, 1.3145155879493546, 1.318079601266064, 1.3216532776031575,
+    1.3252366431597413, 1.3288297242059544, 1.3324325470831615, 1.3360451382041458,
+    1.339667524053303, 1.3432997311868353, 1.3469417862329458, 1.3505937158920345,
+    1.3542555469368927, 1.3579273062129011, 1.3616090206382248, 1.365300717204012,
+    1.3690024229745905, 1.3727141650876684, 1.3764359707545302, 1.380167867260238,
+    1.383909881963832, 1.387662042298529, 1.3914243757719262, 1.3951969099662003,
+    1.3989796725383112, 1.4027726912202048, 1.4065759938190154, 1.4103896082172707,
+    1.4142135623730951, 1.4180478843204152, 1.4218926021691656, 1.4257477441054942,
+    1.42961333839197, 1.433489413367789, 1.4373759974489824, 1.4412731191286257,
+    1.4451808069770467, 1.449099089642035, 1.4530279958490526, 1.4569675544014438,
+    1.460917794180647, 1.4648787441464057, 1.4688504333369818, 1.4728328908693675,
+    1.4768261459394993, 1.4808302278224719, 1.4848451658727524, 1.488870989524397,
+    1.4929077282912648, 1.4969554117672355, 1.5010140696264256, 1.5050837316234065,
+    1.5091644275934228, 1.5132561874526098, 1.5173590411982147, 1.5214730189088146,
+    1.5255981507445384, 1.529734466947287, 1.533881997840956, 1.5380407738316568,
+    1.5422108254079407, 1.5463921831410214, 1.550584877685, 1.5547889397770887,
+    1.559004400237837, 1.5632312899713576, 1.567469639965553, 1.5717194812923414,
+    1.5759808451078865, 1.5802537626528246, 1.5845382652524937, 1.588834384317164,
+    1.593142151342267, 1.597461597908627, 1.6017927556826934, 1.606135656416771,
+    1.6104903319492543, 1.6148568142048607, 1.6192351351948637, 1.6236253270173289,
+    1.6280274218573478, 1.632441451987275, 1.6368674497669644, 1.6413054476440063,
+    1.645755478153965, 1.6502175739206177, 1.6546917676561943, 1.6591780921616162,
+    1.6636765803267364, 1.6681872651305825, 1.6727101796415966, 1.6772453570178785,
+    1.681792830507429, 1.6863526334483934, 1.6909247992693053, 1.6955093614893326,
+    1.7001063537185235, 1.7047158096580513, 1.709337763100463, 1.713972247929926,
+    1.718619298122478, 1.723278947746274, 1.7279512309618377, 1.732636182022311,
+    1.7373338352737062, 1.7420442251551564, 1.746767386199169, 1.7515033530318782,
+    1.7562521603732995, 1.761013843037584, 1.7657884359332727, 1.7705759740635547,
+    1.7753764925265212, 1.7801900265154245, 1.785016611318935, 1.789856282321401,
+    1.7947090750031072, 1.7995750249405351, 1.804454167806624, 1.809346539371032,
+    1.8142521755003989, 1.8191711121586085, 1.8241033854070534, 1.8290490314048973,
+    1.8340080864093424, 1.8389805867758937, 1.843966568958626, 1.8489660695104508,
+    1.8539791250833855, 1.8590057724288205, 1.864046048397789, 1.8690999899412386,
+    1.8741676341103, 1.8792490180565602, 1.8843441790323345, 1.8894531543909392,
+    1.8945759815869656, 1.8997126981765553, 1.9048633418176741, 1.9100279502703899,
+    1.9152065613971474, 1.9203992131630474, 1.925605943636125, 1.930826790987627,
+    1.9360617934922943, 1.9413109895286405, 1.9465744175792332, 1.9518521162309783,
+    1.9571441241754002, 1.9624504802089273, 1.9677712232331759, 1.9731063922552343,
+    1.978456026387951, 1.9838201648502194, 1.9891988469672663, 1.9945921121709402
+};
+constexpr double K256 = 369.3299304675746;  // 256 / ln 2
+
+__device__ __forceinline__ double exp_scaled_f64(double y, const double *tab) {
+    const double jn = rint(y);
+    const double r = y - jn;  // exact
+    double t = fma(1.2126800489957935e-15, r, 2.239395190875157e-12);  // (ln2/256)^k / k!
+    t = fma(t, r, 3.3083026805413713e-09);
+    t = fma(t, r, 3.6655655969101062e-06);
+    t = fma(t, r, 0.0027076061740622863);
+    const double pr = fma(t, r, 1.0);
+    const int j = (int) jn;  // saturates for huge |y|: the ldexp below then returns 0
+    return ldexp(tab[j & 255] * pr, j >> 8);
+}
+
 __device__ __forceinline__ void glds16(const void *src, void *lds_dst) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *) src,
                                      (__attribute__((address_space(3))) void *) lds_dst, 16, 0, 0);
@@ -56,6 +144,8 @@ __global__ __launch_bounds__(256, 2) void kp_tile_kernel(kfun<T> kf, const T *__
     constexpr int OFF_PN = 4 * PANEL;              // p_I, p_J, n_I, n_J
     constexpr int OFF_RED = OFF_PN + 4 * KP_TILE;  // rowbuf[2][128], colbuf[2][128]
     __shared__ __attribute__((aligned(16))) T smem[OFF_RED + 4 * KP_TILE];
+    constexpr bool FAST_EXP = (KERNEL == 2) && sizeof(T) == 8;
+    __shared__ double exp_tab[FAST_EXP ? 256 : 1];
 
     if (status != nullptr && status->converged) return;
 
@@ -103,6 +193,9 @@ __global__ __launch_bounds__(256, 2) void kp_tile_kernel(kfun<T> kf, const T *__
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     smem[OFF_PN + tid] = pin;
     smem[OFF_PN + 2 * KP_TILE + tid] = nin;
+    if constexpr (FAST_EXP) {
+        exp_tab[tid] = c_exp2_256[tid];  // 256 threads; visible after the first K-loop barrier
+    }
 
     const int64_t nk = d_pad / BK;
     for (int64_t kc = 0; kc < nk; ++kc) {
@@ -137,6 +230,11 @@ __global__ __launch_bounds__(256, 2) void kp_tile_kernel(kfun<T> kf, const T *__
         nj[nt] = nJ[jl];
     }
     T cs[4] = { 0, 0, 0, 0 };
+    // fast fp64 RBF: y_ij = 2 g K256 * G_ij + (a_i + b_j), a_i = -g K256 n_i, b_j = -g K256 n_j
+    T bj[4];
+    const T c2 = FAST_EXP ? T(2) * kf.gamma * T(K256) : T(0);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bj[nt] = FAST_EXP ? -kf.gamma * T(K256) * nj[nt] : T(0);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
@@ -144,10 +242,15 @@ __global__ __launch_bounds__(256, 2) void kp_tile_kernel(kfun<T> kf, const T *__
             const int il = wr * 64 + mt * 16 + M::row(lane, r);
             const T pi = pI[il];
             const T ni = nI[il];
+            const T ai = FAST_EXP ? -kf.gamma * T(K256) * ni : T(0);
             T s = 0;
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
-                const T kv = kernel_apply<T>(KERNEL, kf.degree, kf.gamma, kf.coef0, acc[mt][nt][r], ni, nj[nt]);
+                T kv;
+                if constexpr (FAST_EXP)
+                    kv = (T) exp_scaled_f64(fma(c2, acc[mt][nt][r], ai + bj[nt]), exp_tab);
+                else
+                    kv = kernel_apply<T>(KERNEL, kf.degree, kf.gamma, kf.coef0, acc[mt][nt][r], ni, nj[nt]);
                 s = fma(kv, pj[nt], s);
                 cs[nt] = fma(kv, pi, cs[nt]);
             }
