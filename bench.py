@@ -23,8 +23,10 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-import plssvm_sparse_fp22_amd as pm  # noqa: E402  (loads libplssvm_mi355x.so before torch)
+import plssvm_sparse_fp22_amd as pm  # noqa: E402
 from plssvm_sparse_fp22_amd import datagen  # noqa: E402
+
+pm._abi.lib()  # load libplssvm_mi355x.so (and its RCCL, /opt/rocm/lib) before torch brings its own librccl
 
 PEAKS = {"f64": 78.6e12, "f32": 157.3e12, "hbm": 8.0e12}  # MI355X_MICROARCH.md (dense MFMA, HBM3E)
 METRIC = "CG iters/sec + implicit K·p HBM GB/s vs roofline, N×d stated, 1/2/4/8 GPU"
@@ -85,8 +87,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="dense_rbf_100k", choices=sorted(CONFIGS))
-    ap.add_argument("--n", type=int, default=0, help="override number of points")
-    ap.add_argument("--d", type=int, default=0, help="override number of features")
+    ap.add_argument("--points", type=int, default=0, help="override number of points (N)")
+    ap.add_argument("--features", type=int, default=0, help="override number of features (d)")
     ap.add_argument("--kernel", choices=["linear", "polynomial", "rbf"], default=None,
                     help="override the configuration's kernel function (ablations)")
     ap.add_argument("--kp-reps", type=int, default=3)
@@ -114,13 +116,15 @@ def main():
     if args.kernel:
         cfg = (args.kernel,) + tuple(cfg[1:])
     kernel, _, _, dtype, layout, _, desc = cfg
-    p, n, d, y, extra = make_problem(cfg, args.n, args.d, rank)
+    p, n, d, y, extra = make_problem(cfg, args.points, args.features, rank)
     sim = None
     if args.sim_rank:
         if world > 1:
             raise SystemExit("--sim-rank is a single-process option")
         sim = tuple(int(v) for v in args.sim_rank.split("/"))
-    svm = pm.CSVM(p, device=local_rank, rank=rank, world_size=world, uid=uid, sim_rank=sim)
+    ndev = pm.device_count()
+    device = local_rank % ndev if ndev > 0 else local_rank  # more ranks than GPUs: share (rehearsal only)
+    svm = pm.CSVM(p, device=device, rank=rank, world_size=world, uid=uid, sim_rank=sim)
     share = sim[1] if sim else world  # the work split divides the implicit matrix by this
     t0 = time.time()
     svm.setup_data_on_device()
