@@ -155,7 +155,7 @@ void engine<T>::setup_dense(const T *X, int64_t n_, int64_t d_) {
     m = n - 1;
     nb = ceil_div(m, KP_TILE);
     n_pad = std::max<int64_t>(nb, 1) * KP_TILE;
-    d_pad = round_up(d, kp_bk<T>());
+    d_pad = round_up(d, kp_dpad<T>());
     // device layout: feature-major XT[d_pad][n_pad] of the first m points; the last point separately
     // (the reference's data_d_ / data_last_d_, gpu_csvm.cpp:142-155, with 64-bit offsets and tile padding)
     XT.alloc(d_pad * n_pad, stream);

@@ -128,15 +128,20 @@ __device__ __forceinline__ void glds16(const void *src, void *lds_dst) {
                                      (__attribute__((address_space(3))) void *) lds_dst, 16, 0, 0);
 }
 
+// occupancy: 3 workgroups per CU (43 KB LDS, <= 168 VGPRs) hide the chunk barriers / DMA waits best;
+// the fp64 RBF epilogue needs more registers than that (it spills), so it runs 2 per CU
 template <typename T, int KERNEL>
-__global__ __launch_bounds__(256, 2) void kp_tile_kernel(kfun<T> kf, const T *__restrict__ XT,
+constexpr int kp_waves_per_eu() { return (KERNEL == 2 && sizeof(T) == 8) ? 2 : 3; }
+
+template <typename T, int KERNEL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_per_eu<T, KERNEL>(), kp_waves_per_eu<T, KERNEL>()))) void kp_tile_kernel(kfun<T> kf, const T *__restrict__ XT,
                                                          const T *__restrict__ norms, const T *__restrict__ p,
                                                          T *__restrict__ partial, int64_t n_pad, int64_t d_pad,
                                                          int64_t nb, int64_t s0,
                                                          const cg_scalars<T> *__restrict__ status) {
     using M = mfma16<T>;
     using acc_t = typename M::acc_t;
-    constexpr int BK = kp_bk<T>();
+    constexpr int BK = kp_bk<T, KERNEL>();
     constexpr int PANEL = BK * KP_TILE;            // elements of one [BK][128] panel
     constexpr int EPP = 1024 / (int) sizeof(T);    // elements per 1 KiB wave-instruction
     constexpr int PIECES = PANEL / EPP / 4;        // wave-instructions per wave per panel
@@ -168,18 +173,24 @@ __global__ __launch_bounds__(256, 2) void kp_tile_kernel(kfun<T> kf, const T *__
     const T pin = p[pidx];
     const T nin = (KERNEL == 2) ? norms[pidx] : T(0);
 
+    // per-lane byte offsets of this wave's DMA pieces inside a chunk (32-bit, reused for every chunk
+    // and both panels: the chunk / panel bases are wave-uniform, so the loads use saddr + voffset)
+    uint32_t doff[PIECES];
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j) {
+        const int elem = (w * PIECES + j) * EPP + lane * VEC;
+        doff[j] = (uint32_t) (((int64_t) (elem / KP_TILE) * n_pad + elem % KP_TILE) * (int64_t) sizeof(T));
+    }
     auto issue = [&](int64_t kc, int buf) {
-        const int64_t k0 = kc * BK;
+        const char *ba = reinterpret_cast<const char *>(XT + kc * BK * n_pad + I0);
+        const char *bb = reinterpret_cast<const char *>(XT + kc * BK * n_pad + J0);
         T *pa = smem + (2 * buf) * PANEL;
         T *pb = pa + PANEL;
 #pragma unroll
         for (int j = 0; j < PIECES; ++j) {
             const int u = w * PIECES + j;
-            const int elem = u * EPP + lane * VEC;
-            const int row = elem / KP_TILE, col = elem % KP_TILE;
-            const T *src = XT + (k0 + row) * n_pad + col;
-            glds16(src + I0, pa + u * EPP);
-            glds16(src + J0, pb + u * EPP);
+            glds16(ba + doff[j], pa + u * EPP);
+            glds16(bb + doff[j], pb + u * EPP);
         }
     };
 
@@ -308,6 +319,9 @@ template <typename T>
 void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *partial, int64_t n_pad, int64_t d_pad,
                      int64_t nb, int64_t s0, int64_t nsuper, const cg_scalars<T> *status, hipStream_t s) {
     if (nsuper <= 0 || nb <= 0) return;
+    // 32-bit DMA offsets inside a chunk (kp_tile_kernel): (BK - 1) rows of n_pad plus a tile row
+    if ((int64_t) kp_dpad<T>() * n_pad * (int64_t) sizeof(T) >= ((int64_t) 1 << 31))
+        throw mi_error(-5, "too many points for the pairwise tile kernel's 32-bit chunk offsets");
     const dim3 grid((unsigned) (nsuper * KP_SUPER * KP_SUPER)), block(256);
     switch (kf.kernel) {
         case 0:
