@@ -38,7 +38,7 @@ __device__ __forceinline__ T kernel_apply(int kernel, int degree, T gamma, T coe
 // exp for the fp64 RBF epilogue, in the scaled domain y = x * 256 / ln2 (x = -gamma * dist <= 0):
 // exp(x) = 2^(j >> 8) * 2^((j & 255) / 256) * e^(r ln2 / 256), j = rint(y), r = y - j in [-1/2, 1/2];
 // 2^(i/256) from a 256-entry LDS table (correctly rounded), e^(r ln2/256) by a degree-4 polynomial
-// (truncation < 4e-17 relative). 11 fp64 VALU + 3 integer + 1 LDS read per element instead of ~26
+// (truncation < 4e-17 relative). 9 fp64 VALU + 3 integer + 1 LDS read per element instead of ~26
 // for dist + libm exp: on gfx950 every VALU cycle of the epilogue is a cycle of the fp64 MFMA pipe
 // (DESIGN.md §3.1), so the instruction count is what matters. No clamp of y at 0: the norm trick can
 // round dist to -1e-16 relative, giving exp of a tiny positive number (as harmless as the clamp).
@@ -114,8 +114,7 @@ constexpr double K256 = 369.3299304675746;  // 256 / ln 2
 __device__ __forceinline__ double exp_scaled_f64(double y, const double *tab) {
     const double jn = rint(y);
     const double r = y - jn;  // exact
-    double t = fma(1.2126800489957935e-15, r, 2.239395190875157e-12);  // (ln2/256)^k / k!
-    t = fma(t, r, 3.3083026805413713e-09);
+    double t = fma(2.239395190875157e-12, r, 3.3083026805413713e-09);  // (ln2/256)^k / k!, k = 4..1
     t = fma(t, r, 3.6655655969101062e-06);
     t = fma(t, r, 0.0027076061740622863);
     const double pr = fma(t, r, 1.0);
@@ -146,9 +145,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
     constexpr int EPP = 1024 / (int) sizeof(T);    // elements per 1 KiB wave-instruction
     constexpr int PIECES = PANEL / EPP / 4;        // wave-instructions per wave per panel
     constexpr int VEC = 16 / (int) sizeof(T);
-    constexpr int OFF_PN = 4 * PANEL;              // p_I, p_J, n_I, n_J
-    constexpr int OFF_RED = OFF_PN + 4 * KP_TILE;  // rowbuf[2][128], colbuf[2][128]
-    __shared__ __attribute__((aligned(16))) T smem[OFF_RED + 4 * KP_TILE];
+    // LDS: p_I, p_J, n_I, n_J, then the two double-buffered panel pairs; once the K loop is done the
+    // epilogue's reduction buffers overlay the panels: row partials [wc][128 rows][16 (+1 pad)],
+    // column partials [wr][128 cols][4 (+1 pad)]
+    constexpr int OFF_PAN = 4 * KP_TILE;
+    constexpr int RSTR = 17, RHALF = KP_TILE * RSTR + 1, CSTR = 5;
+    constexpr int RED = 2 * RHALF + 2 * KP_TILE * CSTR;
+    constexpr int SMEM = OFF_PAN + (4 * PANEL > RED ? 4 * PANEL : RED);
+    __shared__ __attribute__((aligned(16))) T smem[SMEM];
     constexpr bool FAST_EXP = (KERNEL == 2) && sizeof(T) == 8;
     __shared__ double exp_tab[FAST_EXP ? 256 : 1];
 
@@ -172,6 +176,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
     const int64_t pidx = (tid < KP_TILE) ? I0 + tid : J0 + (tid - KP_TILE);
     const T pin = p[pidx];
     const T nin = (KERNEL == 2) ? norms[pidx] : T(0);
+    // fast fp64 RBF: the accumulators start at -n_j / 2 (column j = lane & 15 of every block), so they
+    // end at g_ij - n_j / 2 and y_ij = 2 g K256 (g_ij - n_j / 2) - g K256 n_i is one fma per element
+    T acc0[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+        acc0[nt] = FAST_EXP ? T(-0.5) * norms[J0 + wc * 64 + nt * 16 + (lane & 15)] : T(0);
 
     // per-lane byte offsets of this wave's DMA pieces inside a chunk (32-bit, reused for every chunk
     // and both panels: the chunk / panel bases are wave-uniform, so the loads use saddr + voffset)
@@ -184,7 +194,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
     auto issue = [&](int64_t kc, int buf) {
         const char *ba = reinterpret_cast<const char *>(XT + kc * BK * n_pad + I0);
         const char *bb = reinterpret_cast<const char *>(XT + kc * BK * n_pad + J0);
-        T *pa = smem + (2 * buf) * PANEL;
+        T *pa = smem + OFF_PAN + (2 * buf) * PANEL;
         T *pb = pa + PANEL;
 #pragma unroll
         for (int j = 0; j < PIECES; ++j) {
@@ -198,12 +208,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = acc_t{ 0, 0, 0, 0 };
+        for (int b = 0; b < 4; ++b) acc[a][b] = acc_t{ acc0[b], acc0[b], acc0[b], acc0[b] };
 
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    smem[OFF_PN + tid] = pin;
-    smem[OFF_PN + 2 * KP_TILE + tid] = nin;
+    smem[tid] = pin;
+    smem[2 * KP_TILE + tid] = nin;
     if constexpr (FAST_EXP) {
         exp_tab[tid] = c_exp2_256[tid];  // 256 threads; visible after the first K-loop barrier
     }
@@ -213,7 +223,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
         if (kc > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // chunk kc visible to all waves; every wave is done reading chunk kc-1
         if (kc + 1 < nk) issue(kc + 1, (int) ((kc + 1) & 1));
-        const T *A = smem + (2 * (kc & 1)) * PANEL;
+        const T *A = smem + OFF_PAN + (2 * (kc & 1)) * PANEL;
         const T *B = A + PANEL;
 #pragma unroll
         for (int ks = 0; ks < BK / 4; ++ks) {
@@ -230,22 +240,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
         }
     }
 
-    // ---- epilogue: kernel function, times p, row and column sums ----
-    const T *pI = smem + OFF_PN, *pJ = pI + KP_TILE, *nI = pI + 2 * KP_TILE, *nJ = pI + 3 * KP_TILE;
-    T *rowbuf = smem + OFF_RED, *colbuf = rowbuf + 2 * KP_TILE;
+    // ---- epilogue: kernel function, times p, row and column partial sums ----
+    const T *pI = smem, *pJ = smem + KP_TILE, *nI = smem + 2 * KP_TILE, *nJ = smem + 3 * KP_TILE;
     T pj[4], nj[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
         const int jl = wc * 64 + nt * 16 + (lane & 15);
         pj[nt] = pJ[jl];
-        nj[nt] = nJ[jl];
+        nj[nt] = (KERNEL == 2 && !FAST_EXP) ? nJ[jl] : T(0);
     }
     T cs[4] = { 0, 0, 0, 0 };
-    // fast fp64 RBF: y_ij = 2 g K256 * G_ij + (a_i + b_j), a_i = -g K256 n_i, b_j = -g K256 n_j
-    T bj[4];
     const T c2 = FAST_EXP ? T(2) * kf.gamma * T(K256) : T(0);
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) bj[nt] = FAST_EXP ? -kf.gamma * T(K256) * nj[nt] : T(0);
+    // Each row has 32 partials (16 lanes x 2 column-half waves), each column 8 (4 lane groups x 2
+    // row-half waves). They are parked in LDS and every thread then sums one half-row and one
+    // half-column: ~20 adds per lane instead of a 4-level shuffle tree per row (64 adds + 128
+    // ds_bpermute); the fixed summation order keeps K·p bitwise reproducible.
+    __syncthreads();  // every wave is done with the last K chunk: the panels become reduction buffers
+    T *rowp = smem + OFF_PAN + wc * RHALF;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
@@ -259,36 +270,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
             for (int nt = 0; nt < 4; ++nt) {
                 T kv;
                 if constexpr (FAST_EXP)
-                    kv = (T) exp_scaled_f64(fma(c2, acc[mt][nt][r], ai + bj[nt]), exp_tab);
+                    kv = (T) exp_scaled_f64(fma(c2, acc[mt][nt][r], ai), exp_tab);
                 else
                     kv = kernel_apply<T>(KERNEL, kf.degree, kf.gamma, kf.coef0, acc[mt][nt][r], ni, nj[nt]);
                 s = fma(kv, pj[nt], s);
                 cs[nt] = fma(kv, pi, cs[nt]);
             }
-            // lanes sharing (lane >> 4) hold the same row: reduce over lane & 15
-            s += __shfl_xor(s, 1);
-            s += __shfl_xor(s, 2);
-            s += __shfl_xor(s, 4);
-            s += __shfl_xor(s, 8);
-            if ((lane & 15) == 0) rowbuf[wc * KP_TILE + il] = s;
+            rowp[il * RSTR + (lane & 15)] = s;
         }
     }
     if (!diag) {
+        T *colp = smem + OFF_PAN + 2 * RHALF + wr * KP_TILE * CSTR;
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {  // lanes sharing (lane & 15) hold the same column
-            T v = cs[nt];
-            v += __shfl_xor(v, 16);
-            v += __shfl_xor(v, 32);
-            if (lane < 16) colbuf[wr * KP_TILE + wc * 64 + nt * 16 + lane] = v;
-        }
+        for (int nt = 0; nt < 4; ++nt) colp[(wc * 64 + nt * 16 + (lane & 15)) * CSTR + (lane >> 4)] = cs[nt];
     }
     __syncthreads();
-    if (tid < KP_TILE) {
-        partial[J * n_pad + I0 + tid] = rowbuf[tid] + rowbuf[KP_TILE + tid];
-    } else if (!diag) {
-        const int t = tid - KP_TILE;
-        partial[I * n_pad + J0 + t] = colbuf[t] + colbuf[KP_TILE + t];
+    const int q = tid >> 1, h = tid & 1;  // row / column q of the tile, half h
+    const T *rp = smem + OFF_PAN + h * RHALF + q * RSTR;
+    T a = rp[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) a += rp[k];
+    a += __shfl_xor(a, 1);
+    if (!diag) {
+        const T *cp = smem + OFF_PAN + 2 * RHALF + (h * KP_TILE + q) * CSTR;
+        T c = (cp[0] + cp[1]) + (cp[2] + cp[3]);
+        c += __shfl_xor(c, 1);
+        if (h == 1) partial[I * n_pad + J0 + q] = c;
     }
+    if (h == 0) partial[J * n_pad + I0 + q] = a;
 }
 
 template <typename T>
