@@ -26,10 +26,10 @@ struct cg_scalars {
 // ---- dense pairwise tiles -----------------------------------------------------------------------
 // tile edge of the implicit Q~ tiles (rows and columns); n_pad is a multiple of this.
 constexpr int KP_TILE = 128;
-// K-chunk depth of the pairwise tile kernel: 8 (fp64) / 16 (fp32) keeps LDS at 43 KB for 3
-// workgroups per CU; the fp64 RBF variant runs 2 per CU (registers) and takes 16-deep chunks
+// K-chunk depth of the pairwise tile kernel: 8 (fp64) / 16 (fp32) keeps LDS at <= 49 KB for 3
+// workgroups per CU
 template <typename T, int KERNEL>
-constexpr int kp_bk() { return sizeof(T) == 8 ? (KERNEL == 2 ? 16 : 8) : 16; }
+constexpr int kp_bk() { return sizeof(T) == 8 ? 8 : 16; }
 // feature padding of the device layout: a multiple of every chunk depth
 template <typename T>
 constexpr int kp_dpad() { return 16; }

@@ -127,10 +127,11 @@ __device__ __forceinline__ void glds16(const void *src, void *lds_dst) {
                                      (__attribute__((address_space(3))) void *) lds_dst, 16, 0, 0);
 }
 
-// occupancy: 3 workgroups per CU (43 KB LDS, <= 168 VGPRs) hide the chunk barriers / DMA waits best;
-// the fp64 RBF epilogue needs more registers than that (it spills), so it runs 2 per CU
+// occupancy: 3 workgroups per CU (<= 49 KB LDS, <= 168 VGPRs) hide the chunk barriers / DMA waits
+// best; the fp64 RBF variant spills a few epilogue values at that budget (outside the K loop), and
+// still runs as fast as with 2 workgroups and 16-deep chunks
 template <typename T, int KERNEL>
-constexpr int kp_waves_per_eu() { return (KERNEL == 2 && sizeof(T) == 8) ? 2 : 3; }
+constexpr int kp_waves_per_eu() { return 3; }
 
 template <typename T, int KERNEL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_per_eu<T, KERNEL>(), kp_waves_per_eu<T, KERNEL>()))) void kp_tile_kernel(kfun<T> kf, const T *__restrict__ XT,
