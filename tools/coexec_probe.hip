@@ -13,7 +13,7 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // MODE 0: MFMA only (all 8 waves)      1: MFMA + NV fp64 FMAs per step in the same wave
 // MODE 2: waves 0-3 MFMA, waves 4-7 fp64 FMA only (NV per step)
 // MODE 3: waves 0-3 MFMA only, waves 4-7 idle     4: waves 0-3 MFMA, waves 4-7 fp32 FMA only
-// MODE 5: waves 0-3 MFMA, waves 4-7 int32 ops only
+// MODE 5: waves 0-3 MFMA, waves 4-7 int32 ops only   6 / 7: fp64 / fp32 FMA only in all waves
 template <int MODE, int NV>
 __global__ __launch_bounds__(512) void probe(double *out, int iters, double a0) {
     const int wave = threadIdx.x >> 6;
@@ -26,7 +26,7 @@ __global__ __launch_bounds__(512) void probe(double *out, int iters, double a0) 
     int vi[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = a0 * (k + 1), vf[k] = (float) v[k], vi[k] = k + threadIdx.x;
-    const bool mfma_wave = (MODE == 0 || MODE == 1) || wave < 4;
+    const bool mfma_wave = MODE < 6 && ((MODE == 0 || MODE == 1) || wave < 4);
     if (mfma_wave) {
         for (int i = 0; i < iters; ++i) {
 #pragma unroll
@@ -45,6 +45,14 @@ __global__ __launch_bounds__(512) void probe(double *out, int iters, double a0) 
         for (int i = 0; i < iters; ++i) {
 #pragma unroll
             for (int j = 0; j < NV; ++j) vf[j & 7] = fmaf(vf[j & 7], 1.0000001f, 1e-9f);
+        }
+    } else if (MODE == 6 || MODE == 7) {  // no MFMA anywhere: fp64 (6) / fp32 (7) FMA throughput alone
+        for (int i = 0; i < iters; ++i) {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+                if (MODE == 6) v[j & 7] = fma(v[j & 7], 1.0000001, 1e-9);
+                else vf[j & 7] = fmaf(vf[j & 7], 1.0000001f, 1e-9f);
+            }
         }
     } else if (MODE == 5) {
         for (int i = 0; i < iters; ++i) {
@@ -86,5 +94,7 @@ int main() {
     printf("MODE2 mfma 0-3 / 64 f64 fma in waves 4-7    %.3f ms\n", run<2, 64>(out, iters));
     printf("MODE4 mfma 0-3 / 64 f32 fma in waves 4-7    %.3f ms\n", run<4, 64>(out, iters));
     printf("MODE5 mfma 0-3 / 64 int ops in waves 4-7    %.3f ms\n", run<5, 64>(out, iters));
+    printf("MODE6 no mfma, 64 f64 fma per step, 8 waves %.3f ms\n", run<6, 64>(out, iters));
+    printf("MODE7 no mfma, 64 f32 fma per step, 8 waves %.3f ms\n", run<7, 64>(out, iters));
     return 0;
 }
