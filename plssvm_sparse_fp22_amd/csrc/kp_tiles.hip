@@ -311,7 +311,16 @@ __global__ __launch_bounds__(256) void kp_reduce_kernel(const T *__restrict__ pa
     if (i >= m) return;
     T s = 0;
     if (s0 == 0 && s1 == s_total) {
-        for (int64_t c = 0; c < nb; ++c) s += partial[c * n_pad + i];
+        // 8 slab rows in flight per step (one thread per i: memory parallelism sets the speed)
+        int64_t c = 0;
+        for (; c + 8 <= nb; c += 8) {
+            T v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = partial[(c + u) * n_pad + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; c < nb; ++c) s += partial[c * n_pad + i];
     } else {
         const int64_t RS = (i / KP_TILE) / KP_SUPER;
         for (int64_t c = 0; c < nb; ++c) {
