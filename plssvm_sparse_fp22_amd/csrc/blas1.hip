@@ -144,7 +144,155 @@ __global__ __launch_bounds__(256) void cg_direction_kernel(T *__restrict__ d, co
     d[i] = t + r[i];
 }
 
+// block_sum with the total broadcast to every thread
+template <typename T>
+__device__ __forceinline__ T block_sum_all(T v, T *red, T *bc) {
+    const T s = block_sum(v, red);
+    if (threadIdx.x == 0) *bc = s;
+    __syncthreads();
+    const T out = *bc;
+    __syncthreads();
+    return out;
+}
+
+// the RED_BLOCKS partial pairs of a dot2_kernel-shaped producer, summed as dot_final_kernel does
+template <typename T>
+__device__ __forceinline__ void partials_total(const T *__restrict__ partials, T *red, T *bc, T &r1, T &r2) {
+    T s1 = 0, s2 = 0;
+    for (int i = threadIdx.x; i < RED_BLOCKS; i += blockDim.x) {
+        s1 += partials[i];
+        s2 += partials[RED_BLOCKS + i];
+    }
+    r1 = block_sum_all(s1, red, bc);
+    r2 = block_sum_all(s2, red, bc);
+}
+
+template <typename T>
+__device__ __forceinline__ void store_partials(T v1, T v2, T *red, T *__restrict__ partials) {
+    const T r1 = block_sum(v1, red);
+    __syncthreads();
+    const T r2 = block_sum(v2, red);
+    if (threadIdx.x == 0) {
+        partials[blockIdx.x] = r1;
+        partials[RED_BLOCKS + blockIdx.x] = r2;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void cg_fin_dad_kernel(const T *__restrict__ raw, const T *__restrict__ q,
+                                                         const T *__restrict__ d, const T *__restrict__ psum,
+                                                         T QA_cost, T cost_inv, int raw_only, int64_t m,
+                                                         T *__restrict__ Ad, T *__restrict__ pdad,
+                                                         cg_scalars<T> *sc) {
+    if (sc->converged) return;
+    __shared__ T red[8], bc[1];
+    T sp, sqp;
+    partials_total(psum, red, bc, sp, sqp);
+    if (blockIdx.x == 0 && threadIdx.x == 0) sc->sp = sp, sc->sqp = sqp;
+    T s1 = 0;
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t) gridDim.x * blockDim.x) {
+        T v;
+        {
+#pragma clang fp contract(fast)  // kp_finalize_kernel's expression, contracted as in dense.hip
+            v = raw_only ? raw[i] : raw[i] + (QA_cost - q[i]) * sp - sqp + cost_inv * d[i];
+            v = T(0) + T(1) * v;
+        }
+        Ad[i] = v;
+        s1 += d[i] * v;
+    }
+    store_partials(s1, T(0), red, pdad);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void cg_upd_rr_kernel(T *__restrict__ x, T *__restrict__ r, const T *__restrict__ d,
+                                                        const T *__restrict__ Ad, const T *__restrict__ b, int reset,
+                                                        const T *__restrict__ pdad, int64_t m, T *__restrict__ prr,
+                                                        cg_scalars<T> *sc) {
+    if (sc->converged) return;
+    __shared__ T red[8], bc[1];
+    T dAd, unused;
+    partials_total(pdad, red, bc, dAd, unused);
+    const T delta = sc->delta;
+    const T alpha = delta / dAd;
+    if (blockIdx.x == 0 && threadIdx.x == 0) sc->dAd = dAd, sc->alpha = alpha, sc->delta_prev = delta;
+    T s1 = 0;
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t) gridDim.x * blockDim.x) {
+        const T t = alpha * d[i];
+        x[i] = x[i] + t;
+        if (reset) {
+            r[i] = b[i];
+        } else {
+            const T u = alpha * Ad[i];
+            const T rn = r[i] - u;
+            r[i] = rn;
+            s1 += rn * rn;
+        }
+    }
+    if (!reset) store_partials(s1, T(0), red, prr);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void cg_dir_sums_kernel(T *__restrict__ d, const T *__restrict__ r,
+                                                          const T *__restrict__ q, const T *__restrict__ prr, int init,
+                                                          int64_t run, double *trace, int64_t trace_cap, int64_t m,
+                                                          T *__restrict__ psum, cg_scalars<T> *sc) {
+    if (sc->converged) return;
+    __shared__ T red[8], bc[1];
+    T beta = 0;
+    if (!init) {
+        T rr, unused;
+        partials_total(prr, red, bc, rr, unused);
+        const bool conv = rr <= sc->eps2delta0;
+        beta = rr / sc->delta_prev;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {  // FIN_DELTA of dot_final_kernel
+            sc->delta = rr;
+            sc->iters = run + 1;
+            if (trace && run + 1 < trace_cap) trace[run + 1] = (double) rr;
+            if (conv) sc->converged = 1;
+            else sc->beta = beta;
+        }
+        if (conv) return;  // the same decision in every block
+    }
+    T s1 = 0, s2 = 0;
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t) gridDim.x * blockDim.x) {
+        T dn;
+        if (init) {
+            dn = r[i];
+        } else {
+            const T t = beta * d[i];
+            dn = t + r[i];
+        }
+        d[i] = dn;
+        s1 += dn;
+        s2 += q[i] * dn;
+    }
+    store_partials(s1, s2, red, psum);
+}
+
 }  // namespace
+
+template <typename T>
+void launch_cg_fin_dad(const T *raw, const T *q, const T *d, const T *psum, T QA_cost, T cost_inv, int raw_only,
+                       int64_t m, T *Ad, T *pdad, cg_scalars<T> *sc, hipStream_t s) {
+    hipLaunchKernelGGL(cg_fin_dad_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, s, raw, q, d, psum, QA_cost, cost_inv,
+                       raw_only, m, Ad, pdad, sc);
+    MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_cg_upd_rr(T *x, T *r, const T *d, const T *Ad, const T *b, int reset, const T *pdad, int64_t m, T *prr,
+                      cg_scalars<T> *sc, hipStream_t s) {
+    hipLaunchKernelGGL(cg_upd_rr_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, s, x, r, d, Ad, b, reset, pdad, m, prr, sc);
+    MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int init, int64_t run, double *trace,
+                        int64_t trace_cap, int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s) {
+    hipLaunchKernelGGL(cg_dir_sums_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, s, d, r, q, prr, init, run, trace,
+                       trace_cap, m, psum, sc);
+    MI_LAUNCH_CHECK();
+}
 
 template <typename T>
 void launch_dot2(const T *a, const T *b, const T *c, const T *e, int64_t n, T *partials, const cg_scalars<T> *status,
@@ -200,7 +348,13 @@ void launch_cg_direction(T *d, const T *r, int64_t m, const cg_scalars<T> *sc, h
     template void launch_copy<T>(const T *, int64_t, T *, const cg_scalars<T> *, hipStream_t);                    \
     template void launch_cg_update<T>(T *, T *, const T *, const T *, const T *, int, int64_t,                    \
                                       const cg_scalars<T> *, hipStream_t);                                        \
-    template void launch_cg_direction<T>(T *, const T *, int64_t, const cg_scalars<T> *, hipStream_t);
+    template void launch_cg_direction<T>(T *, const T *, int64_t, const cg_scalars<T> *, hipStream_t);             \
+    template void launch_cg_fin_dad<T>(const T *, const T *, const T *, const T *, T, T, int, int64_t, T *, T *,    \
+                                       cg_scalars<T> *, hipStream_t);                                               \
+    template void launch_cg_upd_rr<T>(T *, T *, const T *, const T *, const T *, int, const T *, int64_t, T *,      \
+                                      cg_scalars<T> *, hipStream_t);                                                \
+    template void launch_cg_dir_sums<T>(T *, const T *, const T *, const T *, int, int64_t, double *, int64_t,      \
+                                        int64_t, T *, cg_scalars<T> *, hipStream_t);
 INST(float)
 INST(double)
 #undef INST

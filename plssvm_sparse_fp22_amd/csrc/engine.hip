@@ -80,6 +80,7 @@ engine<T>::engine(int kernel_, int degree_, double gamma_, double coef0_, double
     MI_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     sc.alloc(1, stream);
     red.alloc(2 * RED_BLOCKS, stream);
+    cgp.alloc(6 * RED_BLOCKS, stream);
 }
 
 template <typename T>
@@ -246,6 +247,14 @@ void engine<T>::kp_device(const T *p, T *out, T add, bool overwrite, const cg_sc
     // sum(p) and sum(q p): the rank-1 parts of Q~ (QA_cost - q_i - q_j) never enter the tiles
     launch_dot2<T>(p, nullptr, q.get(), p, m, red.get(), status, stream);
     launch_dot_final<T>(red.get(), scp, FIN_SP_SQP, 0, nullptr, 0, nullptr, stream);
+    kp_raw(p, status);
+    const int flags = (overwrite ? 1 : 0) | ((sim_world > 0 && sim_rank != 0) ? 2 : 0);
+    launch_kp_finalize<T>(raw.get(), q.get(), p, scp, QA_cost, cost_inv(), add, flags, m, out, status, stream);
+}
+
+template <typename T>
+void engine<T>::kp_raw(const T *p, const cg_scalars<T> *status) {
+    if (m <= 0) return;
     if (sparse) {
         sparse_kp_raw(p, status);
     } else if (factored()) {
@@ -259,8 +268,6 @@ void engine<T>::kp_device(const T *p, T *out, T add, bool overwrite, const cg_sc
         launch_kp_reduce<T>(partial.get(), nb, n_pad, m, t0, t1, raw.get(), status, stream);
         allreduce(raw.get(), m);
     }
-    const int flags = (overwrite ? 1 : 0) | ((sim_world > 0 && sim_rank != 0) ? 2 : 0);
-    launch_kp_finalize<T>(raw.get(), q.get(), p, scp, QA_cost, cost_inv(), add, flags, m, out, status, stream);
 }
 
 template <typename T>
@@ -298,7 +305,8 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
     // delta = r.r ; delta0 ; d = r   (:92-97)
     launch_dot2<T>(r.get(), r.get(), nullptr, nullptr, m, red.get(), nullptr, stream);
     launch_dot_final<T>(red.get(), sc.get(), FIN_DELTA0, 0, trace.get(), trace_cap, nullptr, stream);
-    launch_copy<T>(r.get(), m, dv.get(), nullptr, stream);
+    // d = r, with sum d / sum q d for the first Q~d
+    launch_cg_dir_sums<T>(dv.get(), r.get(), q.get(), nullptr, 1, 0, nullptr, 0, m, cgp.get(), sc.get(), stream);
     run = 0;
     cg_active = true;
     if (delta0_out) {
@@ -314,21 +322,23 @@ void engine<T>::cg_step(int64_t nsteps, bool &converged, int64_t &iters) {
     if (!cg_active) throw mi_error(-6, "cg_step without cg_begin");
     MI_HIP_CHECK(hipSetDevice(device));
     const cg_scalars<T> *st = sc.get();
-    for (int64_t s = 0; s < nsteps; ++s, ++run) {
-        // Ad = Q~ d   (:111-113)
-        kp_device(dv.get(), Ad.get(), T(1), true, st);
-        // alpha = delta / (d . Ad)   (:116)
-        launch_dot2<T>(dv.get(), Ad.get(), nullptr, nullptr, m, red.get(), st, stream);
-        launch_dot_final<T>(red.get(), sc.get(), FIN_ALPHA, run, nullptr, 0, nullptr, stream);
+    T *psum = cgp.get(), *pdad = psum + 2 * RED_BLOCKS, *prr = psum + 4 * RED_BLOCKS;
+    const int raw_only = (sim_world > 0 && sim_rank != 0) ? 1 : 0;
+    for (int64_t s = 0; s < nsteps; ++s, ++run) {  // m == 0: the kernels see no elements, converge at once
+        // Ad = Q~ d (:111-113); alpha = delta / (d . Ad) (:116) in the next kernel
+        kp_raw(dv.get(), st);
+        launch_cg_fin_dad<T>(raw.get(), q.get(), dv.get(), psum, QA_cost, cost_inv(), raw_only, m, Ad.get(), pdad,
+                             sc.get(), stream);
         // x += alpha d; r = b - Q~x every 50th iteration, else r -= alpha Ad   (:119-132)
         const int reset = (run % 50 == 49) ? 1 : 0;
-        launch_cg_update<T>(x.get(), r.get(), dv.get(), Ad.get(), b.get(), reset, m, st, stream);
-        if (reset) kp_device(x.get(), r.get(), T(-1), false, st);
-        // delta = r.r ; stop test ; beta   (:135-146)
-        launch_dot2<T>(r.get(), r.get(), nullptr, nullptr, m, red.get(), st, stream);
-        launch_dot_final<T>(red.get(), sc.get(), FIN_DELTA, run, trace.get(), trace_cap, nullptr, stream);
-        // d = beta d + r   (:149-151)
-        launch_cg_direction<T>(dv.get(), r.get(), m, st, stream);
+        launch_cg_upd_rr<T>(x.get(), r.get(), dv.get(), Ad.get(), b.get(), reset, pdad, m, prr, sc.get(), stream);
+        if (reset) {
+            kp_device(x.get(), r.get(), T(-1), false, st);
+            launch_dot2<T>(r.get(), r.get(), nullptr, nullptr, m, prr, st, stream);
+        }
+        // delta = r.r ; stop test ; beta (:135-146); d = beta d + r (:149-151), with sum d / sum q d
+        launch_cg_dir_sums<T>(dv.get(), r.get(), q.get(), prr, 0, run, trace.get(), trace_cap, m, psum, sc.get(),
+                              stream);
     }
     cg_scalars<T> h{};
     MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));

@@ -53,6 +53,7 @@ struct engine : engine_base {
 
     // ---- vectors (n_pad, zero padded) ----
     dev_buf<T> partial, q, pv, ret, x, r, dv, Ad, b, raw, w, red;
+    dev_buf<T> cgp;  // fused CG partials: [0, 2R) sum d / sum q d, [2R, 4R) d.Ad, [4R, 6R) r.r
     dev_buf<cg_scalars<T>> sc;
     dev_buf<double> trace;
     int64_t trace_cap = 0;
@@ -79,6 +80,7 @@ struct engine : engine_base {
 
     // out = (overwrite ? 0 : out) + add * Q~ p  (device vectors, length >= m)
     void kp_device(const T *p, T *out, T add, bool overwrite, const cg_scalars<T> *status);
+    void kp_raw(const T *p, const cg_scalars<T> *status);  // raw = the pairwise / sparse part of Q~ p
     void kp_host(const T *q_host, const T *p, T *ret_host, T add);
 
     void cg_begin(const T *b_host, const T *q_host, T eps, bool force, double *delta0_out, int64_t trace_len);
