@@ -158,6 +158,8 @@ def main():
     roof = roofline(cfg, info, n, d, share, ms_dom, extra)
     tkey = args.config + (f"_sim{sim[0]}of{sim[1]}" if sim else "")
     roof["traffic"], roof["traffic_source"] = pmc_traffic(tkey, n, d, world, roof["kernel"])
+    if roof["bound"] == "mfma":
+        roof["mfma_util"], roof["mfma_util_source"] = pmc_mfma(tkey, n, d, world, kernel)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -243,6 +245,18 @@ def pmc_traffic(config, n, d, world, kernel):
         t = json.load(open(path))
         if t["N"] == n and t["d"] == d and t["n_gpus"] == world and kernel == t["kernel"]:
             return t["hbm_read_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
+def pmc_mfma(config, n, d, world, kernel):
+    """MFMA utilisation of the dense tile kernel from the newest committed PMC pass of this exact
+    workload (profiles/*_<config>_mfma.json, written from tools/pmc_dense.sh), else None."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_mfma.json")), reverse=True):
+        t = json.load(open(path))
+        if t["N"] == n and t["d"] == d and t["n_gpus"] == world and t["kernel"] == kernel:
+            return t["mfma_util"], os.path.relpath(path, ROOT)
     return None, None
 
 
