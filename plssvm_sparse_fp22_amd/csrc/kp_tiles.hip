@@ -4,9 +4,10 @@
 // and its OpenMP twin (src/plssvm/backends/OpenMP/svm_kernel.cpp:21-47). Per 128x128 lower-triangle
 // tile (I >= J) of k(x_i, x_j):
 //   * X is feature-major in HBM (XT[k][i]); each BK-deep K chunk of the two 128-column panels is
-//     streamed global -> LDS with global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPR
-//     staging), double-buffered so chunk kc+1 lands while chunk kc feeds the MFMAs: one barrier
-//     per chunk;
+//     streamed global -> LDS with buffer_load_dwordx4 ... lds (1 KiB per wave-instruction, no VGPR
+//     staging; scalar descriptor base + constant per-lane offset, so no VALU address math in the K
+//     loop), double-buffered so chunk kc+1 lands while chunk kc feeds the MFMAs: one barrier per
+//     chunk;
 //   * 4 waves as 2x2, each a 64x64 sub-tile = 4x4 accumulators of v_mfma_f64_16x16x4_f64 /
 //     v_mfma_f32_16x16x4_f32 (exact fma chains in k order);
 //   * epilogue in registers: kernel function (RBF via ||a||^2 + ||b||^2 - 2 a.b, clamped at 0),
@@ -122,10 +123,13 @@ __device__ __forceinline__ double exp_scaled_f64(double y, const double *tab) {
     return ldexp(tab[j & 255] * pr, j >> 8);
 }
 
-__device__ __forceinline__ void glds16(const void *src, void *lds_dst) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *) src,
-                                     (__attribute__((address_space(3))) void *) lds_dst, 16, 0, 0);
+// 16 B per lane global -> LDS through a buffer descriptor on a wave-uniform base: the per-lane part is
+// voff, a wave-uniform offset goes in soff (SGPR), so no VALU address math is needed per load
+__device__ __forceinline__ void glds16_buf(const void *base, void *lds_dst, uint32_t voff, uint32_t soff) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *) base, (short) 0, 0x7FFFFFFF, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *) lds_dst, 16, voff, soff, 0, 0);
 }
+
 
 // occupancy: 3 workgroups per CU (<= 49 KB LDS, <= 168 VGPRs) hide the chunk barriers / DMA waits
 // best; the fp64 RBF variant spills a few epilogue values at that budget (outside the K loop), and
@@ -170,7 +174,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int w = tid >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably (scalar LDS bases)
     const int wr = w >> 1, wc = w & 1;
 
     // p and norms of the tile's rows/cols -> LDS (issued first: their wait must not drain the DMA)
@@ -185,23 +189,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
         acc0[nt] = FAST_EXP ? T(-0.5) * norms[J0 + wc * 64 + nt * 16 + (lane & 15)] : T(0);
 
     // per-lane byte offsets of this wave's DMA pieces inside a chunk (32-bit, reused for every chunk
-    // and both panels: the chunk / panel bases are wave-uniform, so the loads use saddr + voffset)
+    // and both panels: the chunk base and the panel offset are wave-uniform, see glds16_buf)
     uint32_t doff[PIECES];
 #pragma unroll
     for (int j = 0; j < PIECES; ++j) {
         const int elem = (w * PIECES + j) * EPP + lane * VEC;
         doff[j] = (uint32_t) (((int64_t) (elem / KP_TILE) * n_pad + elem % KP_TILE) * (int64_t) sizeof(T));
     }
+    // LDS-DMA through a buffer descriptor: the chunk base is a scalar pointer (SALU), the per-lane part
+    // is the constant doff and the panel offset goes in soffset — no VALU address math per chunk
+    const uint32_t offI = __builtin_amdgcn_readfirstlane((uint32_t) (I0 * (int64_t) sizeof(T)));
+    const uint32_t offJ = __builtin_amdgcn_readfirstlane((uint32_t) (J0 * (int64_t) sizeof(T)));
     auto issue = [&](int64_t kc, int buf) {
-        const char *ba = reinterpret_cast<const char *>(XT + kc * BK * n_pad + I0);
-        const char *bb = reinterpret_cast<const char *>(XT + kc * BK * n_pad + J0);
+        const T *cb = XT + kc * BK * n_pad;
         T *pa = smem + OFF_PAN + (2 * buf) * PANEL;
         T *pb = pa + PANEL;
 #pragma unroll
         for (int j = 0; j < PIECES; ++j) {
             const int u = w * PIECES + j;
-            glds16(ba + doff[j], pa + u * EPP);
-            glds16(bb + doff[j], pb + u * EPP);
+            glds16_buf(cb, pa + u * EPP, doff[j], offI);
+            glds16_buf(cb, pb + u * EPP, doff[j], offJ);
         }
     };
 
