@@ -328,12 +328,22 @@ __global__ __launch_bounds__(256) void kp_reduce_kernel(const T *__restrict__ pa
             for (int u = 0; u < 8; ++u) s += v[u];
         }
         for (; c < nb; ++c) s += partial[c * n_pad + i];
-    } else {
+    } else {  // one rank's share: only the slab rows of its super-blocks (same c order as above)
         const int64_t RS = (i / KP_TILE) / KP_SUPER;
-        for (int64_t c = 0; c < nb; ++c) {
-            const int64_t CS = c / KP_SUPER;
+        const int64_t ns = (nb + KP_SUPER - 1) / KP_SUPER;
+        for (int64_t CS = 0; CS < ns; ++CS) {
             const int64_t sb = (RS >= CS) ? tri_index(RS, CS) : tri_index(CS, RS);
-            if (sb >= s0 && sb < s1) s += partial[c * n_pad + i];
+            if (sb < s0 || sb >= s1) continue;
+            const int64_t c0 = CS * KP_SUPER, c1 = min(nb, c0 + KP_SUPER);
+            if (c1 - c0 == KP_SUPER) {
+                T v[KP_SUPER];
+#pragma unroll
+                for (int u = 0; u < KP_SUPER; ++u) v[u] = partial[(c0 + u) * n_pad + i];
+#pragma unroll
+                for (int u = 0; u < KP_SUPER; ++u) s += v[u];
+            } else {
+                for (int64_t c = c0; c < c1; ++c) s += partial[c * n_pad + i];
+            }
         }
     }
     raw[i] = s;
