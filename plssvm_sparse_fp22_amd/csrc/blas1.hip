@@ -13,6 +13,10 @@ namespace plssvm_mi {
 
 namespace {
 
+// fused CG kernels: RED_BLOCKS blocks of CG_NT threads (16 waves per block: memory parallelism for
+// the vector streams; one partial per block as for dot2_kernel)
+constexpr int CG_NT = 1024;
+
 template <typename T>
 __device__ __forceinline__ T block_sum(T v, T *red) {
 #pragma unroll
@@ -179,13 +183,13 @@ __device__ __forceinline__ void store_partials(T v1, T v2, T *red, T *__restrict
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void cg_fin_dad_kernel(const T *__restrict__ raw, const T *__restrict__ q,
+__global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__ raw, const T *__restrict__ q,
                                                          const T *__restrict__ d, const T *__restrict__ psum,
                                                          T QA_cost, T cost_inv, int raw_only, int64_t m,
                                                          T *__restrict__ Ad, T *__restrict__ pdad,
                                                          cg_scalars<T> *sc) {
     if (sc->converged) return;
-    __shared__ T red[8], bc[1];
+    __shared__ T red[CG_NT / 64], bc[1];
     T sp, sqp;
     partials_total(psum, red, bc, sp, sqp);
     if (blockIdx.x == 0 && threadIdx.x == 0) sc->sp = sp, sc->sqp = sqp;
@@ -204,12 +208,12 @@ __global__ __launch_bounds__(256) void cg_fin_dad_kernel(const T *__restrict__ r
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void cg_upd_rr_kernel(T *__restrict__ x, T *__restrict__ r, const T *__restrict__ d,
+__global__ __launch_bounds__(CG_NT) void cg_upd_rr_kernel(T *__restrict__ x, T *__restrict__ r, const T *__restrict__ d,
                                                         const T *__restrict__ Ad, const T *__restrict__ b, int reset,
                                                         const T *__restrict__ pdad, int64_t m, T *__restrict__ prr,
                                                         cg_scalars<T> *sc) {
     if (sc->converged) return;
-    __shared__ T red[8], bc[1];
+    __shared__ T red[CG_NT / 64], bc[1];
     T dAd, unused;
     partials_total(pdad, red, bc, dAd, unused);
     const T delta = sc->delta;
@@ -232,12 +236,12 @@ __global__ __launch_bounds__(256) void cg_upd_rr_kernel(T *__restrict__ x, T *__
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void cg_dir_sums_kernel(T *__restrict__ d, const T *__restrict__ r,
+__global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, const T *__restrict__ r,
                                                           const T *__restrict__ q, const T *__restrict__ prr, int init,
                                                           int64_t run, double *trace, int64_t trace_cap, int64_t m,
                                                           T *__restrict__ psum, cg_scalars<T> *sc) {
     if (sc->converged) return;
-    __shared__ T red[8], bc[1];
+    __shared__ T red[CG_NT / 64], bc[1];
     T beta = 0;
     if (!init) {
         T rr, unused;
@@ -274,7 +278,7 @@ __global__ __launch_bounds__(256) void cg_dir_sums_kernel(T *__restrict__ d, con
 template <typename T>
 void launch_cg_fin_dad(const T *raw, const T *q, const T *d, const T *psum, T QA_cost, T cost_inv, int raw_only,
                        int64_t m, T *Ad, T *pdad, cg_scalars<T> *sc, hipStream_t s) {
-    hipLaunchKernelGGL(cg_fin_dad_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, s, raw, q, d, psum, QA_cost, cost_inv,
+    hipLaunchKernelGGL(cg_fin_dad_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, raw, q, d, psum, QA_cost, cost_inv,
                        raw_only, m, Ad, pdad, sc);
     MI_LAUNCH_CHECK();
 }
@@ -282,14 +286,14 @@ void launch_cg_fin_dad(const T *raw, const T *q, const T *d, const T *psum, T QA
 template <typename T>
 void launch_cg_upd_rr(T *x, T *r, const T *d, const T *Ad, const T *b, int reset, const T *pdad, int64_t m, T *prr,
                       cg_scalars<T> *sc, hipStream_t s) {
-    hipLaunchKernelGGL(cg_upd_rr_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, s, x, r, d, Ad, b, reset, pdad, m, prr, sc);
+    hipLaunchKernelGGL(cg_upd_rr_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, x, r, d, Ad, b, reset, pdad, m, prr, sc);
     MI_LAUNCH_CHECK();
 }
 
 template <typename T>
 void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int init, int64_t run, double *trace,
                         int64_t trace_cap, int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s) {
-    hipLaunchKernelGGL(cg_dir_sums_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, s, d, r, q, prr, init, run, trace,
+    hipLaunchKernelGGL(cg_dir_sums_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, d, r, q, prr, init, run, trace,
                        trace_cap, m, psum, sc);
     MI_LAUNCH_CHECK();
 }
