@@ -166,25 +166,39 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
     }
 }
 
-// out[s] = sum_q partial[q][s] in panel order (8 panel loads in flight per step; the CSC pass has few
-// segments and many panels, so per-thread memory parallelism, not thread count, sets its speed)
+// out[s] = sum_q partial[q][s]. Many panels (split): a block of 256 threads takes 64 segments and its
+// 4 waves each sum one quarter of the panels (coalesced 64-segment rows, 8 loads in flight); the
+// quarters are added in order through LDS — a fixed order, so deterministic. The CSC pass has few
+// segments and many panels: splitting its panel loop gives it 4x the memory parallelism of one
+// thread per segment. Few panels: one thread per segment (256 segments per block).
 template <typename T>
 __global__ __launch_bounds__(256) void panel_reduce_kernel(const T *__restrict__ partial, int64_t P, int64_t nseg,
-                                                           T *__restrict__ out, const cg_scalars<T> *__restrict__ status) {
+                                                           int split, T *__restrict__ out,
+                                                           const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
-    const int64_t s = (int64_t) blockIdx.x * 256 + threadIdx.x;
-    if (s >= nseg) return;
+    __shared__ T part[3][64];
+    const int lane = split ? (threadIdx.x & 63) : threadIdx.x, quarter = split ? (threadIdx.x >> 6) : 0;
+    const int64_t s = (int64_t) blockIdx.x * (split ? 64 : 256) + lane;
+    const int64_t per = split ? (P + 3) / 4 : P, q0 = quarter * per, q1 = min(P, q0 + per);
     T a = 0;
-    int64_t q = 0;
-    for (; q + 8 <= P; q += 8) {
-        T v[8];
+    if (s < nseg) {
+        int64_t q = q0;
+        for (; q + 8 <= q1; q += 8) {
+            T v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = partial[(q + u) * nseg + s];
+            for (int u = 0; u < 8; ++u) v[u] = partial[(q + u) * nseg + s];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) a += v[u];
+            for (int u = 0; u < 8; ++u) a += v[u];
+        }
+        for (; q < q1; ++q) a += partial[q * nseg + s];
     }
-    for (; q < P; ++q) a += partial[q * nseg + s];
-    out[s] = a;
+    if (!split) {
+        if (s < nseg) out[s] = a;
+        return;
+    }
+    if (quarter > 0) part[quarter - 1][lane] = a;
+    __syncthreads();
+    if (quarter == 0 && s < nseg) out[s] = ((a + part[0][lane]) + part[1][lane]) + part[2][lane];
 }
 
 // out[0..nseg) = the pass result (partial slabs + reduction when P > 1)
@@ -206,8 +220,9 @@ inline void launch_panel_spmv(const spmv_plan<T> &pl, const T *x, int64_t xn, T 
     }
     MI_LAUNCH_CHECK();
     if (pl.P > 1) {
-        hipLaunchKernelGGL(panel_reduce_kernel<T>, dim3((unsigned) ceil_div(pl.nseg, 256)), dim3(256), 0, stream,
-                           pl.partial.get(), pl.P, pl.nseg, out, status);
+        const int split = pl.P >= 16 ? 1 : 0;
+        hipLaunchKernelGGL(panel_reduce_kernel<T>, dim3((unsigned) ceil_div(pl.nseg, split ? 64 : 256)), dim3(256), 0,
+                           stream, pl.partial.get(), pl.P, pl.nseg, split, out, status);
         MI_LAUNCH_CHECK();
     }
 }
