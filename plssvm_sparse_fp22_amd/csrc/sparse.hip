@@ -112,13 +112,29 @@ __global__ __launch_bounds__(256) void gram_gen_kernel(const int64_t *__restrict
     }
 }
 
+// pairs per group g = (window, row): the unique keys are sorted by group, so each group is one run;
+// its first key writes gstart[g], its last writes rowcnt[g] = end (exclusive), no atomics (a hot
+// counter per row serialised the former atomicAdd version: 3.3 ms per row block)
+__device__ __forceinline__ int64_t gram_group(uint64_t k) {
+    return (int64_t) (k >> 32) * GRAM_RB + (int64_t) ((k >> 16) & 0xFFFF);
+}
+
 __global__ __launch_bounds__(256) void gram_rowcount_kernel(const uint64_t *__restrict__ ukeys,
                                                             const int64_t *__restrict__ nruns,
-                                                            int32_t *__restrict__ rowcnt) {
+                                                            int32_t *__restrict__ rowcnt, int32_t *__restrict__ gstart) {
     const int64_t u = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= *nruns) return;
-    const uint64_t k = ukeys[u];
-    atomicAdd(&rowcnt[(k >> 32) * GRAM_RB + ((k >> 16) & 0xFFFF)], 1);
+    const int64_t nu = *nruns;
+    if (u >= nu) return;
+    const int64_t g = gram_group(ukeys[u]);
+    if (u == 0 || gram_group(ukeys[u - 1]) != g) gstart[g] = (int32_t) u;
+    if (u == nu - 1 || gram_group(ukeys[u + 1]) != g) rowcnt[g] = (int32_t) (u + 1);
+}
+
+// rowcnt[g] = end - start for the groups written above, 0 elsewhere
+__global__ __launch_bounds__(256) void gram_runlen_kernel(int32_t *__restrict__ rowcnt,
+                                                          const int32_t *__restrict__ gstart, int64_t n) {
+    const int64_t g = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < n && rowcnt[g] > 0) rowcnt[g] -= gstart[g];
 }
 
 // rows are padded to a multiple of 8 pairs per cell (pads: j = 0, s = 0), so an 8-pair chunk never
@@ -138,7 +154,7 @@ __global__ __launch_bounds__(256) void gram_store_kernel(const uint64_t *__restr
     const int64_t u = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= *nruns) return;
     const uint64_t k = ukeys[u];
-    const int64_t g = (int64_t) (k >> 32) * GRAM_RB + (int64_t) ((k >> 16) & 0xFFFF);
+    const int64_t g = gram_group(k);
     const int64_t dst = (int64_t) padded[g] + (u - (int64_t) uoff[g]);
     pj[dst] = (uint16_t) (k & 0xFFFF);
     ps[dst] = usum[u];
@@ -739,8 +755,13 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
                                                            stream));
             MI_HIP_CHECK(hipMemcpyAsync(&nu, nruns.get(), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
             MI_HIP_CHECK(hipStreamSynchronize(stream));
+            // cnt8 holds the group starts here (gram_pad_kernel rewrites it below)
             hipLaunchKernelGGL(gram_rowcount_kernel, dim3((unsigned) ceil_div(nu, 256)), dim3(256), 0, stream,
-                               keys.get(), nruns.get(), rowcnt.get());
+                               keys.get(), nruns.get(), rowcnt.get(), cnt8.get());
+            MI_LAUNCH_CHECK();
+            const int64_t ngr = nw * GRAM_RB;
+            hipLaunchKernelGGL(gram_runlen_kernel, dim3((unsigned) ceil_div(ngr, 256)), dim3(256), 0, stream,
+                               rowcnt.get(), cnt8.get(), ngr);
             MI_LAUNCH_CHECK();
         }
         const int ng = (int) (nw * GRAM_RB + 1);
