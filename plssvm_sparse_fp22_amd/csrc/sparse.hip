@@ -210,7 +210,7 @@ __device__ __forceinline__ unsigned long long fx_round(double x) {
     return (unsigned long long) (__double_as_longlong(x + 6755399441055744.0) - 0x4338000000000000LL);
 }
 
-template <typename T, int KERNEL>
+template <typename T, int KERNEL, int ABL>
 __global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__restrict__ cells,
                                                        const int64_t *__restrict__ rb_base,
                                                        const int32_t *__restrict__ rowoff,
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__res
                                                        const T *__restrict__ norms, const T *__restrict__ ev,
                                                        const T *__restrict__ p, T *__restrict__ slab_row,
                                                        T *__restrict__ slab_col, int64_t m, int64_t m_pad, kfun<T> kf,
-                                                       T kappa, const cg_scalars<T> *__restrict__ status, int ablate) {
+                                                       T kappa, const cg_scalars<T> *__restrict__ status) {
     constexpr int CW = GRAM_CW, NWAVE = GRAM_WG / 64;
     constexpr bool NEED_N = KERNEL == 2, NEED_E = KERNEL == 2;
     using acc_t = unsigned long long;
@@ -285,11 +285,15 @@ __global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__res
     const int64_t wbeg = c0 + wave * per_wave;
     const int64_t wend = min<int64_t>(c1, wbeg + per_wave);
 
-    // lane state: current row, its end (absolute pair index), its p (e p) / norm / e
-    int r = 0;
-    int64_t rend = base + ro[0];
-    T pi = 0, ni = 0, ei = 0;
-    auto seek = [&](int64_t e) {  // move r forward to the row containing pair e (rend <= e)
+    // Software pipeline, one step deep: while step k is evaluated, step k+1's pair stream (j, s) AND
+    // its lanes' row factors are already in flight. The row seek for step k+1 (LDS only) runs before
+    // step k's pairs, and every load is issued unconditionally (indices clamped), so the only vmcnt
+    // wait per step is at its end, covering loads that had the whole step to land. (Loading the row
+    // factors after the seek of the *same* step forced a vmcnt(0) before every step: the stream
+    // prefetch was waited for with them and never overlapped anything.)
+    int r = 0;                      // row of the lane's chunk in the step being prefetched
+    int64_t rend = base + ro[0];    // end (absolute pair index) of row r
+    auto seek = [&](int64_t e) {    // move r forward to the row containing pair e (rend <= e)
         const int32_t rel = (int32_t) (e - base);
         int steps = 0;
         while (steps < 8 && ro[r + 1] <= rel) ++r, ++steps;
@@ -303,50 +307,75 @@ __global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__res
             r = lo;
         }
         rend = base + ro[r + 1];
+    };
+    // row factors of row r: p (e p for the factored rbf), norm, e — plain loads, consumed one step later
+    T pa_n = 0, pb_n = 0, ni_n = 0, ei_n = 0;
+    auto load_row = [&]() {
+        const int64_t g = I0 + min(r, rows - 1);
         if (KERNEL == 3) {
-            pi = ev[I0 + r] * p[I0 + r];
+            pa_n = ev[g], pb_n = p[g];
         } else {
-            pi = p[I0 + r];
-            if (NEED_N) ni = norms[I0 + r];
-            if (NEED_E) ei = ev[I0 + r];
+            pa_n = p[g];
+            if (NEED_N) ni_n = norms[g];
+            if (NEED_E) ei_n = ev[g];
         }
     };
     // exp(-g dist) = exp2(-g log2(e) dist); exp(2 g s) = exp2(2 g log2(e) s)
     const T lg = gamma * T(1.4426950408889634);
+    const int64_t clast = wend - 1;  // clamp target for the loads of idle lanes (wend > wbeg when used)
 
     uint4 jv_n = make_uint4(0, 0, 0, 0);
     T s_n[8];
-    if (wbeg + lane < wend) {
-        jv_n = *reinterpret_cast<const uint4 *>(pj + ((wbeg + lane) << 3));
-        load8<T>(ps, (wbeg + lane) << 3, s_n);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s_n[k] = T(0);
+    int r_n = 0;
+    if (wbeg < wend) {
+        const int64_t cf = min<int64_t>(wbeg + lane, clast);
+        jv_n = *reinterpret_cast<const uint4 *>(pj + (cf << 3));
+        load8<T>(ps, cf << 3, s_n);
+        if ((cf << 3) >= rend) seek(cf << 3);
+        r_n = r;
+        load_row();
     }
     for (int64_t cb = wbeg; cb < wend; cb += 64) {  // wave-uniform trip count
-        const int64_t c = cb + lane;
-        const bool have = c < wend;
+        const bool have = cb + lane < wend;
+        // this step's operands (loaded during the previous step)
         const uint4 jv = jv_n;
         T s[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) s[k] = s_n[k];
-        if (cb + 64 + lane < wend) {  // prefetch the next step
-            jv_n = *reinterpret_cast<const uint4 *>(pj + ((cb + 64 + lane) << 3));
-            load8<T>(ps, (cb + 64 + lane) << 3, s_n);
+        const int rc = r_n;
+        const T pi = KERNEL == 3 ? pa_n * pb_n : pa_n, ni = ni_n, ei = ei_n;
+        // issue the next step: stream, seek, row factors
+        if (cb + 64 < wend) {  // wave-uniform
+            const int64_t cn = cb + 64 + lane;
+            const int64_t cl = min<int64_t>(cn, clast);
+            jv_n = *reinterpret_cast<const uint4 *>(pj + (cl << 3));
+            load8<T>(ps, cl << 3, s_n);
+            if (cn < wend && (cn << 3) >= rend) seek(cn << 3);
+            r_n = r;
+            load_row();
         }
         int rl = -1;  // row of this lane's chunk (for the cross-lane reduction)
         T acc = 0;
         if (have) {
-            const int64_t e0 = c << 3;
-            if (e0 >= rend) seek(e0);
             const uint32_t jw[4] = { jv.x, jv.y, jv.z, jv.w };
+            int jl[8];
+            T wpj[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const int jl = (int) ((jw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+                jl[k] = (int) ((jw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
+                wpj[k] = wp[jl[k]];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
                 T cv;
                 if (KERNEL == 3) {
-                    cv = (ablate & 2) ? lg * s[k] : fast_exp2(T(2) * lg * s[k]) - T(1);  // pads: s = 0 -> 0
+                    cv = (ABL & 2) ? lg * s[k] : fast_exp2(T(2) * lg * s[k]) - T(1);  // pads: s = 0 -> 0
                 } else if (KERNEL == 2) {
-                    T dist = ni + wn[jl] - T(2) * s[k];
+                    T dist = ni + wn[jl[k]] - T(2) * s[k];
                     dist = dist > T(0) ? dist : T(0);
-                    cv = (ablate & 2) ? dist - ei * we[jl] : fast_exp2(-lg * dist) - ei * we[jl];
+                    cv = (ABL & 2) ? dist - ei * we[jl[k]] : fast_exp2(-lg * dist) - ei * we[jl[k]];
                     cv = s[k] == T(0) ? T(0) : cv;  // pads (and exact-zero pairs, whose c is 0)
                 } else if (KERNEL == 1) {
                     const T bse = fma(gamma, s[k], kf.coef0);
@@ -356,11 +385,11 @@ __global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__res
                 } else {
                     cv = s[k];
                 }
-                acc = fma(cv, wp[jl], acc);
-                if (ablate & 1) acc += cv * pi;  // timing-only ablation: no LDS column accumulation
-                else atomicAdd(&colacc[jl], quant(cv * pi));
+                acc = fma(cv, wpj[k], acc);
+                if (ABL & 1) acc += cv * pi;  // timing-only ablation: no LDS column accumulation
+                else atomicAdd(&colacc[jl[k]], quant(cv * pi));
             }
-            rl = r;
+            rl = rc;
         }
         // segmented reduction of (row, partial) across the wave: rows are non-decreasing in lane order
         T sacc = acc;
@@ -871,12 +900,21 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(), csr.rowoff.get(),
                            csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p, csr.slab_row.get(),
-                           csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status, gram_ablate());
+                           csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status);
     };
-    if (kernel == 0) launch(gram_kp_kernel<T, 0>);
-    else if (kernel == 1) launch(gram_kp_kernel<T, 1>);
-    else if (csr.rbf_factored) launch(gram_kp_kernel<T, 3>);
-    else launch(gram_kp_kernel<T, 2>);
+    auto pick = [&](auto abl) {
+        constexpr int A = decltype(abl)::value;
+        if (kernel == 0) launch(gram_kp_kernel<T, 0, A>);
+        else if (kernel == 1) launch(gram_kp_kernel<T, 1, A>);
+        else if (csr.rbf_factored) launch(gram_kp_kernel<T, 3, A>);
+        else launch(gram_kp_kernel<T, 2, A>);
+    };
+    switch (gram_ablate() & 3) {  // ablations are timing-only variants (wrong results)
+    case 1: pick(std::integral_constant<int, 1>{}); break;
+    case 2: pick(std::integral_constant<int, 2>{}); break;
+    case 3: pick(std::integral_constant<int, 3>{}); break;
+    default: pick(std::integral_constant<int, 0>{});
+    }
     MI_LAUNCH_CHECK();
 }
 
