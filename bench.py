@@ -91,6 +91,8 @@ def main():
     ap.add_argument("--features", type=int, default=0, help="override number of features (d)")
     ap.add_argument("--kernel", choices=["linear", "polynomial", "rbf"], default=None,
                     help="override the configuration's kernel function (ablations)")
+    ap.add_argument("--dtype", choices=["f32", "f64"], default=None,
+                    help="override the configuration's real type (parity/throughput studies, not the headline line)")
     ap.add_argument("--kp-reps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--sim-rank", default=None, metavar="R/W",
@@ -115,6 +117,8 @@ def main():
     cfg = CONFIGS[args.config]
     if args.kernel:
         cfg = (args.kernel,) + tuple(cfg[1:])
+    if args.dtype:
+        cfg = cfg[:3] + ({"f32": np.float32, "f64": np.float64}[args.dtype],) + tuple(cfg[4:])
     kernel, _, _, dtype, layout, _, desc = cfg
     p, n, d, y, extra = make_problem(cfg, args.points, args.features, rank)
     sim = None

@@ -210,8 +210,14 @@ __device__ __forceinline__ unsigned long long fx_round(double x) {
     return (unsigned long long) (__double_as_longlong(x + 6755399441055744.0) - 0x4338000000000000LL);
 }
 
+// Workgroup size: 512 threads (two workgroups per CU) when the cell's LDS fits twice in a CU
+// (fp32 linear / poly / factored rbf: 72 KB); otherwise one workgroup per CU of 1024 threads, so a CU
+// still streams with 16 waves (fp64: window factors 32 KB; direct rbf: norms and e of the window too).
+template <typename T, int KERNEL>
+constexpr int gram_wg() { return sizeof(T) == 8 || KERNEL == 2 ? 1024 : GRAM_WG; }
+
 template <typename T, int KERNEL, int ABL>
-__global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__restrict__ cells,
+__global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const gram_cell *__restrict__ cells,
                                                        const int64_t *__restrict__ rb_base,
                                                        const int32_t *__restrict__ rowoff,
                                                        const uint16_t *__restrict__ pj, const T *__restrict__ ps,
@@ -219,7 +225,8 @@ __global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__res
                                                        const T *__restrict__ p, T *__restrict__ slab_row,
                                                        T *__restrict__ slab_col, int64_t m, int64_t m_pad, kfun<T> kf,
                                                        T kappa, const cg_scalars<T> *__restrict__ status) {
-    constexpr int CW = GRAM_CW, NWAVE = GRAM_WG / 64;
+    constexpr int NT = gram_wg<T, KERNEL>();
+    constexpr int CW = GRAM_CW, NWAVE = NT / 64;
     constexpr bool NEED_N = KERNEL == 2, NEED_E = KERNEL == 2;
     using acc_t = unsigned long long;
     __shared__ T wn[NEED_N ? CW : 1], we[NEED_E ? CW : 1], wp[CW];
@@ -235,7 +242,7 @@ __global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__res
     const int wlen = (int) min<int64_t>(CW, m - W0);
     const T gamma = kf.gamma;
     T pmax = 0;
-    for (int t = tid; t < CW; t += GRAM_WG) {
+    for (int t = tid; t < CW; t += NT) {
         const bool ok = t < wlen;
         if (NEED_N) wn[t] = ok ? norms[W0 + t] : T(0);
         if (NEED_E) we[t] = ok ? ev[W0 + t] : T(0);
@@ -244,11 +251,11 @@ __global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__res
         pmax = max(pmax, fabs(pv));
         colacc[t] = 0;
     }
-    for (int t = tid; t < GRAM_RB; t += GRAM_WG) {
+    for (int t = tid; t < GRAM_RB; t += NT) {
         rowacc[t] = 0;
         if (t < rows) pmax = max(pmax, fabs(KERNEL == 3 ? ev[I0 + t] * p[I0 + t] : p[I0 + t]));
     }
-    for (int t = tid; t <= rows; t += GRAM_WG) ro[t] = rowoff[cell.rowoff + t];
+    for (int t = tid; t <= rows; t += NT) ro[t] = rowoff[cell.rowoff + t];
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) pmax = max(pmax, __shfl_xor(pmax, o));
     if (lane == 0) wmax[wave] = pmax;
@@ -403,12 +410,12 @@ __global__ __launch_bounds__(GRAM_WG) void gram_kp_kernel(const gram_cell *__res
         if (rl >= 0 && (lane == 0 || rprev != rl)) atomicAdd(&rowacc[rl], quant_sum(sacc));
     }
     __syncthreads();
-    for (int t = tid; t < rows; t += GRAM_WG) {
+    for (int t = tid; t < rows; t += NT) {
         T v = (T) ldexp((double) (long long) rowacc[t], qe);
         if (KERNEL == 3) v *= ev[I0 + t];
         slab_row[(int64_t) cell.W * m_pad + I0 + t] = v;
     }
-    for (int t = tid; t < wlen; t += GRAM_WG) {
+    for (int t = tid; t < wlen; t += NT) {
         T v = (T) ldexp((double) (long long) colacc[t], qe);
         if (KERNEL == 3) v *= ev[W0 + t];
         slab_col[(int64_t) cell.I * m_pad + W0 + t] = v;
@@ -896,18 +903,18 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
         kappa = 1;
         for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
     }
-    const dim3 grid((unsigned) csr.ncells), block(GRAM_WG);
-    auto launch = [&](auto kern) {
-        hipLaunchKernelGGL(kern, grid, block, 0, stream, csr.cells.get(), csr.rb_base.get(), csr.rowoff.get(),
+    const dim3 grid((unsigned) csr.ncells);
+    auto launch = [&](auto kern, int nt) {
+        hipLaunchKernelGGL(kern, grid, dim3(nt), 0, stream, csr.cells.get(), csr.rb_base.get(), csr.rowoff.get(),
                            csr.pj.get(), csr.ps.get(), norms.get(), csr.e.get(), p, csr.slab_row.get(),
                            csr.slab_col.get(), m, csr.m_pad, kf(), kappa, status);
     };
     auto pick = [&](auto abl) {
         constexpr int A = decltype(abl)::value;
-        if (kernel == 0) launch(gram_kp_kernel<T, 0, A>);
-        else if (kernel == 1) launch(gram_kp_kernel<T, 1, A>);
-        else if (csr.rbf_factored) launch(gram_kp_kernel<T, 3, A>);
-        else launch(gram_kp_kernel<T, 2, A>);
+        if (kernel == 0) launch(gram_kp_kernel<T, 0, A>, gram_wg<T, 0>());
+        else if (kernel == 1) launch(gram_kp_kernel<T, 1, A>, gram_wg<T, 1>());
+        else if (csr.rbf_factored) launch(gram_kp_kernel<T, 3, A>, gram_wg<T, 3>());
+        else launch(gram_kp_kernel<T, 2, A>, gram_wg<T, 2>());
     };
     switch (gram_ablate() & 3) {  // ablations are timing-only variants (wrong results)
     case 1: pick(std::integral_constant<int, 1>{}); break;

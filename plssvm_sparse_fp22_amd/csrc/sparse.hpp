@@ -19,7 +19,7 @@ constexpr int GRAM_RB = 2048;
 // window edge: the K·p kernel stages n_j, e_j, p_j of the window plus int64 column and row
 // accumulators in LDS (fp64: 3 x 32 + 32 + 16 KiB + row offsets = 152 KiB; fp32: 96 KiB)
 constexpr int GRAM_CW = 4096;
-constexpr int GRAM_WG = 512;  // K·p workgroup size
+constexpr int GRAM_WG = 512;  // K·p workgroup size when two fit a CU (else 1024: gram_wg in sparse.hip)
 
 struct gram_cell {
     int32_t I, W;
