@@ -137,7 +137,15 @@ __global__ __launch_bounds__(256) void gram_runlen_kernel(int32_t *__restrict__ 
     if (g < n && rowcnt[g] > 0) rowcnt[g] -= gstart[g];
 }
 
-// rows are padded to a multiple of 8 pairs per cell (pads: j = 0, s = 0), so an 8-pair chunk never
+// pads of the pattern: s = 0 (contributes exactly 0) and j = (chunk index mod 64), so the pads that the
+// lanes of one wave-instruction meet hit 64 distinct LDS column accumulators (with j = 0 for every pad
+// their zero-valued ds_add_u64 all went to one address and serialised)
+__global__ __launch_bounds__(256) void gram_pad_index_kernel(uint16_t *__restrict__ pj, int64_t n) {
+    const int64_t x = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < n) pj[x] = (uint16_t) ((x >> 3) & 63);
+}
+
+// rows are padded to a multiple of 8 pairs per cell (pads: s = 0, spread j), so an 8-pair chunk never
 // spans two rows; pair u of group g = (W, row) goes to padded[g] + (u - uoff[g])
 __global__ __launch_bounds__(256) void gram_pad_kernel(const int32_t *__restrict__ cnt, int64_t n,
                                                        int32_t *__restrict__ cnt8) {
@@ -721,7 +729,10 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     for (int64_t I = csr.rb0; I < csr.rb1; ++I)
         groups += (std::min<int64_t>(m, (I + 1) * GRAM_RB) - I * GRAM_RB) * gram_nw(I, m, CW);
     const int64_t pcap = csr.pair_bound + 7 * std::min(csr.pair_bound, groups) + 16;
-    csr.pj.alloc(pcap, stream);
+    csr.pj.alloc(pcap, stream, false);
+    hipLaunchKernelGGL(gram_pad_index_kernel, dim3((unsigned) ceil_div(pcap, 256)), dim3(256), 0, stream, csr.pj.get(),
+                       pcap);
+    MI_LAUNCH_CHECK();
     csr.ps.alloc(pcap, stream);
     csr.slab_row.alloc(std::max<int64_t>(csr.nW, 1) * csr.m_pad, stream);
     csr.slab_col.alloc(std::max<int64_t>(csr.nRB, 1) * csr.m_pad, stream);
