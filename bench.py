@@ -47,12 +47,14 @@ CONFIGS = {
                     "COO/CSR RBF with FP22-packed features, 2M x 100k @ 0.05% nnz (configs[4])"),
 }
 
+CONFIG_DTYPE = {k: ("f64" if v[3] == np.float64 else "f32") for k, v in CONFIGS.items()}
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_problem(cfg, n_override, d_override, rank):
+def make_problem(cfg, n_override, d_override, rank, cache=None):
     kernel, n, d, dtype, layout, k, desc = cfg
     if n_override:
         if layout != "dense" and not d_override:  # keep the column occupancy c_f = n k / d fixed
@@ -67,7 +69,14 @@ def make_problem(cfg, n_override, d_override, rank):
         p.data, p.labels = X, y
         extra = dict(X=X)
     else:
-        csr, y = datagen.sparse_csr(n, d, k, seed=3 if layout == "csr" else 5, dtype=dtype)
+        key = (n, d, k, layout, np.dtype(dtype).name)
+        if cache is not None and key in cache:
+            csr, y = cache[key]
+        else:
+            csr, y = datagen.sparse_csr(n, d, k, seed=3 if layout == "csr" else 5, dtype=dtype)
+            if cache is not None:
+                cache.clear()  # one sparse matrix at a time (config 5 is 1e8 entries)
+                cache[key] = (csr, y)
         if layout == "fp22":
             from plssvm_sparse_fp22_amd.fp22 import pack
 
@@ -81,11 +90,93 @@ def make_problem(cfg, n_override, d_override, rank):
     return p, n, d, y, extra
 
 
+def collective_desc(world, sim, exchange):
+    if sim:
+        return (f"one MI355X computing rank {sim[0]}'s share of a {sim[1]}-GPU job (no collective); "
+                "value = CG iterations/s of that share")
+    if world == 1:
+        return "single GPU, no collective"
+    via = "host-staged exchange over gloo" if exchange else "RCCL over xGMI"
+    return f"{world} GPUs, one process each: work split of the implicit matrix, one all-reduce of m per K·p ({via})"
+
+
+def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_seconds, kp_reps, sim=None,
+               kernel=None, dtype=None, points=0, features=0, data_cache=None):
+    """Measure one BASELINE configuration: setup, q, r0, `warmup` + `steps` CG iterations (timed with
+    a barrier and stream synchronisation on both sides, max over ranks), the dominant kernel's
+    average launch time (hipEvents on the engine stream), roofline, committed PMC traffic and the
+    oracle's CPU baseline. Returns the record (bench-line keys) without the metric header."""
+    cfg = CONFIGS[name]
+    if kernel:
+        cfg = (kernel,) + tuple(cfg[1:])
+    if dtype:
+        cfg = cfg[:3] + ({"f32": np.float32, "f64": np.float64}[dtype],) + tuple(cfg[4:])
+    kern, _, _, dt, layout, _, desc = cfg
+    p, n, d, y, extra = make_problem(cfg, points, features, rank, data_cache)
+    ndev = pm.device_count()
+    device = int(os.environ.get("LOCAL_RANK", str(rank))) % ndev if ndev > 0 else 0
+    svm = pm.CSVM(p, device=device, rank=rank, world_size=world, uid=uid, sim_rank=sim)
+    share = sim[1] if sim else world  # the work split divides the implicit matrix by this
+    t0 = time.time()
+    svm.setup_data_on_device()
+    t_setup = time.time() - t0
+    q = svm.generate_q()
+    b = (y[:-1] - y[-1]).astype(dt)
+    delta0 = svm.cg_begin(b, q, eps=1e-3)
+    log(f"[rank {rank}] {name}: setup {t_setup:.2f}s, q + r0 {time.time() - t0 - t_setup:.2f}s, delta0={delta0:.6e}")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    if warmup:
+        svm.cg_step(warmup, force=True)
+    barrier()
+    t_start = time.perf_counter()
+    svm.cg_step(steps, force=True)  # ends with hipStreamSynchronize on the engine stream
+    elapsed = time.perf_counter() - t_start
+    barrier()
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    info = svm.info()
+    ms_kp, ms_dom = svm.time_kp(kp_reps)
+    svm.close()
+    roof = roofline(cfg, info, n, d, share, ms_dom, extra)
+    dts = "f64" if dt == np.float64 else "f32"
+    tkey = name + (f"_sim{sim[0]}of{sim[1]}" if sim else "")
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(tkey, n, d, world, roof["kernel"], dts, kern, cfg is CONFIGS[name])
+    if roof["traffic"] and roof["bound"] == "hbm":
+        roof["traffic_GBps"] = roof["traffic"] / (ms_dom * 1e-3) / 1e9
+        roof["traffic_frac"] = roof["traffic_GBps"] * 1e9 / PEAKS["hbm"]
+    if roof["bound"] == "mfma":
+        roof["mfma_util"], roof["mfma_util_source"] = pmc_mfma(tkey, n, d, world, kern, dts)
+    cpu = None
+    if want_cpu and rank == 0 and world == 1 and not sim:
+        cpu = cpu_baseline(kern, dt, d, n - 1, cpu_seconds, extra)
+    rec = {
+        "value": steps / elapsed, "unit": "CG iterations/s", "ms_per_step": elapsed / steps * 1e3, "steps": steps,
+        "warmup": warmup, "dtype": dts,
+        "config": {"workload": desc, "N": n, "d": d, "kernel": kern, "layout": layout,
+                   "kp_mode": {1: "pairwise", 2: "factored"}[info["kp_mode"]],
+                   "parallelism": collective_desc(world, sim, args.host_exchange), "setup_s": round(t_setup, 3)},
+        "roofline": roof, "cpu_baseline": cpu, "kp_ms": ms_kp,
+    }
+    if info["is_sparse"]:
+        rec["config"]["nnz"] = info["nnz"]
+    if sim:
+        rec["config"]["simulated_rank"] = f"{sim[0]}/{sim[1]}"
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="dense_rbf_100k", choices=sorted(CONFIGS))
     ap.add_argument("--points", type=int, default=0, help="override number of points (N)")
     ap.add_argument("--features", type=int, default=0, help="override number of features (d)")
@@ -95,108 +186,78 @@ def main():
                     help="override the configuration's real type (parity/throughput studies, not the headline line)")
     ap.add_argument("--kp-reps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the sparse BASELINE rows measured beside the default headline (configs[2], 3-RBF)")
+    ap.add_argument("--host-exchange", action="store_true",
+                    help="N > 1: exchange through the host over gloo (plssvm_mi_comm_init_host) instead of RCCL")
     ap.add_argument("--sim-rank", default=None, metavar="R/W",
                     help="one GPU computes rank R's share of a W-GPU job (no collective): measures one rank of a "
                          "multi-GPU configuration that does not fit one GPU (e.g. configs[4])")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     dist = None
     uid = None
     if world > 1:
         import torch.distributed as dist
 
         dist.init_process_group("gloo")
-        box = [pm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        uid = box[0]
-
-    cfg = CONFIGS[args.config]
-    if args.kernel:
-        cfg = (args.kernel,) + tuple(cfg[1:])
-    if args.dtype:
-        cfg = cfg[:3] + ({"f32": np.float32, "f64": np.float64}[args.dtype],) + tuple(cfg[4:])
-    kernel, _, _, dtype, layout, _, desc = cfg
-    p, n, d, y, extra = make_problem(cfg, args.points, args.features, rank)
+        if not args.host_exchange:
+            box = [pm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            uid = box[0]
     sim = None
     if args.sim_rank:
         if world > 1:
             raise SystemExit("--sim-rank is a single-process option")
         sim = tuple(int(v) for v in args.sim_rank.split("/"))
-    ndev = pm.device_count()
-    device = local_rank % ndev if ndev > 0 else local_rank  # more ranks than GPUs: share (rehearsal only)
-    svm = pm.CSVM(p, device=device, rank=rank, world_size=world, uid=uid, sim_rank=sim)
-    share = sim[1] if sim else world  # the work split divides the implicit matrix by this
-    t0 = time.time()
-    svm.setup_data_on_device()
-    t_setup = time.time() - t0
-    q = svm.generate_q()
-    b = (y[:-1] - y[-1]).astype(dtype)
-    delta0 = svm.cg_begin(b, q, eps=1e-3)
-    log(f"[rank {rank}] setup {t_setup:.2f}s, q + r0 {time.time() - t0 - t_setup:.2f}s, delta0={delta0:.6e}")
+    if args.host_exchange and world > 1:
+        _orig = pm.CSVM
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
+        def _csvm(p, **kw):  # host-staged group (test transport / no-RCCL groups)
+            kw.pop("uid", None)
+            return _orig(p, exchange=pm.torch_exchange(dist), **kw)
 
-    if args.warmup:
-        svm.cg_step(args.warmup, force=True)
-    barrier()
-    t_start = time.perf_counter()
-    svm.cg_step(args.steps, force=True)  # ends with hipStreamSynchronize on the engine stream
-    elapsed = time.perf_counter() - t_start
-    barrier()
-    if dist is not None:
-        import torch
+        pm.CSVM = _csvm
 
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    iters_per_s = args.steps / elapsed
-
-    info = svm.info()
-    ms_kp, ms_dom = svm.time_kp(args.kp_reps)
-    roof = roofline(cfg, info, n, d, share, ms_dom, extra)
-    tkey = args.config + (f"_sim{sim[0]}of{sim[1]}" if sim else "")
-    roof["traffic"], roof["traffic_source"] = pmc_traffic(tkey, n, d, world, roof["kernel"])
-    if roof["bound"] == "mfma":
-        roof["mfma_util"], roof["mfma_util_source"] = pmc_mfma(tkey, n, d, world, kernel)
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(kernel, dtype, d, n - 1, args.cpu_seconds, extra)
-
+    cache = {}
+    rec = run_config(args.config, args, rank, world, dist, uid, args.steps, args.warmup, not args.no_cpu,
+                     args.cpu_seconds, args.kp_reps, sim=sim, kernel=args.kernel, dtype=args.dtype,
+                     points=args.points, features=args.features, data_cache=cache)
+    extra = None
+    default_run = (args.config == "dense_rbf_100k" and not (args.kernel or args.dtype or args.points or
+                                                            args.features or sim) and world == 1)
+    if default_run and not args.no_extra:
+        # north_star's sparse target measured under the same clock: configs[2] with RBF (the >= 70 % HBM
+        # row) and configs[2] itself (sparse linear), same seeded matrix
+        extra = {}
+        for name, steps in (("csr_rbf_1m", 10), ("csr_linear_1m", 200)):
+            extra[name] = run_config(name, args, rank, world, dist, uid, steps, 2, not args.no_cpu,
+                                     args.cpu_seconds * 0.6, args.kp_reps, data_cache=cache)
     if rank == 0:
         out = {
             "metric": METRIC,
-            "value": iters_per_s,
-            "unit": "CG iterations/s",
+            "value": rec["value"],
+            "unit": rec["unit"],
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": rec["ms_per_step"],
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64" if dtype == np.float64 else "f32",
+            "dtype": rec["dtype"],
             "data": "synthetic (seeded generate_data.py-style blobs / sparse CSR)",
-            "config": {"workload": desc, "N": n, "d": d, "kernel": kernel, "layout": layout,
-                       "kp_mode": {1: "pairwise", 2: "factored"}[info["kp_mode"]],
-                       "parallelism": f"x{world} GPUs: work split of the implicit matrix, RCCL all-reduce per K·p",
-                       "setup_s": round(t_setup, 3)},
-            "roofline": roof,
-            "cpu_baseline": cpu,
-            "kp_ms": ms_kp,
+            "config": rec["config"],
+            "roofline": rec["roofline"],
+            "cpu_baseline": rec["cpu_baseline"],
+            "kp_ms": rec["kp_ms"],
         }
-        if sim:
-            out["config"]["simulated_rank"] = f"{sim[0]}/{sim[1]}"
-            out["config"]["parallelism"] = (f"one MI355X computing rank {sim[0]}'s share of a {sim[1]}-GPU job "
-                                            "(no collective); value = CG iterations/s of that share")
+        if extra:
+            out["extra"] = extra
         print(json.dumps(out), flush=True)
-    svm.close()
     if dist is not None:
         dist.destroy_process_group()
 
@@ -232,34 +293,49 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
     c = np.bincount(col, minlength=d).astype(np.float64)
     vb = 2.75 if layout == "fp22" else es
     co = float((c * (c + 1) / 2).sum())
-    alg = (co * (4 + vb) + col.size * (4 + vb) + 3 * m * es) / world
-    stream = info["pair_slots"] * (2 + es)  # stored slots (rows padded to 8 per cell)
-    return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s", frac=alg / s / PEAKS["hbm"],
-                traffic=None, kernel="gram_kp_kernel", launch_ms=ms_dom, alg_bytes=alg,
-                stream_bytes_per_launch=stream, stream_GBps=stream / s / 1e9, pairs=info["pairs"],
-                pair_slots=info["pair_slots"])
+    survey = (co * (4 + vb) + col.size * (4 + vb) + 3 * m * es) / world
+    # the kernel's algorithmic bytes: the stored pair stream it must read once per K·p (uint16 j + s_ij
+    # per slot, rows padded to 8 per cell); SURVEY's column-join figure counts every co-occurrence
+    # with multiplicity at 8 B, more than this algorithm needs, so it is reported as an effective rate
+    stream = info["pair_slots"] * (2 + es)
+    return dict(bound="hbm", achieved=stream / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
+                frac=stream / s / PEAKS["hbm"], traffic=None, kernel="gram_kp_kernel", launch_ms=ms_dom,
+                alg_bytes=stream, alg_bytes_def="stored pair stream: pair_slots x (2 + sizeof(real))",
+                survey_alg_bytes=survey, survey_effective_GBps=survey / s / 1e9,
+                survey_effective_frac=survey / s / PEAKS["hbm"], pairs=info["pairs"], pair_slots=info["pair_slots"])
 
 
-def pmc_traffic(config, n, d, world, kernel):
+def _pmc_match(t, n, d, world, dtype, kfun, default_cfg):
+    """A committed PMC summary applies only to the exact workload: N, d, world, real type and kernel
+    function (files written before these fields existed hold the configuration's defaults)."""
+    if t["N"] != n or t["d"] != d or t["n_gpus"] != world:
+        return False
+    if "dtype" in t or "kernel_function" in t:
+        return t.get("dtype") == dtype and t.get("kernel_function") == kfun
+    return default_cfg
+
+
+def pmc_traffic(config, n, d, world, kernel, dtype, kfun, default_cfg):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC pass of this exact
     workload (profiles/*_<config>_traffic.json, written by tools/pmc_traffic.py), else None."""
     import glob
 
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_traffic.json")), reverse=True):
         t = json.load(open(path))
-        if t["N"] == n and t["d"] == d and t["n_gpus"] == world and kernel == t["kernel"]:
+        if kernel == t["kernel"] and _pmc_match(t, n, d, world, dtype, kfun, default_cfg):
             return t["hbm_read_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None
 
 
-def pmc_mfma(config, n, d, world, kernel):
+def pmc_mfma(config, n, d, world, kfun, dtype):
     """MFMA utilisation of the dense tile kernel from the newest committed PMC pass of this exact
     workload (profiles/*_<config>_mfma.json, written from tools/pmc_dense.sh), else None."""
     import glob
 
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_mfma.json")), reverse=True):
         t = json.load(open(path))
-        if t["N"] == n and t["d"] == d and t["n_gpus"] == world and t["kernel"] == kernel:
+        if t["N"] == n and t["d"] == d and t["n_gpus"] == world and t["kernel"] == kfun and \
+                t.get("dtype", CONFIG_DTYPE.get(config)) == dtype:
             return t["mfma_util"], os.path.relpath(path, ROOT)
     return None, None
 

@@ -97,6 +97,25 @@ PLSSVM_MI_API int plssvm_mi_set_qa_cost(plssvm_mi_ctx *ctx, double qa_cost);
 PLSSVM_MI_API int plssvm_mi_get_unique_id(void *id_out);
 PLSSVM_MI_API int plssvm_mi_comm_init(plssvm_mi_ctx *ctx, int rank, int world_size, const void *unique_id);
 
+/* Host-staged group exchange: the reference's own device_reduction semantics
+ * (src/plssvm/backends/gpu_csvm.cpp:366-386: synchronise, copy the partial vector to the host,
+ * combine there, copy the result back) with the combine step supplied by the caller, e.g. a
+ * torch.distributed / MPI / gloo collective. Every rank of the group calls it with the same
+ * world_size instead of plssvm_mi_comm_init; the engine then runs exactly the multi-rank work split
+ * of the RCCL path (partition -> this rank's share -> exchange -> replicated CG) but moves each
+ * exchange through `fn` on the host. Use: groups without RCCL, and several ranks sharing one GPU
+ * (RCCL refuses two ranks on one device) — the multi-rank path's test transport on a 1-GPU box.
+ *   fn(buf, count, real_bytes, op, user) must return 0 on success and be called collectively:
+ *   op == PLSSVM_MI_XCHG_ALLREDUCE: buf[count] (real_bytes-wide reals) := sum over ranks, the same
+ *                                   bits on every rank;
+ *   op == PLSSVM_MI_XCHG_ALLGATHER: buf[world_size * count]: rank r's chunk [r*count, (r+1)*count)
+ *                                   is valid on rank r; fill every other rank's chunk. */
+#define PLSSVM_MI_XCHG_ALLREDUCE 0
+#define PLSSVM_MI_XCHG_ALLGATHER 1
+typedef int (*plssvm_mi_exchange_fn)(void *buf, int64_t count, int real_bytes, int op, void *user);
+PLSSVM_MI_API int plssvm_mi_comm_init_host(plssvm_mi_ctx *ctx, int rank, int world_size, plssvm_mi_exchange_fn fn,
+                                           void *user);
+
 /* Host-only (no GPU needed): the work split of the implicit matrix for m = n - 1 rows.
  * out4 = { first super-block, end super-block, total tiles, tiles owned by `rank` } where a tile
  * is 128x128 of the lower triangle and a super-block 8x8 tiles (linear index I(I+1)/2 + J). */
@@ -130,6 +149,18 @@ PLSSVM_MI_API int plssvm_mi_generate_q(plssvm_mi_ctx *ctx, void *q_out, double *
  * ret[m] += add * Q~ p, Q~_ij = k(x_i,x_j) + QA_cost - q_i - q_j + [i==j]/C. q may be NULL to use
  * the context's q (from generate_q); otherwise q[m] is uploaded first. All host buffers. */
 PLSSVM_MI_API int plssvm_mi_kp(plssvm_mi_ctx *ctx, const void *q, const void *p, void *ret, double add);
+
+/* Test hook (the protected-for-mock parts of run_device_kernel, tests/backends/HIP/mock_hip_csvm.hpp:
+ * 24-51): out[m] = one part of Q~p for host p[m], after the group exchange:
+ *   PLSSVM_MI_PART_KERNEL  : sum_{j<m} k(x_i, x_j) p_j  (Q~p without the QA_cost - q_i - q_j and 1/C
+ *                            terms, which are applied analytically in O(m));
+ *   PLSSVM_MI_PART_OVERLAP : sparse poly/rbf only — sum over j != i sharing a feature with i of
+ *                            (k_ij - kappa_ij) p_j, kappa_ij the value non-overlapping pairs take
+ *                            (e_i e_j for rbf, coef0^degree for poly): exactly the per-pair work of the
+ *                            sparse K·p kernels, without the separable and diagonal terms. */
+#define PLSSVM_MI_PART_KERNEL 0
+#define PLSSVM_MI_PART_OVERLAP 1
+PLSSVM_MI_API int plssvm_mi_kp_part(plssvm_mi_ctx *ctx, const void *p, void *out, int part);
 
 /* gpu_csvm::solver_CG (src/plssvm/backends/gpu_csvm.cpp:186-324) with the OpenMP backend's
  * normative semantics (src/plssvm/backends/OpenMP/csvm.cpp:82-170; including the every-50th

@@ -25,7 +25,7 @@ from . import io as _io
 from .io import parse_libsvm, parse_model, read_binary, write_binary
 
 __all__ = ["Parameter", "CSVM", "BackendError", "parse_libsvm", "parse_model", "read_binary", "write_binary",
-           "device_count", "unique_id", "partition"]
+           "device_count", "unique_id", "partition", "torch_exchange"]
 
 
 def device_count() -> int:
@@ -45,6 +45,32 @@ def partition(m, rank, world_size):
     out = (ctypes.c_int64 * 4)()
     _abi.check(_abi.lib().plssvm_mi_partition(m, rank, world_size, out))
     return tuple(out)
+
+
+def torch_exchange(dist, group=None):
+    """Host-staged exchange (plssvm_mi_comm_init_host) over torch.distributed, e.g. gloo: every rank
+    all-gathers the buffers and sums them in rank order 0..G-1, so all ranks get the same bits — the
+    reference's device_reduction, which sums devices 0..G-1 on the host (gpu_csvm.cpp:366-386)."""
+    import torch
+
+    def fn(buf, op):
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        if op == _abi.XCHG_ALLGATHER:
+            count = buf.size // world
+            parts = [torch.empty(count, dtype=torch.from_numpy(buf[:0]).dtype) for _ in range(world)]
+            dist.all_gather(parts, torch.from_numpy(buf[rank * count:(rank + 1) * count].copy()), group=group)
+            for r in range(world):
+                buf[r * count:(r + 1) * count] = parts[r].numpy()
+        else:
+            parts = [torch.empty(buf.size, dtype=torch.from_numpy(buf[:0]).dtype) for _ in range(world)]
+            dist.all_gather(parts, torch.from_numpy(buf.copy()), group=group)
+            acc = parts[0].numpy().copy()
+            for r in range(1, world):
+                acc += parts[r].numpy()
+            buf[:] = acc
+
+    return fn
 
 
 def _ptr(a):
@@ -111,7 +137,7 @@ class CSVM:
     """One MI355X context (one GPU, one HIP stream). ``world_size > 1`` joins a row-block group."""
 
     def __init__(self, params: Parameter, device=0, rank=0, world_size=1, uid=None, kp_mode="auto",
-                 sim_rank=None, rbf_form=0):
+                 sim_rank=None, rbf_form=0, exchange=None):
         if params.data is None and params.csr is None and params.coo is None:
             raise ValueError("No data points provided!")
         if params.data is not None:
@@ -135,7 +161,10 @@ class CSVM:
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_RBF_FORM, rbf_form))
         if sim_rank is not None:  # (rank, world): single-GPU test hook, see PLSSVM_MI_OPT_SIM_RANK
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_SIM_RANK, sim_rank[0] | (sim_rank[1] << 16)))
-        if world_size > 1 or uid is not None:  # a single-rank group (uid given) also runs its collectives on RCCL
+        if exchange is not None:  # host-staged group: fn(numpy buffer, op) combines in place (torch_exchange)
+            self._xchg = _abi.EXCHANGE_FN(self._exchange_cb(exchange, world_size))
+            self._check(L.plssvm_mi_comm_init_host(self._ctx, rank, world_size, self._xchg, None))
+        elif world_size > 1 or uid is not None:  # a single-rank group (uid given) also runs its collectives on RCCL
             if uid is None:
                 raise ValueError("world_size > 1 needs the group's unique id (rank 0: plssvm_sparse_fp22_amd.unique_id())")
             self._uid = ctypes.create_string_buffer(uid, _abi.UNIQUE_ID_BYTES)
@@ -149,6 +178,23 @@ class CSVM:
         self.trace = None
         self.iters = None
         self._on_device = False
+
+    @staticmethod
+    def _exchange_cb(exchange, world_size):
+        def cb(ptr, count, real_bytes, op, user):
+            try:
+                n = count * (world_size if op == _abi.XCHG_ALLGATHER else 1)
+                ct = ctypes.c_float if real_bytes == 4 else ctypes.c_double
+                buf = np.ctypeslib.as_array((ct * n).from_address(ptr))
+                exchange(buf, op)
+                return 0
+            except Exception:  # noqa: BLE001 — reported as PLSSVM_MI_ERR_RCCL by the library
+                import traceback
+
+                traceback.print_exc()
+                return -1
+
+        return cb
 
     # ---- lifetime ----
     def close(self):
@@ -217,6 +263,15 @@ class CSVM:
         dd = np.ascontiguousarray(d, dtype=self.dtype)
         self._check(_abi.lib().plssvm_mi_kp(self._ctx, _ptr(qq), _ptr(dd), _ptr(ret), float(add)))
         return ret
+
+    def kp_part(self, p, part="kernel"):
+        """Test hook (plssvm_mi_kp_part): 'kernel' = sum_j k(x_i, x_j) p_j; 'overlap' = the sparse
+        poly/rbf overlap sum (the per-pair work of the sparse kernels only)."""
+        pp = np.ascontiguousarray(p, dtype=self.dtype)
+        out = np.zeros(max(self.m, 1), dtype=self.dtype)
+        code = {"kernel": _abi.PART_KERNEL, "overlap": _abi.PART_OVERLAP}[part]
+        self._check(_abi.lib().plssvm_mi_kp_part(self._ctx, _ptr(pp), _ptr(out), code))
+        return out[: self.m]
 
     def solver_CG(self, b, imax, eps, q=None):
         b = np.ascontiguousarray(b, dtype=self.dtype)

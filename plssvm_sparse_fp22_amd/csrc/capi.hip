@@ -149,6 +149,11 @@ int plssvm_mi_comm_init(plssvm_mi_ctx *ctx, int rank, int world_size, const void
     return ctx->call([&](auto &e) { e.comm_init(rank, world_size, unique_id); });
 }
 
+int plssvm_mi_comm_init_host(plssvm_mi_ctx *ctx, int rank, int world_size, plssvm_mi_exchange_fn fn, void *user) {
+    if (!ctx || !fn) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) { e.comm_init_host(rank, world_size, fn, user); });
+}
+
 int plssvm_mi_setup_dense(plssvm_mi_ctx *ctx, const void *X, int64_t n, int64_t d) {
     if (!ctx) return PLSSVM_MI_ERR_ARG;
     return ctx->call([&](auto &e) {
@@ -228,6 +233,14 @@ int plssvm_mi_kp(plssvm_mi_ctx *ctx, const void *q, const void *p, void *ret, do
     return ctx->call([&](auto &e) {
         using T = std::remove_reference_t<decltype(e.gamma)>;
         e.kp_host(static_cast<const T *>(q), static_cast<const T *>(p), static_cast<T *>(ret), (T) add);
+    });
+}
+
+int plssvm_mi_kp_part(plssvm_mi_ctx *ctx, const void *p, void *out, int part) {
+    if (!ctx || !p || !out) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        using T = std::remove_reference_t<decltype(e.gamma)>;
+        e.kp_part(static_cast<const T *>(p), static_cast<T *>(out), part);
     });
 }
 

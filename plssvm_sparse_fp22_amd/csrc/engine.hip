@@ -135,15 +135,53 @@ void engine<T>::comm_init(int rank_, int world_, const void *uid) {
 }
 
 template <typename T>
+void engine<T>::comm_init_host(int rank_, int world_, int (*fn)(void *, int64_t, int, int, void *), void *user) {
+    if (world_ < 1 || rank_ < 0 || rank_ >= world_) throw mi_error(-1, "invalid rank/world_size");
+    if (fn == nullptr) throw mi_error(-1, "a host-staged group needs an exchange function");
+    if (have_data) throw mi_error(-6, "plssvm_mi_comm_init_host must be called before setup");
+    if (sim_world > 0) throw mi_error(-1, "a simulated rank cannot join a group");
+    MI_HIP_CHECK(hipSetDevice(device));
+    if (comm) {
+        (void) ncclCommDestroy(comm);
+        comm = nullptr;
+    }
+    rank = rank_;
+    world = world_;
+    xchg = fn;
+    xchg_user = user;
+}
+
+// Exchange step of one K·p. RCCL: in-stream collective. Host-staged: the reference's
+// device_reduction (gpu_csvm.cpp:366-386) — synchronise, D2H, combine on the host (caller's
+// collective), H2D — so the device work before and after is exactly the RCCL path's.
+template <typename T>
 void engine<T>::allreduce(T *buf, int64_t count) {
-    if (comm == nullptr || count <= 0) return;
-    MI_NCCL_CHECK(ncclAllReduce(buf, buf, (size_t) count, nccl_type<T>(), ncclSum, comm, stream));
+    if (count <= 0) return;
+    if (comm != nullptr) {
+        MI_NCCL_CHECK(ncclAllReduce(buf, buf, (size_t) count, nccl_type<T>(), ncclSum, comm, stream));
+    } else if (xchg != nullptr) {
+        xbuf.resize((size_t) count);
+        MI_HIP_CHECK(hipMemcpyAsync(xbuf.data(), buf, sizeof(T) * (size_t) count, hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        if (xchg(xbuf.data(), count, (int) sizeof(T), 0, xchg_user) != 0) throw mi_error(-3, "host exchange failed");
+        MI_HIP_CHECK(hipMemcpyAsync(buf, xbuf.data(), sizeof(T) * (size_t) count, hipMemcpyHostToDevice, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));  // xbuf is reused by the next exchange
+    }
 }
 
 template <typename T>
 void engine<T>::allgather_rows(T *buf) {
-    if (comm == nullptr) return;
-    MI_NCCL_CHECK(ncclAllGather(buf + (int64_t) rank * chunk, buf, (size_t) chunk, nccl_type<T>(), comm, stream));
+    if (comm != nullptr) {
+        MI_NCCL_CHECK(ncclAllGather(buf + (int64_t) rank * chunk, buf, (size_t) chunk, nccl_type<T>(), comm, stream));
+    } else if (xchg != nullptr) {
+        const int64_t total = chunk * world;
+        xbuf.resize((size_t) total);
+        MI_HIP_CHECK(hipMemcpyAsync(xbuf.data(), buf, sizeof(T) * (size_t) total, hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        if (xchg(xbuf.data(), chunk, (int) sizeof(T), 1, xchg_user) != 0) throw mi_error(-3, "host exchange failed");
+        MI_HIP_CHECK(hipMemcpyAsync(buf, xbuf.data(), sizeof(T) * (size_t) total, hipMemcpyHostToDevice, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+    }
 }
 
 template <typename T>
@@ -282,6 +320,25 @@ void engine<T>::kp_host(const T *q_host, const T *p, T *ret_host, T add) {
         MI_HIP_CHECK(hipMemcpyAsync(ret.get(), ret_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
         kp_device(pv.get(), ret.get(), add, false, nullptr);
         MI_HIP_CHECK(hipMemcpyAsync(ret_host, ret.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
+    }
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+// test hook: one part of Q~p (PLSSVM_MI_PART_KERNEL: sum_j k_ij p_j; PLSSVM_MI_PART_OVERLAP: the
+// sparse overlap sum only), after the group exchange
+template <typename T>
+void engine<T>::kp_part(const T *p_host, T *out_host, int part) {
+    need_data();
+    if (part != 0 && part != 1) throw mi_error(-1, "unknown K·p part");
+    if (part == 1 && !(sparse && !factored())) throw mi_error(-5, "the overlap part exists for sparse poly/rbf only");
+    MI_HIP_CHECK(hipSetDevice(device));
+    cg_active = false;
+    MI_HIP_CHECK(hipMemsetAsync(sc.get(), 0, sizeof(cg_scalars<T>), stream));
+    if (m > 0) {
+        MI_HIP_CHECK(hipMemcpyAsync(pv.get(), p_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
+        if (part == 1) sparse_kp_raw(pv.get(), nullptr, false);
+        else kp_raw(pv.get(), nullptr);
+        MI_HIP_CHECK(hipMemcpyAsync(out_host, raw.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
 }

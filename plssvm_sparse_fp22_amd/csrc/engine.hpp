@@ -35,6 +35,10 @@ struct engine : engine_base {
     // ---- multi-GPU row-block group ----
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
+    // host-staged exchange (plssvm_mi_comm_init_host): the reference's device_reduction transport
+    int (*xchg)(void *, int64_t, int, int, void *) = nullptr;
+    void *xchg_user = nullptr;
+    std::vector<T> xbuf;
     // test hook: compute only rank sim_rank's share of a sim_world group, no collective, rank-1
     // terms only on sim rank 0 (so the shares of all sim ranks sum to the full K·p)
     int sim_rank = 0, sim_world = 0;
@@ -72,6 +76,8 @@ struct engine : engine_base {
     void need_q() const;
 
     void comm_init(int rank_, int world_, const void *uid);
+    void comm_init_host(int rank_, int world_, int (*fn)(void *, int64_t, int, int, void *), void *user);
+    void kp_part(const T *p_host, T *out_host, int part);  // test hook, PLSSVM_MI_PART_*
     void setup_dense(const T *X, int64_t n_, int64_t d_);
     void setup_csr(const int64_t *rowptr, const int32_t *col, const void *val, int val_fmt, int64_t n_, int64_t d_);
     void finish_setup();
@@ -93,7 +99,8 @@ struct engine : engine_base {
     // sparse paths (sparse.hip)
     void sparse_q();                                              // q, norms, e on CSR data
     void build_gram_blocks(const int64_t *cpos, int64_t max_inc);  // sparse Gram pattern (pairwise kernels)
-    void sparse_kp_raw(const T *p, const cg_scalars<T> *status);  // raw[i] = sum_j k_ij p_j, i < m
+    // raw[i] = sum_j k_ij p_j, i < m (with_base = false: only the overlap terms, PLSSVM_MI_PART_OVERLAP)
+    void sparse_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base = true);
     void sparse_dominant(const T *p, const cg_scalars<T> *status);  // the dominant sparse kernel
     void spmv_pass_csc(const T *p, const cg_scalars<T> *status);    // factored linear: w = X^T p
     void spmv_pass_csr(const cg_scalars<T> *status);                // factored linear: raw = X w

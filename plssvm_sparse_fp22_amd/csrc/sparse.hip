@@ -214,6 +214,27 @@ __device__ __forceinline__ T fast_exp2(T x) {
     else return exp2(x);
 }
 
+// e^y - 1 without the cancellation of exp(y) - 1 near 0 (the factored rbf pair form evaluates it at
+// y = 2 g s_ij, about 1e-5 on the BASELINE sets, where exp(y) - 1 in fp32 keeps only ~2 digits).
+// fp32: degree-7 Taylor polynomial for |y| < 1/4 (truncation < 2e-9 relative), v_exp_f32 - 1 above
+// (relative error < 1e-6 there); both evaluated and selected, no branch. fp64: the device libm expm1.
+template <typename T>
+__device__ __forceinline__ T expm1_acc(T y) {
+    if constexpr (sizeof(T) == 4) {
+        float t = fmaf(y, 1.0f / 5040.0f, 1.0f / 720.0f);
+        t = fmaf(y, t, 1.0f / 120.0f);
+        t = fmaf(y, t, 1.0f / 24.0f);
+        t = fmaf(y, t, 1.0f / 6.0f);
+        t = fmaf(y, t, 0.5f);
+        t = fmaf(y, t, 1.0f);
+        const float small = y * t;
+        const float big = __builtin_amdgcn_exp2f(y * 1.4426950408889634f) - 1.0f;
+        return fabsf(y) < 0.25f ? small : big;
+    } else {
+        return expm1(y);
+    }
+}
+
 __device__ __forceinline__ unsigned long long fx_round(double x) {
     return (unsigned long long) (__double_as_longlong(x + 6755399441055744.0) - 0x4338000000000000LL);
 }
@@ -337,6 +358,7 @@ __global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const g
     };
     // exp(-g dist) = exp2(-g log2(e) dist); exp(2 g s) = exp2(2 g log2(e) s)
     const T lg = gamma * T(1.4426950408889634);
+    const T g2 = T(2) * gamma;
     const int64_t clast = wend - 1;  // clamp target for the loads of idle lanes (wend > wbeg when used)
 
     uint4 jv_n = make_uint4(0, 0, 0, 0);
@@ -386,7 +408,7 @@ __global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const g
             for (int k = 0; k < 8; ++k) {
                 T cv;
                 if (KERNEL == 3) {
-                    cv = (ABL & 2) ? lg * s[k] : fast_exp2(T(2) * lg * s[k]) - T(1);  // pads: s = 0 -> 0
+                    cv = (ABL & 2) ? lg * s[k] : expm1_acc(g2 * s[k]);  // pads: s = 0 -> 0
                 } else if (KERNEL == 2) {
                     T dist = ni + wn[jl[k]] - T(2) * s[k];
                     dist = dist > T(0) ? dist : T(0);
@@ -873,7 +895,7 @@ void engine<T>::sparse_q() {
 }
 
 template <typename T>
-void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status) {
+void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base) {
     if (factored()) {
         spmv_pass_csc(p, status);
         allreduce(w.get(), d);
@@ -889,7 +911,7 @@ void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status) {
                        csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, csr.rb0, csr.rb1, raw.get(), status);
     MI_LAUNCH_CHECK();
     allreduce(raw.get(), m);
-    if (!(sim_world > 0 && sim_rank != 0)) {
+    if (with_base && !(sim_world > 0 && sim_rank != 0)) {
         T kappa = 0;
         if (kernel == 1) {
             kappa = 1;
@@ -940,7 +962,7 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
     template void engine<T>::setup_csr(const int64_t *, const int32_t *, const void *, int, int64_t, int64_t); \
     template void engine<T>::build_gram_blocks(const int64_t *, int64_t);                                     \
     template void engine<T>::sparse_q();                                                                      \
-    template void engine<T>::sparse_kp_raw(const T *, const cg_scalars<T> *);                                 \
+    template void engine<T>::sparse_kp_raw(const T *, const cg_scalars<T> *, bool);                           \
     template void engine<T>::sparse_dominant(const T *, const cg_scalars<T> *);                               \
     template void engine<T>::spmv_pass_csc(const T *, const cg_scalars<T> *);                                 \
     template void engine<T>::spmv_pass_csr(const cg_scalars<T> *);

@@ -137,3 +137,42 @@ def test_partition_covers_triangle(world, m):
     if nb > 64 * world:
         loads = [p[3] for p in parts]
         assert max(loads) - min(loads) <= 2 * 64  # each boundary within one super-block
+
+
+def _xchg_worker(rank, world, port, result):
+    import torch.distributed as dist
+
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import plssvm_sparse_fp22_amd as pm
+    from plssvm_sparse_fp22_amd import _abi
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    fn = pm.torch_exchange(dist)
+    rng = np.random.default_rng(100 + rank)
+    a = rng.standard_normal(1001)
+    parts = [np.random.default_rng(100 + r).standard_normal(1001) for r in range(world)]
+    want = parts[0].copy()
+    for r in range(1, world):
+        want += parts[r]
+    fn(a, _abi.XCHG_ALLREDUCE)
+    g = np.zeros(world * 7, dtype=np.float32)
+    g[rank * 7:(rank + 1) * 7] = rank + 1
+    fn(g, _abi.XCHG_ALLGATHER)
+    result[rank] = dict(sum_ok=bool(np.array_equal(a, want)), gather=g)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_exchange_over_gloo(world):
+    """plssvm_mi_comm_init_host's exchange over torch.distributed (torch_exchange): the all-reduce is the
+    rank-order sum (the reference's device_reduction order, gpu_csvm.cpp:366-386) with identical bits on
+    every rank; the all-gather fills every rank's chunk."""
+    import torch.multiprocessing as mp
+
+    manager = mp.Manager()
+    result = manager.dict()
+    mp.spawn(_xchg_worker, args=(world, _free_port(), result), nprocs=world, join=True)
+    for r in range(world):
+        assert result[r]["sum_ok"]
+        np.testing.assert_array_equal(result[r]["gather"], np.repeat(np.arange(1, world + 1), 7).astype(np.float32))
