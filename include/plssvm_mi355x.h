@@ -216,6 +216,8 @@ typedef struct {
     int64_t pair_slots; /* sparse pairwise kernels: stored pair slots incl. padding (K·p stream) */
     int64_t spmv_bytes; /* sparse factored linear: HBM bytes both SpMV passes move per K·p (padded SELL
                            stream, slot maps, panel partials) */
+    int rbf_small_args; /* sparse factored rbf: 1 = every 2 g |s_ij| is below the short Taylor form's bound */
+    int reserved_;
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
 

@@ -44,7 +44,8 @@ class Info(ctypes.Structure):
     _fields_ = [(k, ctypes.c_int64) for k in ("n", "d", "m", "n_pad", "d_pad", "nnz", "tiles_total", "tiles_local",
                                               "tile_rows", "tile_cols", "device_bytes", "pairs")] + \
                [(k, ctypes.c_int) for k in ("kp_mode", "rank", "world_size", "real_bytes", "kernel", "is_sparse",
-                                            "val_fmt", "rbf_factored")] + [("pair_slots", ctypes.c_int64), ("spmv_bytes", ctypes.c_int64)]
+                                            "val_fmt", "rbf_factored")] + [("pair_slots", ctypes.c_int64), ("spmv_bytes", ctypes.c_int64)] + \
+               [("rbf_small_args", ctypes.c_int), ("reserved_", ctypes.c_int)]
 
 
 class BackendError(RuntimeError):

@@ -366,6 +366,7 @@ int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
         info->rbf_factored = e.csr.rbf_factored ? 1 : 0;
         info->pair_slots = e.csr.slots;
         info->spmv_bytes = e.csr.spmv_csc.stream_bytes() + e.csr.spmv_csr.stream_bytes();
+        info->rbf_small_args = e.csr.rbf_small ? 1 : 0;
     });
 }
 

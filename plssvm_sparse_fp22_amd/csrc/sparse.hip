@@ -235,6 +235,24 @@ __device__ __forceinline__ T expm1_acc(T y) {
     }
 }
 
+// e^y - 1 for |y| < expm1_small_bound<T>(): Taylor polynomial of degree 3 (fp32) / 5 (fp64), relative
+// truncation error < 2^-26 / 2^-55 — cheaper than one v_exp_f32 and exact to rounding, used when the
+// setup's bound 2 g max|s_ij| is below it (every cell of the BASELINE sparse sets: 2 g |s| < 1e-4)
+template <typename T>
+constexpr double expm1_small_bound() { return sizeof(T) == 4 ? 0.007 : 0.0017; }
+
+template <typename T>
+__device__ __forceinline__ T expm1_small(T y) {
+    if constexpr (sizeof(T) == 4) {
+        return y * fmaf(y, fmaf(y, 1.0f / 6.0f, 0.5f), 1.0f);
+    } else {
+        double t = fma(y, 1.0 / 120.0, 1.0 / 24.0);
+        t = fma(y, t, 1.0 / 6.0);
+        t = fma(y, t, 0.5);
+        return y * fma(y, t, 1.0);
+    }
+}
+
 __device__ __forceinline__ unsigned long long fx_round(double x) {
     return (unsigned long long) (__double_as_longlong(x + 6755399441055744.0) - 0x4338000000000000LL);
 }
@@ -257,6 +275,7 @@ __global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const g
     constexpr int NT = gram_wg<T, KERNEL>();
     constexpr int CW = GRAM_CW, NWAVE = NT / 64;
     constexpr bool NEED_N = KERNEL == 2, NEED_E = KERNEL == 2;
+    constexpr bool FACT = KERNEL == 3 || KERNEL == 4;  // factored rbf: c_ij = e_i e_j expm1(2 g s_ij)
     using acc_t = unsigned long long;
     __shared__ T wn[NEED_N ? CW : 1], we[NEED_E ? CW : 1], wp[CW];
     __shared__ acc_t colacc[CW];
@@ -275,14 +294,14 @@ __global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const g
         const bool ok = t < wlen;
         if (NEED_N) wn[t] = ok ? norms[W0 + t] : T(0);
         if (NEED_E) we[t] = ok ? ev[W0 + t] : T(0);
-        const T pv = ok ? (KERNEL == 3 ? ev[W0 + t] * p[W0 + t] : p[W0 + t]) : T(0);
+        const T pv = ok ? (FACT ? ev[W0 + t] * p[W0 + t] : p[W0 + t]) : T(0);
         wp[t] = pv;
         pmax = max(pmax, fabs(pv));
         colacc[t] = 0;
     }
     for (int t = tid; t < GRAM_RB; t += NT) {
         rowacc[t] = 0;
-        if (t < rows) pmax = max(pmax, fabs(KERNEL == 3 ? ev[I0 + t] * p[I0 + t] : p[I0 + t]));
+        if (t < rows) pmax = max(pmax, fabs(FACT ? ev[I0 + t] * p[I0 + t] : p[I0 + t]));
     }
     for (int t = tid; t <= rows; t += NT) ro[t] = rowoff[cell.rowoff + t];
 #pragma unroll
@@ -294,7 +313,7 @@ __global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const g
     for (int w = 1; w < NWAVE; ++w) pmax = max(pmax, wmax[w]);
     // bound on |c| (|g| for the factored rbf) over the cell's pairs
     double cb;
-    if (KERNEL == 3) {
+    if (FACT) {
         cb = expm1(2.0 * fabs((double) gamma) * cell.smax);
     } else if (KERNEL == 2) {
         cb = 1.0;
@@ -348,7 +367,7 @@ __global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const g
     T pa_n = 0, pb_n = 0, ni_n = 0, ei_n = 0;
     auto load_row = [&]() {
         const int64_t g = I0 + min(r, rows - 1);
-        if (KERNEL == 3) {
+        if (FACT) {
             pa_n = ev[g], pb_n = p[g];
         } else {
             pa_n = p[g];
@@ -382,7 +401,7 @@ __global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const g
 #pragma unroll
         for (int k = 0; k < 8; ++k) s[k] = s_n[k];
         const int rc = r_n;
-        const T pi = KERNEL == 3 ? pa_n * pb_n : pa_n, ni = ni_n, ei = ei_n;
+        const T pi = FACT ? pa_n * pb_n : pa_n, ni = ni_n, ei = ei_n;
         // issue the next step: stream, seek, row factors
         if (cb + 64 < wend) {  // wave-uniform
             const int64_t cn = cb + 64 + lane;
@@ -407,7 +426,9 @@ __global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const g
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 T cv;
-                if (KERNEL == 3) {
+                if (KERNEL == 4) {  // |2 g s| below the small-argument bound of every cell (setup)
+                    cv = (ABL & 2) ? lg * s[k] : expm1_small(g2 * s[k]);  // pads: s = 0 -> 0
+                } else if (KERNEL == 3) {
                     cv = (ABL & 2) ? lg * s[k] : expm1_acc(g2 * s[k]);  // pads: s = 0 -> 0
                 } else if (KERNEL == 2) {
                     T dist = ni + wn[jl[k]] - T(2) * s[k];
@@ -442,12 +463,12 @@ __global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const g
     __syncthreads();
     for (int t = tid; t < rows; t += NT) {
         T v = (T) ldexp((double) (long long) rowacc[t], qe);
-        if (KERNEL == 3) v *= ev[I0 + t];
+        if (FACT) v *= ev[I0 + t];
         slab_row[(int64_t) cell.W * m_pad + I0 + t] = v;
     }
     for (int t = tid; t < wlen; t += NT) {
         T v = (T) ldexp((double) (long long) colacc[t], qe);
-        if (KERNEL == 3) v *= ev[W0 + t];
+        if (FACT) v *= ev[W0 + t];
         slab_col[(int64_t) cell.I * m_pad + W0 + t] = v;
     }
 }
@@ -868,6 +889,15 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
     if (kernel == 2) {
         const double gmax = std::fabs((double) gamma) * (double) abs_max(norms.get(), m, stream);
         csr.rbf_factored = rbf_form != 1 && gmax <= (sizeof(T) == 8 ? 300.0 : 40.0);
+        // every pair's 2 g |s_ij| below the small-argument polynomial's bound -> KERNEL 4
+        std::vector<gram_cell> hc((size_t) csr.ncells);
+        if (csr.ncells)
+            MI_HIP_CHECK(hipMemcpyAsync(hc.data(), csr.cells.get(), sizeof(gram_cell) * hc.size(), hipMemcpyDeviceToHost,
+                                        stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        double smax = 0.0;
+        for (const auto &c : hc) smax = std::max(smax, c.smax);
+        csr.rbf_small = 2.0 * std::fabs((double) gamma) * smax < expm1_small_bound<T>();
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
     csr.have_gram = true;
@@ -946,6 +976,7 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
         constexpr int A = decltype(abl)::value;
         if (kernel == 0) launch(gram_kp_kernel<T, 0, A>, gram_wg<T, 0>());
         else if (kernel == 1) launch(gram_kp_kernel<T, 1, A>, gram_wg<T, 1>());
+        else if (csr.rbf_factored && csr.rbf_small) launch(gram_kp_kernel<T, 4, A>, gram_wg<T, 4>());
         else if (csr.rbf_factored) launch(gram_kp_kernel<T, 3, A>, gram_wg<T, 3>());
         else launch(gram_kp_kernel<T, 2, A>, gram_wg<T, 2>());
     };

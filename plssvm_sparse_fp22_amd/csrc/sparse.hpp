@@ -48,6 +48,7 @@ struct csr_data {
     int64_t pairs = 0, pair_bound = 0;  // unique overlapping pairs; incidence bound
     int64_t slots = 0;                   // stored pair slots (rows padded to 8 per cell)
     bool rbf_factored = false;  // rbf pairs as e_i e_j (exp(2 g s) - 1), see sparse.hip
+    bool rbf_small = false;     // ... with 2 g |s_ij| small enough for the short Taylor form (expm1_small)
     int64_t nRB = 0, nW = 0, rb0 = 0, rb1 = 0, m_pad = 0, ncells = 0;
     dev_buf<uint16_t> pj;
     dev_buf<T> ps;

@@ -10,8 +10,10 @@ rank's share of the K·p kernels, the exchange, and the replicated device-reside
 RCCL group in test_gpu_parity.py::test_single_rank_rccl_group.)
 
 Both ranks' q, K·p (add = -1, +1), kernel part, CG delta trace, alpha and bias are compared with the
-oracle (fp64: K·p 1e-12 of max, trace 1e-6 per iteration, alpha 1e-9 of max; fp32/FP22: 1e-4 / 1e-3 /
-2e-2) and with each other (bit for bit: the CG is replicated).
+oracle (fp64: K·p 1e-12 of max, trace 1e-6 per iteration, alpha 1e-9 of max; fp32/FP22: K·p 1e-4,
+trace 1e-3 while |r|/|r0| >= 1e-3 and alpha 2e-2, or 10x the oracle's own 1-vs-8-thread spread where
+that is larger) and with each other (bit for bit:
+the CG is replicated).
 """
 import os
 import socket
@@ -76,6 +78,13 @@ def test_world2_group_matches_oracle(oracle, case, tmp_path):
     f64 = dtype == np.float64
     ktol, ttol, atol_ = (1e-12, 1e-6, 1e-9) if f64 else (1e-4, 1e-3, 2e-2)
     ref = oracle.learn(kernel, od, y, imax=imax, **args)
+    if not f64:  # fp32: the reference's own run-to-run spread (1 vs 8 OpenMP threads) widens the bar
+        ref1 = oracle.learn(kernel, od, y, imax=imax, nthreads=1, **args)
+        ref8 = oracle.learn(kernel, od, y, imax=imax, nthreads=8, **args)
+        n8 = min(len(ref1["trace"]), len(ref8["trace"]))
+        spread_t = np.abs(ref8["trace"][:n8] / ref1["trace"][:n8] - 1).max()
+        spread_a = np.abs(ref8["alpha"] - ref1["alpha"]).max() / np.abs(ref1["alpha"]).max()
+        ttol, atol_ = max(ttol, 10 * spread_t), max(atol_, 10 * spread_a)
 
     # the split is real: every rank owns a non-empty, disjoint part of the work
     if layout == "dense" and kp_mode != "factored":
@@ -91,8 +100,11 @@ def test_world2_group_matches_oracle(oracle, case, tmp_path):
             np.testing.assert_allclose(r[key], want, rtol=0, atol=ktol * np.abs(want).max(),
                                        err_msg=f"{case} rank {rank} add={add}")
         assert int(r["iters"]) == ref["iters"], (case, rank, int(r["iters"]), ref["iters"])
-        n_tr = len(ref["trace"]) if f64 else min(3, len(ref["trace"]))
-        np.testing.assert_allclose(r["trace"][:n_tr], ref["trace"][:n_tr], rtol=ttol, err_msg=f"{case} rank {rank}")
+        # fp32: compare the trace while the residual is above the fp32 rounding floor (delta/delta0 >= 1e-6,
+        # i.e. |r|/|r0| >= 1e-3); below it every fp32 CG, the reference's included, follows its own rounding
+        live = np.ones(len(ref["trace"]), bool) if f64 else ref["trace"] / ref["trace"][0] >= 1e-6
+        np.testing.assert_allclose(r["trace"][:len(live)][live], ref["trace"][live], rtol=ttol,
+                                   err_msg=f"{case} rank {rank}")
         np.testing.assert_allclose(r["alpha"], ref["alpha"], rtol=atol_, atol=atol_ * np.abs(ref["alpha"]).max())
         assert abs(float(r["bias"]) - float(ref["bias"])) <= atol_ * max(1.0, abs(float(ref["bias"])))
     # replicated CG: identical bits on every rank

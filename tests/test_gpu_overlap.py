@@ -45,6 +45,7 @@ def test_overlap_check_sees_an_ablated_kernel():
                          env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     res = json.loads(out.stdout.strip().splitlines()[-1])
-    assert res["err"] > 100 * res["tol"], res
+    # O_i is a signed sum (~2 % of sum |terms| here): the ablation's ~28 % per-term error shows as ~6e-3
+    assert res["err"] > 10 * res["tol"], res
     err, tol, _ = check("csr_rbf_1m", 200_000, np.float32)  # and the real kernel passes on the same data
     assert err <= tol
