@@ -70,6 +70,18 @@ extern "C" {
 /* RBF pair evaluation on sparse data: 0 = auto (factored e_i e_j (exp(2 g s) - 1) when g * max |x|^2
  * keeps it in floating-point range), 1 = always direct exp(-g |x_i - x_j|^2) - e_i e_j. */
 #define PLSSVM_MI_OPT_RBF_FORM 3
+/* K·p algorithm of the pairwise kernels (poly, rbf) on sparse data:
+ *   0 = auto: the kernel expansion when it represents the kernel to rounding (poly degree <= 16; rbf
+ *       in the factored form with a Taylor degree <= 16 for the data's max |2 g x_if x_jf|), else the
+ *       Gram pattern;
+ *   1 = Gram pattern: every overlapping pair (j < i) with s_ij = x_i . x_j stored at setup, the kernel
+ *       function re-evaluated on each per K·p (O(sum_f c_f^2) memory and traffic);
+ *   2 = kernel expansion: per-feature column moments + the stored remainder of the pairs sharing two or
+ *       more features (O(nnz + #multi-feature pairs)); fails with ERR_UNSUPPORTED when not eligible. */
+#define PLSSVM_MI_OPT_SPARSE_ALGO 4
+#define PLSSVM_MI_SPARSE_AUTO 0
+#define PLSSVM_MI_SPARSE_PATTERN 1
+#define PLSSVM_MI_SPARSE_EXPANSION 2
 
 typedef struct plssvm_mi_ctx plssvm_mi_ctx;
 
@@ -217,7 +229,10 @@ typedef struct {
     int64_t spmv_bytes; /* sparse factored linear: HBM bytes both SpMV passes move per K·p (padded SELL
                            stream, slot maps, panel partials) */
     int rbf_small_args; /* sparse factored rbf: 1 = every 2 g |s_ij| is below the short Taylor form's bound */
-    int reserved_;
+    int sparse_algo;    /* sparse poly/rbf: PLSSVM_MI_SPARSE_PATTERN | PLSSVM_MI_SPARSE_EXPANSION (0 otherwise) */
+    int exp_terms;      /* kernel expansion: polynomial degree K of the per-feature pair function */
+    int exp_waves;      /* kernel expansion: waves of the remainder stream */
+    int64_t exp_chunks; /* kernel expansion: 8-slot chunks of the remainder stream (this rank's rows) */
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
 

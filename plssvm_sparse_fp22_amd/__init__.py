@@ -137,7 +137,7 @@ class CSVM:
     """One MI355X context (one GPU, one HIP stream). ``world_size > 1`` joins a row-block group."""
 
     def __init__(self, params: Parameter, device=0, rank=0, world_size=1, uid=None, kp_mode="auto",
-                 sim_rank=None, rbf_form=0, exchange=None):
+                 sim_rank=None, rbf_form=0, exchange=None, sparse_algo="auto"):
         if params.data is None and params.csr is None and params.coo is None:
             raise ValueError("No data points provided!")
         if params.data is not None:
@@ -159,6 +159,9 @@ class CSVM:
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_KP_MODE, mode))
         if rbf_form:  # 1 = direct RBF pair form on sparse data, see PLSSVM_MI_OPT_RBF_FORM
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_RBF_FORM, rbf_form))
+        algo = {"auto": _abi.SPARSE_AUTO, "pattern": _abi.SPARSE_PATTERN, "expansion": _abi.SPARSE_EXPANSION}[sparse_algo]
+        if algo != _abi.SPARSE_AUTO:  # sparse poly/rbf K·p algorithm, see PLSSVM_MI_OPT_SPARSE_ALGO
+            self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_SPARSE_ALGO, algo))
         if sim_rank is not None:  # (rank, world): single-GPU test hook, see PLSSVM_MI_OPT_SIM_RANK
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_SIM_RANK, sim_rank[0] | (sim_rank[1] << 16)))
         if exchange is not None:  # host-staged group: fn(numpy buffer, op) combines in place (torch_exchange)

@@ -33,6 +33,8 @@ EXPORTS = (
 )
 OPT_SIM_RANK = 2
 OPT_RBF_FORM = 3
+OPT_SPARSE_ALGO = 4
+SPARSE_AUTO, SPARSE_PATTERN, SPARSE_EXPANSION = 0, 1, 2
 PART_KERNEL, PART_OVERLAP = 0, 1
 XCHG_ALLREDUCE, XCHG_ALLGATHER = 0, 1
 # int fn(void *buf, int64_t count, int real_bytes, int op, void *user)   (plssvm_mi_exchange_fn)
@@ -45,7 +47,8 @@ class Info(ctypes.Structure):
                                               "tile_rows", "tile_cols", "device_bytes", "pairs")] + \
                [(k, ctypes.c_int) for k in ("kp_mode", "rank", "world_size", "real_bytes", "kernel", "is_sparse",
                                             "val_fmt", "rbf_factored")] + [("pair_slots", ctypes.c_int64), ("spmv_bytes", ctypes.c_int64)] + \
-               [("rbf_small_args", ctypes.c_int), ("reserved_", ctypes.c_int)]
+               [("rbf_small_args", ctypes.c_int), ("sparse_algo", ctypes.c_int), ("exp_terms", ctypes.c_int),
+                ("exp_waves", ctypes.c_int), ("exp_chunks", ctypes.c_int64)]
 
 
 class BackendError(RuntimeError):

@@ -31,6 +31,7 @@ struct engine : engine_base {
     hipStream_t stream = nullptr;
     int kp_mode = 0;  // PLSSVM_MI_KP_*
     int rbf_form = 0;  // PLSSVM_MI_OPT_RBF_FORM
+    int sparse_algo = 0;  // PLSSVM_MI_OPT_SPARSE_ALGO (0 auto, 1 Gram pattern, 2 kernel expansion)
 
     // ---- multi-GPU row-block group ----
     int rank = 0, world = 1;
@@ -99,6 +100,10 @@ struct engine : engine_base {
     // sparse paths (sparse.hip)
     void sparse_q();                                              // q, norms, e on CSR data
     void build_gram_blocks(const int64_t *cpos, int64_t max_inc);  // sparse Gram pattern (pairwise kernels)
+    bool expansion_eligible();                                    // expand.hip: K, coefficients; true if usable
+    void build_expansion(const int64_t *cpos, int64_t max_inc);   // multi-overlap remainder H, diagonal
+    void expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);
+    void expansion_dominant(const T *p, const cg_scalars<T> *status);
     // raw[i] = sum_j k_ij p_j, i < m (with_base = false: only the overlap terms, PLSSVM_MI_PART_OVERLAP)
     void sparse_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base = true);
     void sparse_dominant(const T *p, const cg_scalars<T> *status);  // the dominant sparse kernel

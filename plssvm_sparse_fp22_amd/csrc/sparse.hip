@@ -693,13 +693,19 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     // values in CSC order, decoded (FP22 input included: the Gram build multiplies them once at setup,
     // the K·p stream holds the products s_ij, so FP22 changes only the input format)
     std::vector<T> cval_real(std::max<int64_t>(nnz, 1));
+    double amax = 0.0, nmax = 0.0;  // max x^2 and max |x_i|^2 (kernel expansion eligibility)
     for (int64_t i = 0; i < m; ++i) {
+        double nrm = 0.0;
         for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
             const int64_t t = fill[col[k]]++;
             crow[t] = (int32_t) i;
             cpos[k] = t;
             cval_real[t] = hval(k);
+            const double x = (double) cval_real[t];
+            amax = std::max(amax, x * x);
+            nrm += x * x;
         }
+        nmax = std::max(nmax, nrm);
     }
     csr.colptr.alloc(d + 1, stream);
     MI_HIP_CHECK(hipMemcpyAsync(csr.colptr.get(), colptr.data(), sizeof(int64_t) * (size_t) (d + 1),
@@ -741,7 +747,18 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                                         stream));
         int64_t max_inc = 0;
         for (int64_t I = csr.rb0; I < csr.rb1; ++I) max_inc = std::max(max_inc, inc_rb[I]);
-        build_gram_blocks(cpos_d.get(), max_inc);
+        // kernel expansion (expand.hip) when it represents the kernel to rounding, else the Gram pattern
+        csr.ex.umax = 2.0 * std::fabs((double) gamma) * amax;
+        const bool fact_ok = kernel != 2 || std::fabs((double) gamma) * nmax <= (sizeof(T) == 8 ? 300.0 : 40.0);
+        const bool elig = fact_ok && expansion_eligible();
+        if (sparse_algo == 2 && !elig)
+            throw mi_error(-5, "the kernel expansion cannot represent this kernel on this data (Taylor degree > 16 or "
+                               "the factored rbf form out of range): use the Gram pattern");
+        if (elig && sparse_algo != 1) {
+            build_expansion(cpos_d.get(), max_inc);
+        } else {
+            build_gram_blocks(cpos_d.get(), max_inc);
+        }
     }
 }
 
@@ -933,6 +950,10 @@ void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status, bool with
         allgather_rows(raw.get());
         return;
     }
+    if (csr.ex.on) {
+        expansion_kp_raw(p, status, with_base);
+        return;
+    }
     // separable sum: sum(e p) (rbf) or sum(p) (poly)
     launch_dot2<T>(p, kernel == 2 ? csr.e.get() : nullptr, nullptr, nullptr, m, red.get(), status, stream);
     launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
@@ -958,6 +979,10 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
     if (factored()) {  // both SpMV passes (the factored K·p without its collectives)
         spmv_pass_csc(p, status);
         spmv_pass_csr(status);
+        return;
+    }
+    if (csr.ex.on) {  // timing: the moments + remainder stream (p stands in for w)
+        expansion_dominant(p, status);
         return;
     }
     if (csr.ncells == 0) return;

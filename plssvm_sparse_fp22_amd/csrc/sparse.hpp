@@ -27,6 +27,36 @@ struct gram_cell {
     double smax;     // max |s_ij| over the cell's pairs (fixed-point bound of the K·p accumulators)
 };
 
+// ---- kernel expansion path (sparse poly / rbf), see DESIGN.md §5 and expand.hip ----------------------
+// sum_j k_ij p_j = base_i + scale_i * sum_j [ sum_{f shared by i, j} phi(x_if x_jf) + H_ij ] w_j
+// with phi a polynomial of degree K (exact for poly, Taylor for the factored rbf), evaluated per
+// feature through the column moments M_k(f) = sum_{j in col f} x_jf^k w_j, and H_ij the remainder of
+// the pairs sharing two or more features (stored, symmetric, rows padded to 8 slots).
+constexpr int EXP_KMAX = 16;
+
+template <typename T>
+struct exp_data {
+    bool on = false;
+    int K = 0, KM = 4;                // polynomial degree of phi; template width of the moments (4, 8, 16)
+    double coef[EXP_KMAX + 1] = {};   // phi(a) = sum_{k=1..K} coef[k] a^k
+    double umax = 0.0;                // rbf: 2 |g| max x^2 (Taylor bound)
+    dev_buf<double> M;                // [d][KM]: coef[k] * M_k(f)
+    dev_buf<T> hdiag;                 // [n_pad]: H_ii
+    dev_buf<T> phin;                  // [n_pad]: phi(|x_i|^2) (the diagonal's pair part, for the overlap hook)
+    dev_buf<T> wv;                    // [n_pad]: w = e p (rbf)
+    dev_buf<T> hs;                    // [n_pad]: sum_j H_ij w_j
+    int64_t pairs = 0;                // unordered pairs sharing >= 2 features with H != 0 (this rank's rows)
+    int64_t slots = 0, nchunks = 0, nwaves = 0;
+    dev_buf<int32_t> hj;              // [slots] partner j (pads: j = i, H = 0)
+    dev_buf<T> hv;                    // [slots] H_ij
+    dev_buf<int32_t> hcrow;           // [nchunks] row of each 8-slot chunk
+    dev_buf<int64_t> wave_chunk;      // [nwaves + 1] chunk range of each wave (row-aligned)
+    int64_t bytes() const {
+        return M.bytes() + hdiag.bytes() + phin.bytes() + wv.bytes() + hs.bytes() + hj.bytes() + hv.bytes() + hcrow.bytes() +
+               wave_chunk.bytes();
+    }
+};
+
 template <typename T>
 struct csr_data {
     int64_t nnz = 0;  // entries of rows 0..m-1
@@ -59,12 +89,14 @@ struct csr_data {
     dev_buf<T> slab_col;  // [nRB][m_pad]
     dev_buf<T> ssc;       // device scalars: [0] = sum(e p) or sum(p)
 
+    exp_data<T> ex;       // kernel expansion path (instead of the Gram pattern)
+
     vals_t<T> rvals() const { return vals_t<T>{ val.get(), nullptr }; }
     vals_t<T> cvals() const { return vals_t<T>{ cval.get(), nullptr }; }
     int64_t bytes() const {
         return rowptr.bytes() + col.bytes() + val.bytes() + colptr.bytes() + crow.bytes() +
                cval.bytes() + spmv_csc.bytes() + spmv_csr.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
-               rb_base.bytes() + rowoff.bytes() + cells.bytes() + slab_row.bytes() + slab_col.bytes();
+               rb_base.bytes() + rowoff.bytes() + cells.bytes() + slab_row.bytes() + slab_col.bytes() + ex.bytes();
     }
 };
 

@@ -16,7 +16,8 @@ pytestmark = pytest.mark.gpu
 TOL = {np.float64: 1e-12, np.float32: 1e-4}
 
 
-def sparse_svm(csr, kernel, dtype, fp22=False, mode="auto", sim=None, gamma=None, coef0=1.0, y=None, cost=1.0):
+def sparse_svm(csr, kernel, dtype, fp22=False, mode="auto", sim=None, gamma=None, coef0=1.0, y=None, cost=1.0,
+               algo="auto"):
     rbf_form = 0
     if mode == "direct":  # rbf pairs as exp(-g |x_i - x_j|^2) - e_i e_j instead of the factored form
         mode, rbf_form = "auto", 1
@@ -30,7 +31,7 @@ def sparse_svm(csr, kernel, dtype, fp22=False, mode="auto", sim=None, gamma=None
     else:
         p.csr = (rowptr, col, val.astype(dtype), n, d)
     p.labels = y
-    return pm.CSVM(p, kp_mode=mode, sim_rank=sim, rbf_form=rbf_form)
+    return pm.CSVM(p, kp_mode=mode, sim_rank=sim, rbf_form=rbf_form, sparse_algo=algo)
 
 
 def oracle_data(oracle, csr, dtype, fp22=False):
@@ -40,8 +41,8 @@ def oracle_data(oracle, csr, dtype, fp22=False):
     return oracle.Data(rowptr=rowptr, col=col, val=val.astype(dtype), n=n, d=d, dtype=dtype)
 
 
-def check_sparse_kp(oracle, csr, kernel, dtype, fp22=False, mode="auto", coef0=1.0, gamma=None):
-    svm = sparse_svm(csr, kernel, dtype, fp22=fp22, mode=mode, coef0=coef0, gamma=gamma)
+def check_sparse_kp(oracle, csr, kernel, dtype, fp22=False, mode="auto", coef0=1.0, gamma=None, algo="auto"):
+    svm = sparse_svm(csr, kernel, dtype, fp22=fp22, mode=mode, coef0=coef0, gamma=gamma, algo=algo)
     svm.setup_data_on_device()
     q = svm.generate_q()
     data = oracle_data(oracle, csr, dtype, fp22)
@@ -55,22 +56,39 @@ def check_sparse_kp(oracle, csr, kernel, dtype, fp22=False, mode="auto", coef0=1
         svm.run_device_kernel(None, ret, x, add)
         want = oracle.kp(kernel, data, q_ref, svm.QA_cost, dtype(1.0), add, x, gamma=g, coef0=dtype(coef0))
         np.testing.assert_allclose(ret, want, rtol=0, atol=TOL[dtype] * np.abs(want).max(),
-                                   err_msg=f"{kernel} {np.dtype(dtype).name} fp22={fp22} mode={mode}")
+                                   err_msg=f"{kernel} {np.dtype(dtype).name} fp22={fp22} mode={mode} algo={algo}")
     info = svm.info()
     svm.close()
     return info
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-@pytest.mark.parametrize("kernel,mode", [("linear", "auto"), ("linear", "pairwise"), ("polynomial", "auto"),
-                                         ("rbf", "auto"), ("rbf", "direct")])
+@pytest.mark.parametrize("kernel,mode,algo", [("linear", "auto", "auto"), ("linear", "pairwise", "auto"),
+                                              ("polynomial", "auto", "auto"), ("polynomial", "auto", "pattern"),
+                                              ("rbf", "auto", "auto"), ("rbf", "auto", "pattern"),
+                                              ("rbf", "direct", "auto")])
 @pytest.mark.parametrize("shape", [(300, 500, 10), (2500, 3000, 20), (9000, 20000, 15)])
-def test_sparse_kp(oracle, kernel, mode, dtype, shape):
+def test_sparse_kp(oracle, kernel, mode, algo, dtype, shape):
     n, d, k = shape
     csr, _ = datagen.sparse_csr(n, d, k, seed=n + d, dtype=dtype)
-    info = check_sparse_kp(oracle, csr, kernel, dtype, mode=mode)
+    info = check_sparse_kp(oracle, csr, kernel, dtype, mode=mode, algo=algo)
     assert info["is_sparse"] == 1
     assert info["rbf_factored"] == (kernel == "rbf" and mode == "auto")
+    if kernel != "linear":  # auto picks the kernel expansion on these sets (small 2 g x^2, degree 3)
+        want = pm._abi.SPARSE_PATTERN if (algo == "pattern" or mode == "direct") else pm._abi.SPARSE_EXPANSION
+        assert info["sparse_algo"] == want
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("kernel,gamma,coef0", [("rbf", 0.5, 0.0), ("rbf", 3.0, 0.0), ("polynomial", 0.3, 1.5),
+                                                ("polynomial", 0.05, -0.7)])
+def test_sparse_expansion_large_arguments(oracle, kernel, gamma, coef0, dtype):
+    """Larger 2 g x^2 (Taylor degree up to 16) and poly with coef0 != 0 (all binomial terms), dense-ish
+    rows so that many pairs share several features (the stored remainder H carries real weight)."""
+    csr, _ = datagen.sparse_csr(1500, 60, 12, seed=17, dtype=dtype)
+    info = check_sparse_kp(oracle, csr, kernel, dtype, gamma=gamma, coef0=coef0)
+    if info["sparse_algo"] == pm._abi.SPARSE_EXPANSION:
+        assert info["pairs"] > 0 and info["exp_terms"] >= 1
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
