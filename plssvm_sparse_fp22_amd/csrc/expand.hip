@@ -456,6 +456,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
     auto &ex = csr.ex;
     const phi_fn phi = make_phi<T>(kernel, degree, gamma, coef0);
     ex.M.alloc(std::max<int64_t>(d, 1) * ex.KM, stream);
+    csr.ssc.alloc(2, stream);  // device scalar S = sum_j w_j
     ex.hdiag.alloc(n_pad, stream);
     ex.hs.alloc(n_pad, stream);
     ex.wv.alloc(kernel == 2 ? n_pad : 1, stream);
@@ -618,13 +619,16 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         MI_LAUNCH_CHECK();
     }
     {
-        size_t tb = 0;
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt8.get(), off8.get(), (int) (R + 1), stream));
+        size_t ta = 0, tb = 0, tc = 0;  // each scan queries its own temporary size (types differ)
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ta, cnt8.get(), off8.get(), (int) (R + 1), stream));
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, clo.get(), lo_start.get(), (int) R, stream));
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tc, cup.get(), up_start.get(), (int) R, stream));
         dev_buf<unsigned char> t;
-        t.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, cnt8.get(), off8.get(), (int) (R + 1), stream));
+        t.alloc((int64_t) std::max({ ta, tb, tc, (size_t) 16 }), stream, false);
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), ta, cnt8.get(), off8.get(), (int) (R + 1), stream));
         MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, clo.get(), lo_start.get(), (int) R, stream));
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, cup.get(), up_start.get(), (int) R, stream));
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tc, cup.get(), up_start.get(), (int) R, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
     }
     ex.pairs = 0;
     {
@@ -711,12 +715,24 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
     ex.on = true;
 }
 
+// timing/test-only ablations (results are wrong when non-zero): PLSSVM_MI_EXP_ABLATE bit 0 = drop the
+// stored remainder H of the multi-feature pairs, bit 1 = keep only the first term of phi's polynomial
+int exp_ablate() {
+    static const int v = [] {
+        const char *s = std::getenv("PLSSVM_MI_EXP_ABLATE");
+        return s ? std::atoi(s) : 0;
+    }();
+    return v;
+}
+
 template <typename T>
 void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
     auto &ex = csr.ex;
     if (d > 0) {
         coefs cf;
         std::memcpy(cf.c, ex.coef, sizeof(cf.c));
+        if (exp_ablate() & 2)
+            for (int k = 2; k <= EXP_KMAX; ++k) cf.c[k] = 0.0;
         auto mom = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned) ceil_div(d, 4)), dim3(256), 0, stream, csr.colptr.get(),
                                csr.crow.get(), csr.cval.get(), w, d, cf, ex.M.get(), status);
@@ -727,7 +743,7 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
         MI_LAUNCH_CHECK();
     }
     if (r1 > r0) MI_HIP_CHECK(hipMemsetAsync(ex.hs.get() + r0, 0, sizeof(T) * (size_t) (r1 - r0), stream));
-    if (ex.nwaves > 0) {
+    if (ex.nwaves > 0 && !(exp_ablate() & 1)) {
         hipLaunchKernelGGL(exp_hstream_kernel<T>, dim3((unsigned) ceil_div(ex.nwaves, 4)), dim3(256), 0, stream,
                            ex.wave_chunk.get(), ex.nwaves, ex.hcrow.get(), ex.hj.get(), ex.hv.get(), w, ex.hs.get(),
                            status);

@@ -473,21 +473,6 @@ __global__ __launch_bounds__((gram_wg<T, KERNEL>())) void gram_kp_kernel(const g
     }
 }
 
-// max |v| over an array (bit patterns of non-negative floats order like unsigned integers)
-template <typename T>
-__global__ __launch_bounds__(256) void abs_max_kernel(const T *__restrict__ v, int64_t n,
-                                                      unsigned long long *__restrict__ out) {
-    T a = 0;
-    for (int64_t k = (int64_t) blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t) gridDim.x * 256)
-        a = max(a, fabs(v[k]));
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) a = max(a, __shfl_xor(a, o));
-    if ((threadIdx.x & 63) == 0) {
-        if constexpr (sizeof(T) == 8) atomicMax(out, (unsigned long long) __double_as_longlong(a));
-        else atomicMax(out, (unsigned long long) __float_as_uint(a));
-    }
-}
-
 // per cell: max |s| over its pairs (the fixed-point bound of the K·p kernel)
 template <typename T>
 __global__ __launch_bounds__(256) void gram_cell_smax_kernel(gram_cell *__restrict__ cells,
@@ -575,26 +560,6 @@ void host_check_csr(const int64_t *rowptr, const int32_t *col, int64_t n, int64_
             if (k > rowptr[i] && col[k] <= col[k - 1]) throw mi_error(-1, "CSR columns must be strictly ascending");
         }
     }
-}
-
-template <typename T>
-T abs_max(const T *v, int64_t n, hipStream_t stream) {
-    if (n <= 0) return T(0);
-    dev_buf<unsigned long long> out;
-    out.alloc(1, stream);
-    hipLaunchKernelGGL(abs_max_kernel<T>, dim3((unsigned) std::min<int64_t>(ceil_div(n, 256), 4096)), dim3(256), 0, stream,
-                       v, n, out.get());
-    MI_LAUNCH_CHECK();
-    unsigned long long bits = 0;
-    MI_HIP_CHECK(hipMemcpyAsync(&bits, out.get(), sizeof bits, hipMemcpyDeviceToHost, stream));
-    MI_HIP_CHECK(hipStreamSynchronize(stream));
-    T r;
-    if constexpr (sizeof(T) == 8) std::memcpy(&r, &bits, 8);
-    else {
-        const uint32_t b32 = (uint32_t) bits;
-        std::memcpy(&r, &b32, 4);
-    }
-    return r;
 }
 
 }  // namespace
@@ -901,12 +866,12 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
                            csr.rb_base.get(), csr.rowoff.get(), csr.ps.get(), m);
         MI_LAUNCH_CHECK();
     }
-    // factored rbf when e_i = exp(-g n_i) and exp(2 g s_ij) <= exp(2 g max n) stay in range
+    // factored rbf c_ij = e_i e_j expm1(2 g s_ij): only while 2 g max|s_ij| <= 1. The fixed-point quantum
+    // of the K·p accumulators is set by the cell's bound expm1(2 g smax) max|e p|, which overestimates the
+    // actual terms (|e_i e_j expm1(2 g s)| <= 1) by up to expm1(2 g smax) e_i: above 1 the factored
+    // terms would lose digits to it, and the direct form exp(-g |x_i - x_j|^2) - e_i e_j (bound 1) is used
     csr.rbf_factored = false;
     if (kernel == 2) {
-        const double gmax = std::fabs((double) gamma) * (double) abs_max(norms.get(), m, stream);
-        csr.rbf_factored = rbf_form != 1 && gmax <= (sizeof(T) == 8 ? 300.0 : 40.0);
-        // every pair's 2 g |s_ij| below the small-argument polynomial's bound -> KERNEL 4
         std::vector<gram_cell> hc((size_t) csr.ncells);
         if (csr.ncells)
             MI_HIP_CHECK(hipMemcpyAsync(hc.data(), csr.cells.get(), sizeof(gram_cell) * hc.size(), hipMemcpyDeviceToHost,
@@ -914,7 +879,10 @@ void engine<T>::build_gram_blocks(const int64_t *cpos, int64_t max_inc) {
         MI_HIP_CHECK(hipStreamSynchronize(stream));
         double smax = 0.0;
         for (const auto &c : hc) smax = std::max(smax, c.smax);
-        csr.rbf_small = 2.0 * std::fabs((double) gamma) * smax < expm1_small_bound<T>();
+        const double u = 2.0 * std::fabs((double) gamma) * smax;
+        csr.rbf_factored = rbf_form != 1 && u <= 1.0;
+        // every pair's 2 g |s_ij| below the small-argument polynomial's bound -> KERNEL 4
+        csr.rbf_small = u < expm1_small_bound<T>();
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
     csr.have_gram = true;

@@ -15,8 +15,8 @@ module checks O_i alone, relative to sum_j |c_ij p_j|.
 Reference semantics: every pair's kernel value is part of the result
 (include/plssvm/backends/HIP/svm_kernel.hip.hpp:206-268, src/plssvm/backends/OpenMP/svm_kernel.cpp:21-47).
 
-Run as a script (``python tests/overlap_check.py CONFIG POINTS DTYPE``) it prints one JSON line with
-the max error; tests/test_gpu_overlap.py uses that to show that an ablated kernel fails the check.
+Run as a script (``python tests/overlap_check.py CONFIG POINTS DTYPE [ALGO]``) it prints one JSON line
+with the max error; tests/test_gpu_overlap.py uses that to show that ablated kernels fail the check.
 """
 from __future__ import annotations
 
@@ -98,5 +98,6 @@ def check(config, points=None, dtype=None, kernel=None, rows=256, seed=11, **csv
 
 if __name__ == "__main__":
     cfg, pts, dts = sys.argv[1], int(sys.argv[2]), sys.argv[3]
-    err, tol, info = check(cfg, pts or None, {"f32": np.float32, "f64": np.float64}[dts])
-    print(json.dumps({"err": err, "tol": tol, "pairs": info["pairs"]}), flush=True)
+    algo = sys.argv[4] if len(sys.argv) > 4 else "auto"
+    err, tol, info = check(cfg, pts or None, {"f32": np.float32, "f64": np.float64}[dts], sparse_algo=algo)
+    print(json.dumps({"err": err, "tol": tol, "pairs": info["pairs"], "sparse_algo": info["sparse_algo"]}), flush=True)

@@ -24,28 +24,59 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CASES = [
     ("csr_rbf_1m", None, np.float32, None),     # BASELINE configs[2] with RBF at full size: 1M x 50k
     ("fp22_rbf_2m", 400_000, np.float32, None),  # configs[4] (FP22 input) at N = 400k, same column occupancy
-    ("csr_rbf_1m", 400_000, np.float64, None),   # fp64 at the config-3 occupancy
+    ("csr_rbf_1m", None, np.float64, None),      # fp64 at full size (the kernel expansion fits)
     ("csr_rbf_1m", 400_000, np.float32, "polynomial"),
     ("csr_rbf_1m", 200_000, np.float64, "polynomial"),
 ]
+ALGOS = ["auto", "pattern"]  # auto = the kernel expansion on these sets; pattern = the stored Gram pattern
 
 
-@pytest.mark.parametrize("config,points,dtype,kernel", CASES)
-def test_overlap_sum_full_size(config, points, dtype, kernel):
-    err, tol, info = check(config, points, dtype, kernel)
+def _case_id(c):
+    return f"{c[0]}-{c[1]}-{np.dtype(c[2]).name}-{c[3] or 'cfg'}"
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("config,points,dtype,kernel", CASES, ids=[_case_id(c) for c in CASES])
+def test_overlap_sum_full_size(config, points, dtype, kernel, algo):
+    if algo == "pattern" and dtype == np.float64 and points is None:
+        points = 400_000  # the fp64 pattern of the full set (2.5e10 pairs x 10 B) does not fit one GPU
+    err, tol, info = check(config, points, dtype, kernel, sparse_algo=algo)
     assert info["pairs"] > 0
-    assert err <= tol, (config, points, np.dtype(dtype).name, kernel, err)
+    want = pm_algo(algo)
+    assert info["sparse_algo"] == want
+    print(f"overlap {config} N={points} {np.dtype(dtype).name} {kernel} {algo}: err {err:.3e} (tol {tol:g})")
+    assert err <= tol, (config, points, np.dtype(dtype).name, kernel, algo, err)
 
 
-def test_overlap_check_sees_an_ablated_kernel():
-    """The same check run on the timing-only ablation PLSSVM_MI_GRAM_ABLATE=2 (the pair function
-    replaced by a linear stand-in, no exp) must fail: the test can see the per-pair work."""
-    env = dict(os.environ, PLSSVM_MI_GRAM_ABLATE="2")
-    out = subprocess.run([sys.executable, os.path.join(HERE, "overlap_check.py"), "csr_rbf_1m", "200000", "f32"],
+def pm_algo(algo):
+    import plssvm_sparse_fp22_amd as pm
+
+    return pm._abi.SPARSE_PATTERN if algo == "pattern" else pm._abi.SPARSE_EXPANSION
+
+
+def _ablated(env, dts, algo):
+    env = dict(os.environ, **env)
+    out = subprocess.run([sys.executable, os.path.join(HERE, "overlap_check.py"), "csr_rbf_1m", "200000", dts, algo],
                          env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
-    res = json.loads(out.stdout.strip().splitlines()[-1])
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_overlap_check_sees_an_ablated_pattern_kernel():
+    """The check run on the timing-only ablation PLSSVM_MI_GRAM_ABLATE=2 of the Gram-pattern kernel (the
+    pair function replaced by a linear stand-in, no exp) must fail: the test sees the per-pair work."""
+    res = _ablated({"PLSSVM_MI_GRAM_ABLATE": "2"}, "f32", "pattern")
     # O_i is a signed sum (~2 % of sum |terms| here): the ablation's ~28 % per-term error shows as ~6e-3
     assert res["err"] > 10 * res["tol"], res
-    err, tol, _ = check("csr_rbf_1m", 200_000, np.float32)  # and the real kernel passes on the same data
+    err, tol, _ = check("csr_rbf_1m", 200_000, np.float32, sparse_algo="pattern")  # the real kernel passes
     assert err <= tol
+
+
+@pytest.mark.parametrize("ablate", ["1", "2"])
+def test_overlap_check_sees_an_ablated_expansion(ablate):
+    """Kernel expansion ablations (PLSSVM_MI_EXP_ABLATE): 1 drops the stored remainder of the pairs that
+    share two or more features, 2 keeps only the first Taylor term. Both are ~1e-6 of the overlap scale
+    at this occupancy (below the fp32 bar), so the fp64 check (1e-12) must see them."""
+    res = _ablated({"PLSSVM_MI_EXP_ABLATE": ablate}, "f64", "auto")
+    assert res["sparse_algo"] == pm_algo("auto")
+    assert res["err"] > 10 * res["tol"], res
