@@ -9,6 +9,7 @@
 
 using plssvm_mi::engine;
 using plssvm_mi::mi_error;
+constexpr int EXP_NWV_C = plssvm_mi::EXP_NWV;
 
 struct plssvm_mi_ctx {
     int real_bytes = 8;
@@ -371,7 +372,7 @@ int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
         info->rbf_small_args = e.csr.rbf_small ? 1 : 0;
         info->sparse_algo = e.csr.ex.on ? PLSSVM_MI_SPARSE_EXPANSION : (e.csr.have_gram ? PLSSVM_MI_SPARSE_PATTERN : 0);
         info->exp_terms = e.csr.ex.on ? e.csr.ex.K : 0;
-        info->exp_waves = (int) e.csr.ex.nwaves;
+        info->exp_waves = (int) (e.csr.ex.nblk * EXP_NWV_C);
         info->exp_chunks = e.csr.ex.nchunks;
     });
 }

@@ -32,6 +32,9 @@ namespace plssvm_mi {
 
 namespace {
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
 // phi in double: the exact per-pair function (rbf: expm1(2 g a); poly: sum_k bin_k a^k, no cancellation)
 struct phi_fn {
     int rbf = 0, deg = 0;
@@ -271,80 +274,172 @@ __global__ __launch_bounds__(256) void exp_moments_kernel(const int64_t *__restr
     }
 }
 
-// hs[i] = sum_j H_ij w_j over the stored remainder rows: each wave owns a row-aligned chunk range;
-// lanes take 8-slot chunks (64 per step, coalesced), gather w_j, and the rows' partial sums are
-// combined by a segmented shuffle reduction, the last row of a step carried into the next. Fixed
-// order, no atomics.
+// ---- remainder stream layout (built from the padded symmetric rows) ---------------------------------------
+// count index of (row r, window W): ((I NWV + v) nW + W) RPW + rr,  r = I RB + v RPW + rr
 template <typename T>
-__global__ __launch_bounds__(256) void exp_hstream_kernel(const int64_t *__restrict__ wave_chunk, int64_t nwaves,
-                                                          const int32_t *__restrict__ hcrow,
-                                                          const int32_t *__restrict__ hj, const T *__restrict__ hv,
-                                                          const T *__restrict__ w, T *__restrict__ hs,
-                                                          const cg_scalars<T> *__restrict__ status) {
-    if (status != nullptr && status->converged) return;
-    const int lane = threadIdx.x & 63;
-    const int64_t gw = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (gw >= nwaves) return;
-    const int64_t c0 = wave_chunk[gw], c1 = wave_chunk[gw + 1];
-    T carry = 0;
-    int carry_row = -1;
-    for (int64_t cb = c0; cb < c1; cb += 64) {  // wave-uniform trip count
-        const int64_t c = cb + lane;
-        const bool have = c < c1;
-        int rl = -1;
-        T acc = 0;
-        if (have) {
-            rl = hcrow[c];
-            const int4 ja = *reinterpret_cast<const int4 *>(hj + 8 * c);
-            const int4 jb = *reinterpret_cast<const int4 *>(hj + 8 * c + 4);
-            T h[8];
-            if constexpr (sizeof(T) == 4) {
-                const float4 a = *reinterpret_cast<const float4 *>(hv + 8 * c), b = *reinterpret_cast<const float4 *>(hv + 8 * c + 4);
-                h[0] = a.x, h[1] = a.y, h[2] = a.z, h[3] = a.w, h[4] = b.x, h[5] = b.y, h[6] = b.z, h[7] = b.w;
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const double2 v = *reinterpret_cast<const double2 *>(hv + 8 * c + 2 * q);
-                    h[2 * q] = v.x, h[2 * q + 1] = v.y;
-                }
-            }
-            const int js[8] = { ja.x, ja.y, ja.z, ja.w, jb.x, jb.y, jb.z, jb.w };
-            T wj[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) wj[k] = w[js[k]];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc = fma(h[k], wj[k], acc);
+__device__ __forceinline__ int64_t exp_cidx(int64_t r, int64_t W, int64_t nW) {
+    constexpr int64_t RB = exp_rb<T>(), RPW = RB / EXP_NWV;
+    const int64_t I = r / RB, v = (r % RB) / RPW, rr = r % RPW;
+    return ((I * EXP_NWV + v) * nW + W) * RPW + rr;
+}
+
+// per row r (rank-local), window W: count of its non-zero entries with j in W, rounded up to 4 slots
+template <typename T>
+__global__ __launch_bounds__(256) void exp_cell_count_kernel(const int64_t *__restrict__ off8,
+                                                             const int32_t *__restrict__ sj, const T *__restrict__ sv,
+                                                             int64_t R, int64_t nW, int64_t *__restrict__ cnt) {
+    constexpr int64_t CW = exp_cw<T>();
+    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    int64_t Wc = -1, k = 0;
+    for (int64_t s = off8[r]; s < off8[r + 1]; ++s) {  // entries sorted by j
+        if (sv[s] == T(0)) continue;                    // pads (and no stored H is exactly 0)
+        const int64_t W = sj[s] / CW;
+        if (W != Wc) {
+            if (Wc >= 0) cnt[exp_cidx<T>(r, Wc, nW)] = (k + 3) & ~int64_t(3);
+            Wc = W;
+            k = 0;
         }
-        // segmented suffix sums: rows are non-decreasing in lane order
-        T sacc = acc;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const T so = __shfl_down(sacc, off);
-            const int rr = __shfl_down(rl, off);
-            if (lane + off < 64 && rr == rl) sacc += so;
-        }
-        const int rprev = __shfl_up(rl, 1);
-        const bool head = rl >= 0 && (lane == 0 || rprev != rl);
-        const int row0 = __shfl(rl, 0);
-        if (carry_row >= 0 && row0 != carry_row) {  // the carried row ended at the step boundary
-            if (lane == 0) hs[carry_row] = carry;
-            carry_row = -1;
-        }
-        if (lane == 0 && carry_row >= 0) sacc += carry;
-        const bool more = cb + 64 < c1;
-        const int lastlane = more ? 63 : (int) (c1 - 1 - cb);
-        const int rowL = __shfl(rl, lastlane);
-        const unsigned long long mk = __ballot(rl == rowL);
-        const int hl = __ffsll((long long) mk) - 1;
-        const T segL = __shfl(sacc, hl);
-        if (head && !(more && rl == rowL)) hs[rl] = sacc;
-        if (more) {
-            carry = segL;
-            carry_row = rowL;
-        } else {
-            carry_row = -1;
-        }
+        ++k;
     }
+    if (Wc >= 0) cnt[exp_cidx<T>(r, Wc, nW)] = (k + 3) & ~int64_t(3);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__restrict__ off8,
+                                                               const int32_t *__restrict__ sj, const T *__restrict__ sv,
+                                                               int64_t R, int64_t nW, const int64_t *__restrict__ coff,
+                                                               uint16_t *__restrict__ hjl, T *__restrict__ hv,
+                                                               uint16_t *__restrict__ hrow) {
+    constexpr int64_t CW = exp_cw<T>(), RB = exp_rb<T>();
+    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    const uint16_t rl = (uint16_t) (r % RB);
+    int64_t Wc = -1, base = 0, k = 0;
+    auto close = [&]() {
+        for (int64_t q = 0; q < ((k + 3) >> 2); ++q) hrow[(base >> 2) + q] = rl;
+    };
+    for (int64_t s = off8[r]; s < off8[r + 1]; ++s) {
+        const T h = sv[s];
+        if (h == T(0)) continue;
+        const int64_t W = sj[s] / CW;
+        if (W != Wc) {
+            if (Wc >= 0) close();
+            Wc = W;
+            base = coff[exp_cidx<T>(r, W, nW)];
+            k = 0;
+        }
+        hjl[base + k] = (uint16_t) (sj[s] - W * CW);
+        hv[base + k] = h;
+        ++k;
+    }
+    if (Wc >= 0) close();
+}
+
+// first chunk of (block I, wave v, window W), W = 0..nW (W = nW: the end of the wave's stream)
+template <typename T>
+__global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__restrict__ coff, int64_t nbv, int64_t nW,
+                                                            int64_t *__restrict__ woff) {
+    constexpr int64_t RPW = exp_rb<T>() / EXP_NWV;
+    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nbv * (nW + 1)) return;
+    const int64_t bv = t / (nW + 1), W = t % (nW + 1);
+    woff[t] = coff[(bv * nW + W) * RPW] >> 2;
+}
+
+// hs[i] = sum_j H_ij w_j. One 1024-thread workgroup per block of exp_rb rows walks the windows of
+// partners: the window of w (exp_cw values) is staged in LDS (double-buffered: the next window is loaded
+// into registers while the current one is used), each wave streams its rows' 4-slot chunks (one
+// contiguous range across all windows, coalesced, nontemporal so the stream does not evict w from L2,
+// software-pipelined one step ahead, also across window boundaries), gathers w_j from LDS and adds its
+// rows' partial sums (segmented shuffle reduction) into an LDS row accumulator only it writes.
+// Fixed order, no atomics: bitwise reproducible.
+template <typename T>
+__global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *__restrict__ woff,
+                                                                 const uint16_t *__restrict__ hrow,
+                                                                 const uint16_t *__restrict__ hjl,
+                                                                 const T *__restrict__ hv, const T *__restrict__ w,
+                                                                 int64_t m, int64_t r0, int64_t R, int64_t nW,
+                                                                 T *__restrict__ hs,
+                                                                 const cg_scalars<T> *__restrict__ status) {
+    constexpr int CW = exp_cw<T>(), RB = exp_rb<T>(), NT = EXP_NWV * 64, PER = CW / NT;
+    __shared__ T wl[2][CW];
+    __shared__ T racc[RB];
+    if (status != nullptr && status->converged) return;
+    const int64_t I = xcd_remap(blockIdx.x, gridDim.x);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int t = tid; t < RB; t += NT) racc[t] = T(0);
+    T reg[PER];
+    auto load_win = [&](int64_t W) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int64_t idx = W * CW + q * NT + tid;
+            reg[q] = idx < m ? w[idx] : T(0);
+        }
+    };
+    auto store_win = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) wl[buf][q * NT + tid] = reg[q];
+    };
+    const int64_t *wo = woff + (I * EXP_NWV + wave) * (nW + 1);
+    const int64_t s_end = wo[nW];
+    // one step of the stream in registers: chunk cp (= step start + lane), loads clamped to the stream
+    int rl_n = 0;
+    u32x2 jj_n = { 0u, 0u };
+    T h_n[4] = { T(0), T(0), T(0), T(0) };
+    auto fetch = [&](int64_t c) {
+        if (s_end == wo[0]) return;  // empty stream (wave-uniform)
+        const int64_t cl = c < s_end ? c : s_end - 1;
+        rl_n = (int) __builtin_nontemporal_load(hrow + cl);
+        jj_n = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hjl + 4 * cl));
+        if constexpr (sizeof(T) == 4) {
+            const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(hv + 4 * cl));
+            h_n[0] = v.x, h_n[1] = v.y, h_n[2] = v.z, h_n[3] = v.w;
+        } else {
+            const f64x2 v0 = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(hv + 4 * cl));
+            const f64x2 v1 = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(hv + 4 * cl + 2));
+            h_n[0] = v0.x, h_n[1] = v0.y, h_n[2] = v1.x, h_n[3] = v1.y;
+        }
+    };
+    load_win(0);
+    store_win(0);
+    fetch(wo[0] + lane);
+    __syncthreads();
+    for (int64_t W = 0; W < nW; ++W) {
+        const int buf = (int) (W & 1);
+        if (W + 1 < nW) load_win(W + 1);  // lands while this window is processed
+        const int64_t c_end = wo[W + 1];
+        const T *wb = wl[buf];
+        for (int64_t cb = wo[W]; cb < c_end; cb += 64) {  // wave-uniform trip count
+            const bool have = cb + lane < c_end;
+            const int rl = have ? rl_n : -1;
+            const u32x2 jj = jj_n;
+            const T h0 = h_n[0], h1 = h_n[1], h2 = h_n[2], h3 = h_n[3];
+            fetch((cb + 64 < c_end ? cb + 64 : c_end) + lane);  // next step (next window's first at c_end)
+            T acc = T(0);
+            if (have) {
+                acc = h0 * wb[jj.x & 0xFFFFu];
+                acc = fma(h1, wb[jj.x >> 16], acc);
+                acc = fma(h2, wb[jj.y & 0xFFFFu], acc);
+                acc = fma(h3, wb[jj.y >> 16], acc);
+            }
+            // segmented suffix sums: rows are non-decreasing in lane order
+            T sacc = acc;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const T so = __shfl_down(sacc, off);
+                const int rr = __shfl_down(rl, off);
+                if (lane + off < 64 && rr == rl) sacc += so;
+            }
+            const int rprev = __shfl_up(rl, 1);
+            if (rl >= 0 && (lane == 0 || rprev != rl)) racc[rl] += sacc;  // rows of this wave only
+        }
+        if (W + 1 < nW) store_win(buf ^ 1);
+        __syncthreads();
+    }
+    const int64_t rb0 = I * RB;
+    const int rows = (int) min<int64_t>(RB, R - rb0);
+    for (int t = tid; t < rows; t += NT) hs[r0 + rb0 + t] = racc[t];
 }
 
 // raw_i for rows [r0, r1) (0 elsewhere): base + scale (J_i + H_ii w_i + hs_i) [- the diagonal term when
@@ -640,22 +735,25 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         MI_HIP_CHECK(hipStreamSynchronize(stream));
         for (int64_t r = 0; r < R; ++r) ex.pairs += (int64_t) hlo[r];
     }
-    std::vector<int64_t> hoff(R + 1, 0);
-    MI_HIP_CHECK(hipMemcpyAsync(hoff.data(), off8.get(), sizeof(int64_t) * (size_t) (R + 1), hipMemcpyDeviceToHost, stream));
+    // padded symmetric rows (temporary): row r's entries in [off8[r], off8[r + 1]), sorted by j
+    int64_t nslot8 = 0;
+    MI_HIP_CHECK(hipMemcpyAsync(&nslot8, off8.get() + R, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
     MI_HIP_CHECK(hipStreamSynchronize(stream));
-    ex.slots = hoff[R];
-    ex.nchunks = ex.slots / 8;
-    ex.hj.alloc(std::max<int64_t>(ex.slots, 8), stream, false);
-    ex.hv.alloc(std::max<int64_t>(ex.slots, 8), stream);
-    ex.hcrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream, false);
+    dev_buf<int32_t> sj;
+    dev_buf<T> sv;
+    dev_buf<int32_t> scrow;
+    sj.alloc(std::max<int64_t>(nslot8, 8), stream, false);
+    sv.alloc(std::max<int64_t>(nslot8, 8), stream);
+    scrow.alloc(std::max<int64_t>(nslot8 / 8, 1), stream, false);
     if (R > 0) {
         hipLaunchKernelGGL(exp_init_rows_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream, off8.get(), R,
-                           r0, ex.hj.get(), ex.hv.get(), ex.hcrow.get());
+                           r0, sj.get(), sv.get(), scrow.get());
         MI_LAUNCH_CHECK();
     }
+    scrow.reset();
     if (P > 0) {
         hipLaunchKernelGGL(exp_place_lower_kernel<T>, dim3((unsigned) ceil_div(P, 256)), dim3(256), 0, stream, Li.get(),
-                           Lj.get(), Lh.get(), P, r0, r1, lo_start.get(), off8.get(), ex.hj.get(), ex.hv.get());
+                           Lj.get(), Lh.get(), P, r0, r1, lo_start.get(), off8.get(), sj.get(), sv.get());
         MI_LAUNCH_CHECK();
         // upper part: entries with j in [r0, r1), stably sorted by j (their li order is kept)
         uidx.alloc(P, stream, false);
@@ -685,28 +783,50 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         if (nup > 0) {
             hipLaunchKernelGGL(exp_place_upper_kernel<T>, dim3((unsigned) ceil_div(nup, 256)), dim3(256), 0, stream,
                                ukey_s.get(), uidx_s.get(), nup, Li.get(), Lh.get(), clo.get(), up_start.get(), off8.get(),
-                               ex.hj.get(), ex.hv.get());
+                               sj.get(), sv.get());
             MI_LAUNCH_CHECK();
         }
     }
-    // waves: row-aligned chunk ranges of about equal size
+    Li.reset(), Lj.reset(), Lh.reset(), uidx.reset(), ukey.reset(), ukey_s.reset(), uidx_s.reset();
+
+    // ---- cells: blocks of EXP_RB rows x windows of CW partners, rows padded to 4 slots per cell ----
+    constexpr int64_t CW = exp_cw<T>(), RB = exp_rb<T>();
+    ex.nW = ceil_div(std::max<int64_t>(m, 1), CW);
+    ex.nblk = ceil_div(R, RB);
+    const int64_t nbv = ex.nblk * EXP_NWV, ncnt = ex.nblk * RB * ex.nW;
     {
-        const int64_t target_waves = std::max<int64_t>(1, std::min<int64_t>(R, 8192));
-        const int64_t per = std::max<int64_t>(1, ceil_div(ex.nchunks, target_waves));
-        std::vector<int64_t> wc{ 0 };
-        int64_t next = per;
-        for (int64_t r = 0; r < R; ++r) {
-            const int64_t ce = hoff[r + 1] / 8;
-            if (ce >= next && ce < ex.nchunks) {
-                wc.push_back(ce);
-                next = ce + per;
-            }
+        dev_buf<int64_t> cnt, coff;
+        cnt.alloc(ncnt + 1, stream);
+        coff.alloc(ncnt + 1, stream, false);
+        if (R > 0) {
+            hipLaunchKernelGGL(exp_cell_count_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                               off8.get(), sj.get(), sv.get(), R, ex.nW, cnt.get());
+            MI_LAUNCH_CHECK();
         }
-        wc.push_back(ex.nchunks);
-        ex.nwaves = (int64_t) wc.size() - 1;
-        ex.wave_chunk.alloc((int64_t) wc.size(), stream);
-        MI_HIP_CHECK(hipMemcpyAsync(ex.wave_chunk.get(), wc.data(), sizeof(int64_t) * wc.size(), hipMemcpyHostToDevice,
-                                    stream));
+        size_t tb = 0;
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.get(), coff.get(), ncnt + 1, stream));
+        dev_buf<unsigned char> t;
+        t.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, cnt.get(), coff.get(), ncnt + 1, stream));
+        MI_HIP_CHECK(hipMemcpyAsync(&ex.slots, coff.get() + ncnt, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        ex.nchunks = ex.slots / 4;
+        ex.hjl.alloc(std::max<int64_t>(ex.slots, 4), stream);
+        ex.hv.alloc(std::max<int64_t>(ex.slots, 4), stream);
+        ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
+        if (R > 0) {
+            hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                               off8.get(), sj.get(), sv.get(), R, ex.nW, coff.get(), ex.hjl.get(), ex.hv.get(),
+                               ex.hrow.get());
+            MI_LAUNCH_CHECK();
+        }
+        ex.woff.alloc(std::max<int64_t>(nbv * (ex.nW + 1), 1), stream);
+        if (nbv > 0) {
+            hipLaunchKernelGGL(exp_cell_woff_kernel<T>, dim3((unsigned) ceil_div(nbv * (ex.nW + 1), 256)), dim3(256), 0,
+                               stream, coff.get(), nbv, ex.nW, ex.woff.get());
+            MI_LAUNCH_CHECK();
+        }
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
     csr.pairs = ex.pairs;
@@ -742,12 +862,12 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
         else mom(exp_moments_kernel<T, 16>);
         MI_LAUNCH_CHECK();
     }
-    if (r1 > r0) MI_HIP_CHECK(hipMemsetAsync(ex.hs.get() + r0, 0, sizeof(T) * (size_t) (r1 - r0), stream));
-    if (ex.nwaves > 0 && !(exp_ablate() & 1)) {
-        hipLaunchKernelGGL(exp_hstream_kernel<T>, dim3((unsigned) ceil_div(ex.nwaves, 4)), dim3(256), 0, stream,
-                           ex.wave_chunk.get(), ex.nwaves, ex.hcrow.get(), ex.hj.get(), ex.hv.get(), w, ex.hs.get(),
-                           status);
+    if (ex.nblk > 0 && !(exp_ablate() & 1)) {
+        hipLaunchKernelGGL(exp_hcell_kernel<T>, dim3((unsigned) ex.nblk), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
+                           ex.hrow.get(), ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, ex.hs.get(), status);
         MI_LAUNCH_CHECK();
+    } else if (r1 > r0) {
+        MI_HIP_CHECK(hipMemsetAsync(ex.hs.get() + r0, 0, sizeof(T) * (size_t) (r1 - r0), stream));
     }
 }
 

@@ -33,6 +33,13 @@ struct gram_cell {
 // feature through the column moments M_k(f) = sum_{j in col f} x_jf^k w_j, and H_ij the remainder of
 // the pairs sharing two or more features (stored, symmetric, rows padded to 8 slots).
 constexpr int EXP_KMAX = 16;
+constexpr int EXP_NWV = 16;  // waves per remainder-stream workgroup (one workgroup per CU)
+// rows per remainder-stream block (one workgroup; exp_rb / EXP_NWV rows per wave)
+template <typename T>
+constexpr int exp_rb() { return sizeof(T) == 4 ? 4096 : 2048; }
+// window of partners j staged in LDS (double-buffered: 2 x 64 KiB + the row accumulator = 144 KiB)
+template <typename T>
+constexpr int exp_cw() { return sizeof(T) == 4 ? 16384 : 8192; }
 
 template <typename T>
 struct exp_data {
@@ -46,14 +53,17 @@ struct exp_data {
     dev_buf<T> wv;                    // [n_pad]: w = e p (rbf)
     dev_buf<T> hs;                    // [n_pad]: sum_j H_ij w_j
     int64_t pairs = 0;                // unordered pairs sharing >= 2 features with H != 0 (this rank's rows)
-    int64_t slots = 0, nchunks = 0, nwaves = 0;
-    dev_buf<int32_t> hj;              // [slots] partner j (pads: j = i, H = 0)
+    // remainder stream: per row block I (exp_rb rows), per wave v (its exp_rb / EXP_NWV rows), per
+    // window W of exp_cw partners j, row by row: the row's entries with j in W, padded to a multiple of 4
+    // slots (pads: j = 0, H = 0); each wave's stream is one contiguous range across the windows
+    int64_t slots = 0, nchunks = 0, nblk = 0, nW = 0;
+    dev_buf<uint16_t> hjl;            // [slots] j - W * CW
     dev_buf<T> hv;                    // [slots] H_ij
-    dev_buf<int32_t> hcrow;           // [nchunks] row of each 8-slot chunk
-    dev_buf<int64_t> wave_chunk;      // [nwaves + 1] chunk range of each wave (row-aligned)
+    dev_buf<uint16_t> hrow;           // [nchunks] block-local row of each 4-slot chunk
+    dev_buf<int64_t> woff;            // [nblk][EXP_NWV][nW + 1] first chunk of each (block, wave, window)
     int64_t bytes() const {
-        return M.bytes() + hdiag.bytes() + phin.bytes() + wv.bytes() + hs.bytes() + hj.bytes() + hv.bytes() + hcrow.bytes() +
-               wave_chunk.bytes();
+        return M.bytes() + hdiag.bytes() + phin.bytes() + wv.bytes() + hs.bytes() + hjl.bytes() + hv.bytes() +
+               hrow.bytes() + woff.bytes();
     }
 };
 

@@ -19,7 +19,11 @@ import numpy as np
 
 
 def _lines(path):
-    with open(path, "r") as f:
+    try:
+        f = open(path, "r")
+    except FileNotFoundError:
+        raise FileNotFoundError(f"Couldn't find file: '{path}'!") from None
+    with f:
         for raw in f:
             s = raw.lstrip()
             if not s or s.startswith("#"):
@@ -57,10 +61,10 @@ def parse_libsvm(path, dtype=np.float64, sparse=False):
         rows_v.append(np.asarray(vals, dtype=np.float64)[order])
     n = len(rows_c)
     if n == 0:
-        raise ValueError("Can't parse file: no data points are given!")
+        raise InvalidFileFormat("Can't parse file: no data points are given!")
     d = max((int(c.max()) + 1 for c in rows_c if c.size), default=0)
     if d == 0:
-        raise ValueError("Can't parse file: no data points are given!")
+        raise InvalidFileFormat("Can't parse file: no data points are given!")
     y = None
     if has_label:
         y = np.where(np.asarray(labels) > 0, 1.0, -1.0).astype(dtype)
@@ -76,35 +80,141 @@ def parse_libsvm(path, dtype=np.float64, sparse=False):
     return X, y
 
 
+class InvalidFileFormat(ValueError):
+    """plssvm::invalid_file_format_exception (include/plssvm/exceptions/exceptions.hpp)."""
+
+
+def _type_name(dtype):
+    return "float" if np.dtype(dtype) == np.float32 else "double"
+
+
+def _convert(text, kind):
+    """detail::convert_to (include/plssvm/detail/string_conversion.hpp:39-64): leading whitespace is
+    skipped and the longest valid prefix converted (std::from_chars / fast_float semantics)."""
+    import re
+
+    t = text.lstrip()
+    pat = r"[+-]?(\d+\.?\d*([eE][+-]?\d+)?|\.\d+([eE][+-]?\d+)?|inf|infinity|nan)" if kind not in (
+        "unsigned int", "unsigned long long") else r"\d+"
+    mt = re.match(pat, t, re.IGNORECASE)
+    if mt is None or (kind in ("float", "double") and t.startswith("+")):
+        raise InvalidFileFormat(f"Can't convert '{t}' to a value of type {kind}!")
+    return float(mt.group(0)) if kind in ("float", "double") else int(mt.group(0))
+
+
 def parse_model(path, dtype=np.float64):
-    """LIBSVM model file as written by csvm::write_model (src/plssvm/csvm.cpp:60-204)."""
+    """LIBSVM model file (parameter<T>::parse_model_file, src/plssvm/parameter.cpp:366-520), as written
+    by csvm::write_model (src/plssvm/csvm.cpp:60-204). Same header rules and error messages:
+    lines left-trimmed, '#' comments skipped, header lines lower-cased, the entries svm_type c_svc,
+    kernel_type, gamma, degree, coef0, nr_class 2, total_sv > 0, rho, label 1 -1 (either order),
+    nr_sv a b with a + b == total_sv, then SV and total_sv lines 'alpha idx:val ...'."""
     dtype = np.dtype(dtype)
-    header, svs = {}, []
-    with open(path) as f:
-        lines = [ln.strip() for ln in f if ln.strip() and not ln.lstrip().startswith("#")]
-    k = 0
-    while lines[k] != "SV":
-        key, _, val = lines[k].partition(" ")
-        header[key] = val
-        k += 1
+    tn = _type_name(dtype)
+    try:
+        with open(path) as f:
+            raw = f.read().split("\n")
+    except FileNotFoundError:
+        raise FileNotFoundError(f"Couldn't find file: '{path}'!") from None
+    lines = [ln.lstrip() for ln in raw]
+    lines = [ln for ln in lines if ln and not ln.startswith("#")]
+    header = {}
+    num_sv, labels, rho, nr_sv = 0, (0.0, 0.0), None, None
+    h = 0
+    while h < len(lines):
+        line = lines[h].strip().lower()
+        sp = line.find(" ")
+        value = line[sp + 1:].lstrip() if sp >= 0 else ""
+        if line.startswith("svm_type"):
+            if value != "c_svc":
+                raise InvalidFileFormat(f"Can only use c_svc as svm_type, but '{value}' was given!")
+        elif line.startswith("kernel_type"):
+            tok = value.split()[0] if value.split() else ""
+            k = {"linear": "linear", "0": "linear", "polynomial": "polynomial", "1": "polynomial", "rbf": "rbf",
+                 "2": "rbf"}.get(tok)
+            if k is None:
+                raise InvalidFileFormat(f"Unrecognized kernel type '{value}'!")
+            header["kernel_type"] = k
+        elif line.startswith("gamma"):
+            header["gamma"] = _convert(value, tn)
+        elif line.startswith("degree"):
+            header["degree"] = _convert(value, "int")
+        elif line.startswith("coef0"):
+            header["coef0"] = _convert(value, tn)
+        elif line.startswith("nr_class"):
+            nc = _convert(value, "unsigned int")
+            if nc != 2:
+                raise InvalidFileFormat(f"Can only use 2 classes, but {nc} were given!")
+        elif line.startswith("total_sv"):
+            num_sv = _convert(value, "unsigned long long")
+            if num_sv == 0:
+                raise InvalidFileFormat(f"The number of support vectors must be greater than 0, but is {num_sv}!")
+        elif line.startswith("rho"):
+            rho = _convert(value, tn)
+        elif line.startswith("label"):
+            sp1 = value.find(" ")
+            first = value if sp1 < 0 else value[:sp1]
+            rest = "" if sp1 < 0 else value[sp1 + 1:]
+            sp2 = rest.find(" ")
+            second = rest if sp2 < 0 else rest[:sp2]
+            tail = "" if sp2 < 0 else rest[sp2 + 1:].lstrip()
+            labels = (_convert(first, tn), _convert(second, tn))
+            if tail or labels[0] not in (1.0, -1.0) or labels[1] not in (1.0, -1.0):
+                raise InvalidFileFormat(f"Only the labels 1 and -1 are allowed, but '{line}' were given!")
+        elif line.startswith("nr_sv"):
+            sp1 = value.find(" ")
+            first = value if sp1 < 0 else value[:sp1]
+            rest = "" if sp1 < 0 else value[sp1 + 1:]
+            sp2 = rest.find(" ")
+            second = rest if sp2 < 0 else rest[:sp2]
+            tail = "" if sp2 < 0 else rest[sp2 + 1:].lstrip()
+            a, b = _convert(first, "unsigned long long"), _convert(second, "unsigned long long")
+            if tail:
+                raise InvalidFileFormat(f"Only two numbers are allowed, but more were given '{line}'!")
+            if a + b != num_sv:
+                raise InvalidFileFormat("The number of positive and negative support vectors doesn't add up to the "
+                                        f"total number: {a} + {b} != {num_sv}!")
+            nr_sv = [a, b]
+        elif line == "sv":
+            break
+        else:
+            raise InvalidFileFormat(f"Unrecognized header entry '{lines[h].rstrip()}'! Maybe SV is missing?")
+        h += 1
+    if num_sv == 0:
+        raise InvalidFileFormat("Missing total number of support vectors!")
+    if labels[0] == 0 or labels[1] == 0:
+        raise InvalidFileFormat("Missing labels!")
+    if nr_sv is None:
+        raise InvalidFileFormat("Missing number of support vectors per class!")
+    if rho is None:
+        raise InvalidFileFormat("Missing rho value!")
+    if h + 1 >= len(lines):
+        raise InvalidFileFormat("Can't parse file: no support vectors are given or SV is missing!")
+    sv_lines = lines[h + 1:h + 1 + num_sv]
+    if len(sv_lines) < num_sv:
+        raise InvalidFileFormat(f"total_sv is {num_sv}, but only {len(sv_lines)} support vectors are given!")
     alphas, rows = [], []
-    for ln in lines[k + 1:]:
+    for ln in sv_lines:
         toks = ln.split()
-        alphas.append(float(toks[0]))
-        rows.append({int(t.split(":")[0]): float(t.split(":")[1]) for t in toks[1:]})
-    d = max(max(r) for r in rows if r) + 1
+        alphas.append(_convert(toks[0], tn))
+        r = {}
+        for t in toks[1:]:
+            if ":" not in t:
+                break
+            k, v = t.split(":", 1)
+            r[int(k)] = _convert(v, tn)
+        rows.append(r)
+    d = max((max(r) for r in rows if r), default=-1) + 1
+    if d == 0:
+        raise InvalidFileFormat("Can't parse file: no data points are given!")
     SV = np.zeros((len(rows), d), dtype=dtype)
     for i, r in enumerate(rows):
         for c, v in r.items():
             SV[i, c] = v
-    out = dict(kernel=header["kernel_type"], rho=float(header["rho"]), alpha=np.asarray(alphas, dtype=dtype), SV=SV,
-               nr_sv=[int(t) for t in header["nr_sv"].split()])
-    if "degree" in header:
-        out["degree"] = int(header["degree"])
-    if "gamma" in header:
-        out["gamma"] = float(header["gamma"])
-    if "coef0" in header:
-        out["coef0"] = float(header["coef0"])
+    out = dict(kernel=header.get("kernel_type", "linear"), rho=float(rho), alpha=np.asarray(alphas, dtype=dtype),
+               SV=SV, nr_sv=nr_sv, labels=labels)
+    for key in ("degree", "gamma", "coef0"):
+        if key in header:
+            out[key] = header[key]
     return out
 
 
