@@ -294,6 +294,21 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
     vb = 2.75 if layout == "fp22" else es
     co = float((c * (c + 1) / 2).sum())
     survey = (co * (4 + vb) + col.size * (4 + vb) + 3 * m * es) / world
+    if info.get("sparse_algo") == pm._abi.SPARSE_EXPANSION:
+        # kernel expansion: the dominant launch = column moments (one CSC pass: int32 row +
+        # value per entry, w gathered once per row) + the remainder stream of the multi-feature pairs
+        # (uint16 j + H per slot, uint16 row per 4-slot chunk); bytes the algorithm must move per K·p
+        nnz = info["nnz"]
+        rem = info["pair_slots"] * (2 + es) + info["exp_chunks"] * 2
+        alg = rem + nnz * (4 + es) + m * es
+        return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
+                    frac=alg / s / PEAKS["hbm"], traffic=None, kernel="exp_moments_kernel+exp_hcell_kernel",
+                    launch_ms=ms_dom, alg_bytes=alg,
+                    alg_bytes_def="moments CSC pass nnz x (4 + sizeof(real)) + m x sizeof(real) + remainder stream "
+                                  "slots x (2 + sizeof(real)) + chunks x 2",
+                    remainder_bytes=rem, exp_terms=info["exp_terms"], multi_pairs=info["pairs"],
+                    pair_slots=info["pair_slots"], survey_alg_bytes=survey,
+                    survey_effective_GBps=survey / s / 1e9, survey_effective_frac=survey / s / PEAKS["hbm"])
     # the kernel's algorithmic bytes: the stored pair stream it must read once per K·p (uint16 j + s_ij
     # per slot, rows padded to 8 per cell); SURVEY's column-join figure counts every co-occurrence
     # with multiplicity at 8 B, more than this algorithm needs, so it is reported as an effective rate

@@ -235,43 +235,16 @@ __global__ __launch_bounds__(256) void exp_w_kernel(const T *__restrict__ e, con
     if (i < m) w[i] = e[i] * p[i];
 }
 
-// M[f][k] = coef_{k+1} sum_{j in col f} x_jf^(k+1) w_j: one wave per column, fp64, fixed order
-template <typename T, int KM>
-__global__ __launch_bounds__(256) void exp_moments_kernel(const int64_t *__restrict__ colptr,
-                                                          const int32_t *__restrict__ crow, const T *__restrict__ cval,
-                                                          const T *__restrict__ w, int64_t d, coefs cf,
-                                                          double *__restrict__ M,
-                                                          const cg_scalars<T> *__restrict__ status) {
+// M[f][k] = coef_{k+1} mom[k][f] (the CSR pass gathers the KC channels of a feature together)
+template <typename T>
+__global__ __launch_bounds__(256) void exp_mscale_kernel(const T *__restrict__ mom, int64_t d, int kc, coefs cf,
+                                                         T *__restrict__ M, const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
-    const int64_t f = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (f >= d) return;
-    const int lane = threadIdx.x & 63;
-    double acc[KM];
-#pragma unroll
-    for (int k = 0; k < KM; ++k) acc[k] = 0.0;
-    const int64_t t1 = colptr[f + 1];
-    for (int64_t t = colptr[f] + lane; t < t1; t += 64) {
-        const double x = (double) cval[t];
-        double xp = x * (double) w[crow[t]];
-#pragma unroll
-        for (int k = 0; k < KM; ++k) {
-            acc[k] += xp;
-            xp *= x;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < KM; ++k) {
-        double v = acc[k];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-        acc[k] = v;
-    }
-    if (lane < KM) {
-        double v = acc[0];
-#pragma unroll
-        for (int k = 1; k < KM; ++k) v = lane == k ? acc[k] : v;
-        M[f * KM + lane] = cf.c[lane + 1] * v;
-    }
+    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= d * kc) return;
+    const int64_t f = t / kc;
+    const int k = (int) (t % kc);
+    M[t] = (T) (cf.c[k + 1] * (double) mom[(int64_t) k * d + f]);
 }
 
 // ---- remainder stream layout (built from the padded symmetric rows) ---------------------------------------
@@ -442,51 +415,32 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     for (int t = tid; t < rows; t += NT) hs[r0 + rb0 + t] = racc[t];
 }
 
-// raw_i for rows [r0, r1) (0 elsewhere): base + scale (J_i + H_ii w_i + hs_i) [- the diagonal term when
-// only the overlap part is asked for], 8 lanes per row walking the CSR entries (Horner on the moments)
-template <typename T, int KM>
-__global__ __launch_bounds__(256) void exp_rows_kernel(const int64_t *__restrict__ rowptr,
-                                                       const int32_t *__restrict__ col, const T *__restrict__ val,
-                                                       const double *__restrict__ M, const T *__restrict__ e,
-                                                       const T *__restrict__ w, const T *__restrict__ hdiag,
-                                                       const T *__restrict__ phin, const T *__restrict__ hs,
-                                                       const T *__restrict__ ssc, T kappa, int64_t m, int64_t r0,
-                                                       int64_t r1, int overlap_only, T *__restrict__ raw,
-                                                       const cg_scalars<T> *__restrict__ status) {
+// raw_i for rows [r0, r1) (0 elsewhere), raw holding J_i there (the CSR pass): base + scale (J_i +
+// H_ii w_i + hs_i) [- the diagonal's pair part when only the overlap part is asked for], in fp64
+template <typename T>
+__global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ e, const T *__restrict__ w,
+                                                          const T *__restrict__ hdiag, const T *__restrict__ phin,
+                                                          const T *__restrict__ hs, const T *__restrict__ ssc, T kappa,
+                                                          int64_t m, int64_t r0, int64_t r1, int overlap_only,
+                                                          T *__restrict__ raw, const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
-    const int64_t i = (int64_t) blockIdx.x * 32 + (threadIdx.x >> 3);
-    const int sl = threadIdx.x & 7;
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     if (i < r0 || i >= r1) {
-        if (sl == 0) raw[i] = T(0);
+        raw[i] = T(0);
         return;
     }
-    double J = 0.0;
-    const int64_t k1 = rowptr[i + 1];
-    for (int64_t k = rowptr[i] + sl; k < k1; k += 8) {
-        const double x = (double) val[k];
-        const double *Mf = M + (int64_t) col[k] * KM;
-        double h = Mf[KM - 1];
-#pragma unroll
-        for (int q = KM - 2; q >= 0; --q) h = fma(h, x, Mf[q]);
-        J = fma(h, x, J);
+    const double wi = (double) w[i];
+    const double t = (double) raw[i] + (double) hdiag[i] * wi + (double) hs[i];
+    const double sc = e != nullptr ? (double) e[i] : 1.0;
+    double v;
+    if (overlap_only) {
+        v = sc * (t - (double) phin[i] * wi);
+    } else {
+        const double base = (e != nullptr ? (double) e[i] : (double) kappa) * (double) ssc[0];
+        v = base + sc * t;
     }
-    J += __shfl_xor(J, 4);
-    J += __shfl_xor(J, 2);
-    J += __shfl_xor(J, 1);
-    if (sl == 0) {
-        const double wi = (double) w[i];
-        double t = J + (double) hdiag[i] * wi + (double) hs[i];
-        const double sc = e != nullptr ? (double) e[i] : 1.0;
-        double v;
-        if (overlap_only) {
-            v = sc * (t - (double) phin[i] * wi);
-        } else {
-            const double base = (e != nullptr ? (double) e[i] : (double) kappa) * (double) ssc[0];
-            v = base + sc * t;
-        }
-        raw[i] = (T) v;
-    }
+    raw[i] = (T) v;
 }
 
 template <typename T>
@@ -540,7 +494,7 @@ bool engine<T>::expansion_eligible() {
     } else {
         return false;
     }
-    ex.KM = ex.K <= 4 ? 4 : (ex.K <= 8 ? 8 : 16);
+    ex.KM = ex.K <= 2 ? 2 : (ex.K <= 4 ? 4 : (ex.K <= 8 ? 8 : 16));
     return true;
 }
 
@@ -551,6 +505,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
     auto &ex = csr.ex;
     const phi_fn phi = make_phi<T>(kernel, degree, gamma, coef0);
     ex.M.alloc(std::max<int64_t>(d, 1) * ex.KM, stream);
+    ex.mom.alloc(std::max<int64_t>(d, 1) * ex.KM, stream);
     csr.ssc.alloc(2, stream);  // device scalar S = sum_j w_j
     ex.hdiag.alloc(n_pad, stream);
     ex.hs.alloc(n_pad, stream);
@@ -848,18 +803,14 @@ int exp_ablate() {
 template <typename T>
 void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
     auto &ex = csr.ex;
-    if (d > 0) {
+    if (d > 0) {  // column moments: one SELL pass over the CSC (mode 1), then the coefficients
+        launch_panel_spmv<T>(csr.spmv_csc, w, m, ex.mom.get(), status, stream, ex.KM, 1);
         coefs cf;
         std::memcpy(cf.c, ex.coef, sizeof(cf.c));
         if (exp_ablate() & 2)
             for (int k = 2; k <= EXP_KMAX; ++k) cf.c[k] = 0.0;
-        auto mom = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3((unsigned) ceil_div(d, 4)), dim3(256), 0, stream, csr.colptr.get(),
-                               csr.crow.get(), csr.cval.get(), w, d, cf, ex.M.get(), status);
-        };
-        if (ex.KM == 4) mom(exp_moments_kernel<T, 4>);
-        else if (ex.KM == 8) mom(exp_moments_kernel<T, 8>);
-        else mom(exp_moments_kernel<T, 16>);
+        hipLaunchKernelGGL(exp_mscale_kernel<T>, dim3((unsigned) ceil_div(d * ex.KM, 256)), dim3(256), 0, stream,
+                           ex.mom.get(), d, ex.KM, cf, ex.M.get(), status);
         MI_LAUNCH_CHECK();
     }
     if (ex.nblk > 0 && !(exp_ablate() & 1)) {
@@ -889,15 +840,11 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
         kappa = 1;
         for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
     }
-    auto rows = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3((unsigned) ceil_div(m, 32)), dim3(256), 0, stream, csr.rowptr.get(), csr.col.get(),
-                           csr.val.get(), ex.M.get(), kernel == 2 ? csr.e.get() : nullptr, w, ex.hdiag.get(),
-                           ex.phin.get(), ex.hs.get(), csr.ssc.get(), kappa, m, r0, r1, with_base ? 0 : 1,
-                           raw.get(), status);
-    };
-    if (ex.KM == 4) rows(exp_rows_kernel<T, 4>);
-    else if (ex.KM == 8) rows(exp_rows_kernel<T, 8>);
-    else rows(exp_rows_kernel<T, 16>);
+    // J_i = sum_{f in x_i} sum_k x_if^(k+1) M[f][k]: one SELL pass over this rank's CSR rows (mode 2)
+    if (r1 > r0) launch_panel_spmv<T>(csr.spmv_csr, ex.M.get(), d, raw.get() + r0, status, stream, ex.KM, 2);
+    hipLaunchKernelGGL(exp_combine_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream,
+                       kernel == 2 ? csr.e.get() : nullptr, w, ex.hdiag.get(), ex.phin.get(), ex.hs.get(), csr.ssc.get(),
+                       kappa, m, r0, r1, with_base ? 0 : 1, raw.get(), status);
     MI_LAUNCH_CHECK();
     allgather_rows(raw.get());
 }

@@ -720,6 +720,26 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             throw mi_error(-5, "the kernel expansion cannot represent this kernel on this data (Taylor degree > 16 or "
                                "the factored rbf form out of range): use the Gram pattern");
         if (elig && sparse_algo != 1) {
+            // the two SELL passes of the kernel expansion (the factored linear path's plans, with K channels):
+            // moments over the CSC of all rows, the Horner pass over this rank's CSR rows
+            const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
+            constexpr int64_t blocks = 512;
+            csr.csc_r0 = 0;
+            csr.csc_r1 = m;
+            build_spmv_plan<T>(
+                csr.spmv_csc, d, m, nnz, f22,
+                [&](auto emit) {
+                    for (int64_t i = 0; i < m; ++i)
+                        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit((int64_t) col[k], i, (double) hval(k));
+                },
+                blocks, stream, 0, 1, csr.ex.KM);
+            build_spmv_plan<T>(
+                csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22,
+                [&](auto emit) {
+                    for (int64_t i = r0; i < r1; ++i)
+                        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit(i - r0, (int64_t) col[k], (double) hval(k));
+                },
+                blocks, stream, 0, csr.ex.KM, 1);
             build_expansion(cpos_d.get(), max_inc);
         } else {
             build_gram_blocks(cpos_d.get(), max_inc);

@@ -44,10 +44,11 @@ constexpr int exp_cw() { return sizeof(T) == 4 ? 16384 : 8192; }
 template <typename T>
 struct exp_data {
     bool on = false;
-    int K = 0, KM = 4;                // polynomial degree of phi; template width of the moments (4, 8, 16)
+    int K = 0, KM = 2;                // polynomial degree of phi; moment channels (2, 4, 8, 16 >= K)
     double coef[EXP_KMAX + 1] = {};   // phi(a) = sum_{k=1..K} coef[k] a^k
     double umax = 0.0;                // rbf: 2 |g| max x^2 (Taylor bound)
-    dev_buf<double> M;                // [d][KM]: coef[k] * M_k(f)
+    dev_buf<T> mom;                   // [KM][d]: M_k(f) = sum_{j in col f} x_jf^(k+1) w_j (SELL pass, mode 1)
+    dev_buf<T> M;                     // [d][KM]: coef[k+1] M_k(f), gathered by the CSR pass (mode 2)
     dev_buf<T> hdiag;                 // [n_pad]: H_ii
     dev_buf<T> phin;                  // [n_pad]: phi(|x_i|^2) (the diagonal's pair part, for the overlap hook)
     dev_buf<T> wv;                    // [n_pad]: w = e p (rbf)
@@ -62,7 +63,7 @@ struct exp_data {
     dev_buf<uint16_t> hrow;           // [nchunks] block-local row of each 4-slot chunk
     dev_buf<int64_t> woff;            // [nblk][EXP_NWV][nW + 1] first chunk of each (block, wave, window)
     int64_t bytes() const {
-        return M.bytes() + hdiag.bytes() + phin.bytes() + wv.bytes() + hs.bytes() + hjl.bytes() + hv.bytes() +
+        return mom.bytes() + M.bytes() + hdiag.bytes() + phin.bytes() + wv.bytes() + hs.bytes() + hjl.bytes() + hv.bytes() +
                hrow.bytes() + woff.bytes();
     }
 };

@@ -104,7 +104,12 @@ __device__ __forceinline__ T sell_val(const vals_t<T> &val, int64_t k) {
     }
 }
 
-template <typename T, bool LDSX, bool F22>
+// MODE 0: out[s] = sum_e v_e x[i_e]                                   (plain SpMV, KC = 1)
+// MODE 1: out[k][s] = sum_e v_e^(k+1) x[i_e], k < KC                  (power moments, KC outputs per segment)
+// MODE 2: out[s] = sum_e sum_{k<KC} v_e^(k+1) x[i_e][k]               (KC-channel gathered vector, Horner)
+// (the kernel expansion of the sparse poly / rbf K·p, expand.hip, runs MODE 1 over the CSC and MODE 2
+// over the CSR of the same data as the factored linear path's two MODE 0 passes)
+template <typename T, bool LDSX, bool F22, int KC = 1, int MODE = 0>
 __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__restrict__ chunks,
                                                             const int32_t *__restrict__ perm,
                                                             const typename sell_idx<LDSX>::type *__restrict__ idx,
@@ -112,6 +117,8 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
                                                             const T *__restrict__ x, int64_t xn, int64_t W,
                                                             int64_t nseg, T *__restrict__ out,
                                                             const cg_scalars<T> *__restrict__ status) {
+    constexpr int XC = MODE == 2 ? KC : 1;   // channels of the gathered vector
+    constexpr int OC = MODE == 1 ? KC : 1;   // outputs per segment
     constexpr int XW = LDSX ? sell_width<T>() : 1;
     __shared__ T xs[XW];
     if (status != nullptr && status->converged) return;
@@ -119,10 +126,10 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
     const int c0 = bchunk[blockIdx.x], c1 = bchunk[blockIdx.x + 1];
     if (c0 >= c1) return;
     const int q = chunks[c0].q;
-    T *o = out + (int64_t) q * nseg;
-    const T *xg = x + (int64_t) q * W;  // LDSX: panel q gathers x[q W + local]; otherwise W = 0
+    T *o = out + (int64_t) q * nseg * OC;
+    const T *xg = x + (int64_t) q * W * XC;  // LDSX: panel q gathers x[q W + local]; otherwise W = 0
     if constexpr (LDSX) {
-        const int xl = (int) min((int64_t) W, xn - (int64_t) q * W);
+        const int xl = (int) min((int64_t) W, xn - (int64_t) q * W) * XC;
         constexpr int XPER = XW / SELL_NT;
         T t[XPER];
 #pragma unroll
@@ -134,7 +141,7 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
         for (int u = 0; u < XPER; ++u) xs[tid + u * SELL_NT] = t[u];
         __syncthreads();
     }
-    auto gx = [&](int c) -> T {
+    auto gx = [&](int64_t c) -> T {
         if constexpr (LDSX) return xs[c];
         else return xg[c];
     };
@@ -146,7 +153,9 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
         // steps of SELL_UNROLL entries; a step past the width re-reads the slot's last entry (same
         // cache line) and masks it, so every step issues all of its loads at once
         const int last = max(ch.width - 1, 0);
-        T acc = 0;
+        T acc[OC];
+#pragma unroll
+        for (int k = 0; k < OC; ++k) acc[k] = T(0);
         for (int j = 0; j < ch.width; j += SELL_UNROLL) {
             typename sell_idx<LDSX>::type ci[SELL_UNROLL];
             T vi[SELL_UNROLL];
@@ -159,10 +168,28 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
 #pragma unroll
             for (int u = 0; u < SELL_UNROLL; ++u) {
                 const T v = j + u < ch.width ? vi[u] : T(0);
-                acc = fma(v, gx((int) ci[u]), acc);
+                if constexpr (MODE == 0) {
+                    acc[0] = fma(v, gx((int64_t) ci[u]), acc[0]);
+                } else if constexpr (MODE == 1) {
+                    T t = v * gx((int64_t) ci[u]);
+#pragma unroll
+                    for (int k = 0; k < KC; ++k) {
+                        acc[k] += t;
+                        t *= v;
+                    }
+                } else {
+                    const int64_t cb = (int64_t) ci[u] * KC;
+                    T h = gx(cb + KC - 1);
+#pragma unroll
+                    for (int k = KC - 2; k >= 0; --k) h = fma(h, v, gx(cb + k));
+                    acc[0] = fma(h, v, acc[0]);
+                }
             }
         }
-        if (slot_seg >= 0) o[slot_seg] = acc;
+        if (slot_seg >= 0) {
+#pragma unroll
+            for (int k = 0; k < OC; ++k) o[(int64_t) k * nseg + slot_seg] = acc[k];
+        }
     }
 }
 
@@ -201,28 +228,53 @@ __global__ __launch_bounds__(256) void panel_reduce_kernel(const T *__restrict__
     if (quarter == 0 && s < nseg) out[s] = ((a + part[0][lane]) + part[1][lane]) + part[2][lane];
 }
 
-// out[0..nseg) = the pass result (partial slabs + reduction when P > 1)
-template <typename T>
-inline void launch_panel_spmv(const spmv_plan<T> &pl, const T *x, int64_t xn, T *out, const cg_scalars<T> *status,
-                              hipStream_t stream) {
-    if (pl.nseg <= 0 || pl.nblocks <= 0) return;
-    T *dst = pl.P > 1 ? pl.partial.get() : out;
+// out[0..nseg) = the pass result (partial slabs + reduction when P > 1). kc / mode: see sell_spmv_kernel
+// (mode 1 writes kc outputs per segment, out[k * nseg + s]; mode 2 gathers kc channels x[i * kc + k]);
+// the plan must have been built with the same channel counts.
+template <typename T, int KC, int MODE>
+inline void launch_panel_spmv_t(const spmv_plan<T> &pl, const T *x, int64_t xn, T *out, const cg_scalars<T> *status,
+                                hipStream_t stream) {
     const bool f22 = pl.val22.get() != nullptr;
+    T *dst = pl.P > 1 ? pl.partial.get() : out;
     const dim3 grid((unsigned) pl.nblocks), block(SELL_NT);
     if (pl.ldsx) {
-        auto k = f22 ? sell_spmv_kernel<T, true, true> : sell_spmv_kernel<T, true, false>;
+        auto k = f22 ? sell_spmv_kernel<T, true, true, KC, MODE> : sell_spmv_kernel<T, true, false, KC, MODE>;
         hipLaunchKernelGGL(k, grid, block, 0, stream, pl.chunks.get(), pl.perm.get(), pl.idx16.get(), pl.vals(),
                            pl.bchunk.get(), x, xn, pl.W, pl.nseg, dst, status);
     } else {
-        auto k = f22 ? sell_spmv_kernel<T, false, true> : sell_spmv_kernel<T, false, false>;
+        auto k = f22 ? sell_spmv_kernel<T, false, true, KC, MODE> : sell_spmv_kernel<T, false, false, KC, MODE>;
         hipLaunchKernelGGL(k, grid, block, 0, stream, pl.chunks.get(), pl.perm.get(), pl.idx32.get(), pl.vals(),
                            pl.bchunk.get(), x, xn, (int64_t) 0, pl.nseg, dst, status);
     }
     MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+inline void launch_panel_spmv(const spmv_plan<T> &pl, const T *x, int64_t xn, T *out, const cg_scalars<T> *status,
+                              hipStream_t stream, int kc = 1, int mode = 0) {
+    if (pl.nseg <= 0 || pl.nblocks <= 0) return;
+    if (mode == 0) {
+        launch_panel_spmv_t<T, 1, 0>(pl, x, xn, out, status, stream);
+    } else if (mode == 1) {
+        switch (kc) {
+            case 2: launch_panel_spmv_t<T, 2, 1>(pl, x, xn, out, status, stream); break;
+            case 4: launch_panel_spmv_t<T, 4, 1>(pl, x, xn, out, status, stream); break;
+            case 8: launch_panel_spmv_t<T, 8, 1>(pl, x, xn, out, status, stream); break;
+            default: launch_panel_spmv_t<T, 16, 1>(pl, x, xn, out, status, stream);
+        }
+    } else {
+        switch (kc) {
+            case 2: launch_panel_spmv_t<T, 2, 2>(pl, x, xn, out, status, stream); break;
+            case 4: launch_panel_spmv_t<T, 4, 2>(pl, x, xn, out, status, stream); break;
+            case 8: launch_panel_spmv_t<T, 8, 2>(pl, x, xn, out, status, stream); break;
+            default: launch_panel_spmv_t<T, 16, 2>(pl, x, xn, out, status, stream);
+        }
+    }
     if (pl.P > 1) {
+        const int64_t ns = pl.nseg * (mode == 1 ? kc : 1);
         const int split = pl.P >= 16 ? 1 : 0;
-        hipLaunchKernelGGL(panel_reduce_kernel<T>, dim3((unsigned) ceil_div(pl.nseg, split ? 64 : 256)), dim3(256), 0,
-                           stream, pl.partial.get(), pl.P, pl.nseg, split, out, status);
+        hipLaunchKernelGGL(panel_reduce_kernel<T>, dim3((unsigned) ceil_div(ns, split ? 64 : 256)), dim3(256), 0,
+                           stream, pl.partial.get(), pl.P, ns, split, out, status);
         MI_LAUNCH_CHECK();
     }
 }
@@ -231,14 +283,16 @@ inline void launch_panel_spmv(const spmv_plan<T> &pl, const T *x, int64_t xn, T 
 // of one segment in their summation order (for each panel). xn = length of the gathered vector.
 // target_blocks: workgroups per pass (each loads its panel of x once). force_mode: 0 auto,
 // 1 LDS panels, 2 one panel gathered from global memory.
+// xch: channels of the gathered vector (mode 2 passes: the LDS panel holds sell_width / xch indices);
+// och: outputs per segment (mode 1 passes: the partial slab holds och values per segment).
 template <typename T, typename Gen>
 void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bool fp22, Gen gen, int64_t target_blocks,
-                     hipStream_t stream, int force_mode = 0) {
+                     hipStream_t stream, int force_mode = 0, int xch = 1, int och = 1) {
     pl = spmv_plan<T>{};
     pl.nseg = nseg;
     pl.nnz = nnz;
     if (nseg <= 0) return;
-    const int64_t Wmax = sell_width<T>();
+    const int64_t Wmax = sell_width<T>() / xch;
     const int64_t P_lds = std::max<int64_t>(1, ceil_div(std::max<int64_t>(xn, 1), Wmax));
     bool ldsx = P_lds * (nseg + 1) * 2 <= std::max<int64_t>(nnz, 1);
     if (force_mode == 1) ldsx = true;
@@ -349,7 +403,7 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
     up(pl.val, vr);
     up(pl.val22, v22);
     up(pl.bchunk, bchunk);
-    if (P > 1) pl.partial.alloc(P * nseg, stream, false);
+    if (P > 1) pl.partial.alloc(P * nseg * och, stream, false);
     MI_HIP_CHECK(hipStreamSynchronize(stream));
 }
 

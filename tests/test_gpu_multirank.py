@@ -10,9 +10,9 @@ rank's share of the K·p kernels, the exchange, and the replicated device-reside
 RCCL group in test_gpu_parity.py::test_single_rank_rccl_group.)
 
 Both ranks' q, K·p (add = -1, +1), kernel part, CG delta trace, alpha and bias are compared with the
-oracle (fp64: K·p 1e-12 of max, trace 1e-6 per iteration, alpha 1e-9 of max; fp32/FP22: K·p 1e-4,
-trace 1e-3 while |r|/|r0| >= 1e-3 and alpha 2e-2, or 10x the oracle's own 1-vs-8-thread spread where
-that is larger) and with each other (bit for bit:
+oracle (fp64: K·p 1e-12 of max, trace 1e-6 per iteration, alpha 1e-9 of max; fp32/FP22: K·p 1e-4 vs
+the fp32 oracle, and trace / alpha / bias vs the fp64 oracle within 1e-3 / 2e-2 or twice the fp32
+oracle's own distance from the fp64 one, whichever is larger) and with each other (bit for bit:
 the CG is replicated).
 """
 import os
@@ -78,13 +78,21 @@ def test_world2_group_matches_oracle(oracle, case, tmp_path):
     f64 = dtype == np.float64
     ktol, ttol, atol_ = (1e-12, 1e-6, 1e-9) if f64 else (1e-4, 1e-3, 2e-2)
     ref = oracle.learn(kernel, od, y, imax=imax, **args)
-    if not f64:  # fp32: the reference's own run-to-run spread (1 vs 8 OpenMP threads) widens the bar
-        ref1 = oracle.learn(kernel, od, y, imax=imax, nthreads=1, **args)
-        ref8 = oracle.learn(kernel, od, y, imax=imax, nthreads=8, **args)
-        n8 = min(len(ref1["trace"]), len(ref8["trace"]))
-        spread_t = np.abs(ref8["trace"][:n8] / ref1["trace"][:n8] - 1).max()
-        spread_a = np.abs(ref8["alpha"] - ref1["alpha"]).max() / np.abs(ref1["alpha"]).max()
-        ttol, atol_ = max(ttol, 10 * spread_t), max(atol_, 10 * spread_a)
+    if not f64:
+        # fp32: compare with the fp64 oracle on the same (fp32-representable) inputs; the bar is the
+        # larger of the fixed fp32 tolerance and twice the fp32 oracle's own distance from it (an fp32 CG
+        # that removes most of the residual in one step is rounding-bound: here the fp32 oracle's
+        # alpha_m is 5 % off the fp64 one)
+        od64 = oracle.Data(rowptr=od.rowptr, col=od.col, val=od.X.astype(np.float64), n=od.n, d=od.d,
+                           dtype=np.float64) if od.csr else oracle.Data(od.X.astype(np.float64))
+        args64 = {k: (np.float64(v) if k != "degree" else v) for k, v in args.items()}
+        ref32 = ref
+        ref = oracle.learn(kernel, od64, y.astype(np.float64), imax=imax, **args64)
+        n8 = min(len(ref32["trace"]), len(ref["trace"]))
+        ttol = max(ttol, 2 * float(np.abs(ref32["trace"][:n8] / ref["trace"][:n8] - 1).max()))
+        amax = float(np.abs(ref["alpha"]).max())
+        atol_ = max(atol_, 2 * float(np.abs(ref32["alpha"] - ref["alpha"]).max()) / amax)
+        atol_m = 2 * abs(float(ref32["alpha"][m]) - float(ref["alpha"][m]))
 
     # the split is real: every rank owns a non-empty, disjoint part of the work
     if layout == "dense" and kp_mode != "factored":
@@ -107,10 +115,11 @@ def test_world2_group_matches_oracle(oracle, case, tmp_path):
                                    err_msg=f"{case} rank {rank}")
         np.testing.assert_allclose(r["alpha"][:m], ref["alpha"][:m], rtol=atol_, atol=atol_ * np.abs(ref["alpha"]).max())
         # alpha_m = -sum(alpha) (csvm.cpp:258) carries the summed error of all m alphas
-        tol_m = atol_ * (np.abs(ref["alpha"]).max() if f64 else np.abs(ref["alpha"][:m]).sum())
+        tol_m = atol_ * np.abs(ref["alpha"]).max() if f64 else max(atol_ * np.abs(ref["alpha"]).max(), atol_m)
         assert abs(float(r["alpha"][m]) - float(ref["alpha"][m])) <= tol_m, (case, rank)
-        assert abs(float(r["bias"]) - float(ref["bias"])) <= atol_ * max(1.0, abs(float(ref["bias"])), 0.0 if f64 else
-                                                                       float(np.abs(ref["alpha"][:m]).sum()))
+        tol_b = atol_ * max(1.0, abs(float(ref["bias"]))) if f64 else max(atol_ * max(1.0, abs(float(ref["bias"]))),
+                                                                         2 * abs(float(ref32["bias"]) - float(ref["bias"])))
+        assert abs(float(r["bias"]) - float(ref["bias"])) <= tol_b, (case, rank)
     # replicated CG: identical bits on every rank
     for key in ("kp_plus", "kpart", "alpha", "trace"):
         np.testing.assert_array_equal(res[0][key], res[1][key])
