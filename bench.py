@@ -231,9 +231,10 @@ def main():
                                                             args.features or sim) and world == 1)
     if default_run and not args.no_extra:
         # north_star's sparse target measured under the same clock: configs[2] with RBF (the >= 70 % HBM
-        # row) and configs[2] itself (sparse linear), same seeded matrix
+        # row), configs[2] itself (sparse linear, same seeded matrix) and configs[4] (2M x 100k FP22 RBF,
+        # on one GPU: the kernel expansion's memory is O(nnz + multi-feature pairs))
         extra = {}
-        for name, steps in (("csr_rbf_1m", 10), ("csr_linear_1m", 200)):
+        for name, steps in (("csr_rbf_1m", 50), ("csr_linear_1m", 200), ("fp22_rbf_2m", 30)):
             extra[name] = run_config(name, args, rank, world, dist, uid, steps, 2, not args.no_cpu,
                                      args.cpu_seconds * 0.6, args.kp_reps, data_cache=cache)
     if rank == 0:
@@ -295,19 +296,15 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
     co = float((c * (c + 1) / 2).sum())
     survey = (co * (4 + vb) + col.size * (4 + vb) + 3 * m * es) / world
     if info.get("sparse_algo") == pm._abi.SPARSE_EXPANSION:
-        # kernel expansion: the dominant launch = column moments (one CSC pass: int32 row +
-        # value per entry, w gathered once per row) + the remainder stream of the multi-feature pairs
-        # (uint16 j + H per slot, uint16 row per 4-slot chunk); bytes the algorithm must move per K·p
-        nnz = info["nnz"]
+        # kernel expansion: the dominant kernel is the remainder stream of the pairs sharing
+        # two or more features (uint16 j + H per slot, uint16 row per 4-slot chunk), read once per K·p;
+        # the column-moment and Horner passes are the two SELL SpMV passes of the linear path
         rem = info["pair_slots"] * (2 + es) + info["exp_chunks"] * 2
-        alg = rem + nnz * (4 + es) + m * es
-        return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
-                    frac=alg / s / PEAKS["hbm"], traffic=None, kernel="exp_moments_kernel+exp_hcell_kernel",
-                    launch_ms=ms_dom, alg_bytes=alg,
-                    alg_bytes_def="moments CSC pass nnz x (4 + sizeof(real)) + m x sizeof(real) + remainder stream "
-                                  "slots x (2 + sizeof(real)) + chunks x 2",
-                    remainder_bytes=rem, exp_terms=info["exp_terms"], multi_pairs=info["pairs"],
-                    pair_slots=info["pair_slots"], survey_alg_bytes=survey,
+        return dict(bound="hbm", achieved=rem / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
+                    frac=rem / s / PEAKS["hbm"], traffic=None, kernel="exp_hcell_kernel", launch_ms=ms_dom,
+                    alg_bytes=rem, alg_bytes_def="remainder stream: slots x (2 + sizeof(real)) + chunks x 2",
+                    exp_terms=info["exp_terms"], multi_pairs=info["pairs"], pair_slots=info["pair_slots"],
+                    spmv_bytes=info["spmv_bytes"], survey_alg_bytes=survey,
                     survey_effective_GBps=survey / s / 1e9, survey_effective_frac=survey / s / PEAKS["hbm"])
     # the kernel's algorithmic bytes: the stored pair stream it must read once per K·p (uint16 j + s_ij
     # per slot, rows padded to 8 per cell); SURVEY's column-join figure counts every co-occurrence

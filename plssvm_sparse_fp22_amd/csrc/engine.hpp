@@ -103,7 +103,8 @@ struct engine : engine_base {
     bool expansion_eligible();                                    // expand.hip: K, coefficients; true if usable
     void build_expansion(const int64_t *cpos, int64_t max_inc);   // multi-overlap remainder H, diagonal
     void expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);
-    void expansion_dominant(const T *p, const cg_scalars<T> *status);
+    void expansion_dominant(const T *p, const cg_scalars<T> *status);  // the remainder stream
+    void expansion_moments(const T *w, const cg_scalars<T> *status);   // column moments (SELL CSC pass)
     // raw[i] = sum_j k_ij p_j, i < m (with_base = false: only the overlap terms, PLSSVM_MI_PART_OVERLAP)
     void sparse_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base = true);
     void sparse_dominant(const T *p, const cg_scalars<T> *status);  // the dominant sparse kernel

@@ -800,8 +800,21 @@ int exp_ablate() {
     return v;
 }
 
+// the remainder stream alone (the dominant kernel of the expansion's K·p; time_kp / bench roofline)
 template <typename T>
 void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
+    auto &ex = csr.ex;
+    if (ex.nblk > 0 && !(exp_ablate() & 1)) {
+        hipLaunchKernelGGL(exp_hcell_kernel<T>, dim3((unsigned) ex.nblk), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
+                           ex.hrow.get(), ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, ex.hs.get(), status);
+        MI_LAUNCH_CHECK();
+    } else if (r1 > r0) {
+        MI_HIP_CHECK(hipMemsetAsync(ex.hs.get() + r0, 0, sizeof(T) * (size_t) (r1 - r0), stream));
+    }
+}
+
+template <typename T>
+void engine<T>::expansion_moments(const T *w, const cg_scalars<T> *status) {
     auto &ex = csr.ex;
     if (d > 0) {  // column moments: one SELL pass over the CSC (mode 1), then the coefficients
         launch_panel_spmv<T>(csr.spmv_csc, w, m, ex.mom.get(), status, stream, ex.KM, 1);
@@ -812,13 +825,6 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
         hipLaunchKernelGGL(exp_mscale_kernel<T>, dim3((unsigned) ceil_div(d * ex.KM, 256)), dim3(256), 0, stream,
                            ex.mom.get(), d, ex.KM, cf, ex.M.get(), status);
         MI_LAUNCH_CHECK();
-    }
-    if (ex.nblk > 0 && !(exp_ablate() & 1)) {
-        hipLaunchKernelGGL(exp_hcell_kernel<T>, dim3((unsigned) ex.nblk), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
-                           ex.hrow.get(), ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, ex.hs.get(), status);
-        MI_LAUNCH_CHECK();
-    } else if (r1 > r0) {
-        MI_HIP_CHECK(hipMemsetAsync(ex.hs.get() + r0, 0, sizeof(T) * (size_t) (r1 - r0), stream));
     }
 }
 
@@ -834,6 +840,7 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     }
     launch_dot2<T>(w, nullptr, nullptr, nullptr, m, red.get(), status, stream);  // S = sum_j w_j
     launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+    expansion_moments(w, status);
     expansion_dominant(w, status);
     T kappa = 0;
     if (kernel == 1) {
@@ -853,6 +860,7 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     template bool engine<T>::expansion_eligible();                                           \
     template void engine<T>::build_expansion(const int64_t *, int64_t);                      \
     template void engine<T>::expansion_dominant(const T *, const cg_scalars<T> *);           \
+    template void engine<T>::expansion_moments(const T *, const cg_scalars<T> *);            \
     template void engine<T>::expansion_kp_raw(const T *, const cg_scalars<T> *, bool);
 INST(float)
 INST(double)

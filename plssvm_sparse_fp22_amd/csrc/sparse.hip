@@ -969,7 +969,7 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
         spmv_pass_csr(status);
         return;
     }
-    if (csr.ex.on) {  // timing: the moments + remainder stream (p stands in for w)
+    if (csr.ex.on) {  // timing: the remainder stream (p stands in for w)
         expansion_dominant(p, status);
         return;
     }

@@ -60,6 +60,7 @@ def main():
     fetch_kib = sum(statistics.mean(v) * mult[k] for k, v in vals.items())
     out = {
         "config": config, "N": bench["config"]["N"], "d": bench["config"]["d"], "n_gpus": bench["n_gpus"],
+        "dtype": bench["dtype"], "kernel_function": bench["config"]["kernel"],
         "kernel": bench["roofline"]["kernel"], "dispatches": min(len(v) for v in vals.values()), "fetch_size_kib_mean": fetch_kib,
         "hbm_read_bytes_per_launch": fetch_kib * 1024 * 2,
         "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 counts half of wide streaming reads)",
