@@ -99,8 +99,11 @@ class Parameter:
         self.labels = None
 
     def parse_train_file(self, path, sparse=False):
-        with open(path, "rb") as f:
-            binary = f.read(8) == _io.BIN_MAGIC
+        try:
+            with open(path, "rb") as f:
+                binary = f.read(8) == _io.BIN_MAGIC
+        except FileNotFoundError:  # file_not_found_exception (src/plssvm/detail/file_reader.cpp:104-108)
+            raise FileNotFoundError(f"Couldn't find file: '{path}'!") from None
         if binary:  # PLSSVMB1 binary CSR / FP22 file (io.write_binary): always sparse
             csr, y, fmt = _io.read_binary(path, dtype=self.real_type)
             self.csr, self.data, self.labels = csr, None, y

@@ -23,6 +23,7 @@
 #include <stdexcept>
 #include <string>
 #include <string_view>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -46,10 +47,38 @@ inline kernel_type parse_kernel(std::string s) {
     throw std::invalid_argument("Unrecognized kernel type '" + s + "'!");
 }
 
+// plssvm::invalid_file_format_exception / file_not_found_exception (include/plssvm/exceptions/exceptions.hpp)
 struct invalid_file_format_exception : std::runtime_error {
     using std::runtime_error::runtime_error;
 };
+struct file_not_found_exception : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
 
+template <typename T>
+constexpr const char *arithmetic_type_name() {  // include/plssvm/detail/arithmetic_type_name.hpp
+    if constexpr (std::is_same_v<T, float>) return "float";
+    else if constexpr (std::is_same_v<T, double>) return "double";
+    else if constexpr (std::is_same_v<T, int>) return "int";
+    else if constexpr (std::is_same_v<T, unsigned int>) return "unsigned int";
+    else if constexpr (std::is_same_v<T, unsigned long>) return "unsigned long";
+    else return "unsigned long long";
+}
+
+// detail::convert_to (include/plssvm/detail/string_conversion.hpp:39-64): leading whitespace skipped, the
+// longest valid prefix converted (std::from_chars; correctly rounded like fast_float), error message verbatim
+template <typename T>
+T convert_to(std::string_view sv) {
+    while (!sv.empty() && std::isspace((unsigned char) sv.front())) sv.remove_prefix(1);
+    T v{};
+    const auto r = std::from_chars(sv.data(), sv.data() + sv.size(), v);
+    if (r.ec != std::errc{})
+        throw invalid_file_format_exception("Can't convert '" + std::string(sv) + "' to a value of type " +
+                                            arithmetic_type_name<T>() + "!");
+    return v;
+}
+
+// a whole token as a real (data values: trailing characters are an error)
 template <typename T>
 T to_real(std::string_view sv) {
     while (!sv.empty() && std::isspace((unsigned char) sv.front())) sv.remove_prefix(1);
@@ -57,7 +86,8 @@ T to_real(std::string_view sv) {
     T v{};
     const auto r = std::from_chars(sv.data(), sv.data() + sv.size(), v);  // correctly rounded, like fast_float
     if (r.ec != std::errc{} || r.ptr != sv.data() + sv.size())
-        throw invalid_file_format_exception("Can't convert '" + std::string(sv) + "' to a floating point value!");
+        throw invalid_file_format_exception("Can't convert '" + std::string(sv) + "' to a value of type " +
+                                            arithmetic_type_name<T>() + "!");
     return v;
 }
 
@@ -127,7 +157,8 @@ struct parameter {
                 unsigned long index = 0;
                 const auto res = std::from_chars(idx.data(), idx.data() + idx.size(), index);
                 if (res.ec != std::errc{})
-                    throw invalid_file_format_exception("Can't convert '" + std::string(idx) + "' to an index!");
+                    throw invalid_file_format_exception("Can't convert '" + std::string(idx) +
+                                                        "' to a value of type unsigned long!");
                 p = c + 1;
                 std::size_t e = line.find(' ', p);
                 if (e == std::string_view::npos) e = line.size();
@@ -142,7 +173,7 @@ struct parameter {
 
     static std::string read_file(const std::string &filename) {
         std::ifstream f(filename, std::ios::binary);
-        if (!f) throw std::runtime_error("Couldn't find file: '" + filename + "'!");
+        if (!f) throw file_not_found_exception("Couldn't find file: '" + filename + "'!");
         std::stringstream ss;
         ss << f.rdbuf();
         return ss.str();
@@ -276,54 +307,120 @@ struct parameter {
             for (const real_type v : pr.first) labels.push_back(v > real_type{ 0 } ? real_type{ 1 } : real_type{ -1 });
     }
 
-    // parse_model_file (src/plssvm/parameter.cpp:366-520): header (kernel_type, degree, gamma, coef0,
-    // rho, ...) until "SV", then one "alpha idx:val ..." line per support vector; the support vectors
-    // become this object's data, their alphas `alpha`, -rho the bias
+    // parse_model_file (src/plssvm/parameter.cpp:366-520): the header lines (left-trimmed, '#' comments
+    // skipped, lower-cased) until "sv", with the reference's checks and messages; then total_sv lines
+    // "alpha idx:val ..." — the support vectors become this object's data, their alphas `alpha`, -rho the bias
     real_type rho = 0;
     std::vector<real_type> alpha;
+    std::vector<int64_t> nr_sv;
+    real_type label_first = 0, label_second = 0;
     void parse_model_file(const std::string &filename, bool keep_sparse = false, int64_t min_features = 0) {
         const std::string content = read_file(filename);
-        std::size_t pos = 0;
-        bool have_kernel = false, have_rho = false;
-        while (true) {
-            if (pos >= content.size()) throw invalid_file_format_exception("Can't parse file: no support vectors are given!");
+        // lines as detail::file_reader keeps them (file_reader.cpp:129-153)
+        std::vector<std::string_view> lines;
+        for (std::size_t pos = 0; pos <= content.size();) {
             std::size_t nl = content.find('\n', pos);
             if (nl == std::string::npos) nl = content.size();
-            std::string line(content.data() + pos, nl - pos);
+            std::string_view l(content.data() + pos, nl - pos);
             pos = nl + 1;
-            while (!line.empty() && std::isspace((unsigned char) line.back())) line.pop_back();
-            std::size_t b = 0;
-            while (b < line.size() && std::isspace((unsigned char) line[b])) ++b;
-            line = line.substr(b);
-            if (line.empty()) continue;
-            if (line == "SV") break;
-            const std::size_t sp = line.find(' ');
-            const std::string key = line.substr(0, sp), value = sp == std::string::npos ? "" : line.substr(sp + 1);
-            if (key == "svm_type") {
-                if (value != "c_svc") throw invalid_file_format_exception("Can only use c_svc as svm_type, but '" + value + "' was given!");
-            } else if (key == "kernel_type") {
-                kernel = parse_kernel(value);
-                have_kernel = true;
-            } else if (key == "degree") {
-                degree = std::stoi(value);
-            } else if (key == "gamma") {
-                gamma = to_real<real_type>(value);
-            } else if (key == "coef0") {
-                coef0 = to_real<real_type>(value);
-            } else if (key == "rho") {
-                rho = to_real<real_type>(value);
-                have_rho = true;
-            } else if (key == "nr_class") {
-                if (std::stoi(value) != 2) throw invalid_file_format_exception("Can only use 2 classes, but " + value + " were given!");
-            } else if (key == "total_sv" || key == "label" || key == "nr_sv") {
-                // informational (the SV section defines the support vectors)
+            while (!l.empty() && std::isspace((unsigned char) l.front())) l.remove_prefix(1);
+            if (!l.empty() && l.front() != '#') lines.push_back(l);
+        }
+        unsigned long long num_sv = 0;
+        bool rho_set = false, nr_sv_set = false;
+        label_first = label_second = 0;
+        auto trim_left = [](std::string_view v) {
+            while (!v.empty() && std::isspace((unsigned char) v.front())) v.remove_prefix(1);
+            return v;
+        };
+        std::size_t header = 0;
+        for (; header < lines.size(); ++header) {
+            std::string_view raw = lines[header];
+            while (!raw.empty() && std::isspace((unsigned char) raw.back())) raw.remove_suffix(1);
+            std::string line(raw);
+            std::transform(line.begin(), line.end(), line.begin(), [](unsigned char c) { return (char) std::tolower(c); });
+            std::string_view value{ line };
+            value.remove_prefix(std::min(value.find_first_of(' ') + 1, value.size()));
+            value = trim_left(value);
+            auto starts = [&](const char *k) { return line.rfind(k, 0) == 0; };
+            if (starts("svm_type")) {
+                if (value != "c_svc")
+                    throw invalid_file_format_exception("Can only use c_svc as svm_type, but '" + std::string(value) +
+                                                        "' was given!");
+            } else if (starts("kernel_type")) {
+                std::string_view tok = value.substr(0, value.find_first_of(' '));
+                if (tok == "linear" || tok == "0") kernel = kernel_type::linear;
+                else if (tok == "polynomial" || tok == "1") kernel = kernel_type::polynomial;
+                else if (tok == "rbf" || tok == "2") kernel = kernel_type::rbf;
+                else throw invalid_file_format_exception("Unrecognized kernel type '" + std::string(value) + "'!");
+            } else if (starts("gamma")) {
+                gamma = convert_to<real_type>(value);
+            } else if (starts("degree")) {
+                degree = convert_to<int>(value);
+            } else if (starts("coef0")) {
+                coef0 = convert_to<real_type>(value);
+            } else if (starts("nr_class")) {
+                const auto nr_class = convert_to<unsigned int>(value);
+                if (nr_class != 2)
+                    throw invalid_file_format_exception("Can only use 2 classes, but " + std::to_string(nr_class) +
+                                                        " were given!");
+            } else if (starts("total_sv")) {
+                num_sv = convert_to<unsigned long long>(value);
+                if (num_sv == 0)
+                    throw invalid_file_format_exception("The number of support vectors must be greater than 0, but is 0!");
+            } else if (starts("rho")) {
+                rho = convert_to<real_type>(value);
+                rho_set = true;
+            } else if (starts("label")) {
+                const std::string_view first = value.substr(0, value.find_first_of(' '));
+                label_first = convert_to<real_type>(first);
+                value.remove_prefix(std::min(first.size() + 1, value.size()));
+                const std::string_view second = value.substr(0, value.find_first_of(" \n"));
+                label_second = convert_to<real_type>(second);
+                value.remove_prefix(std::min(second.size() + 1, value.size()));
+                value = trim_left(value);
+                if (!value.empty() || (label_first != 1 && label_first != -1) || (label_second != 1 && label_second != -1))
+                    throw invalid_file_format_exception("Only the labels 1 and -1 are allowed, but '" + line +
+                                                        "' were given!");
+            } else if (starts("nr_sv")) {
+                const std::string_view first = value.substr(0, value.find_first_of(' '));
+                const auto a = convert_to<unsigned long long>(first);
+                value.remove_prefix(std::min(first.size() + 1, value.size()));
+                const std::string_view second = value.substr(0, value.find_first_of(" \n"));
+                const auto b = convert_to<unsigned long long>(second);
+                value.remove_prefix(std::min(second.size() + 1, value.size()));
+                value = trim_left(value);
+                if (!value.empty())
+                    throw invalid_file_format_exception("Only two numbers are allowed, but more were given '" + line + "'!");
+                if (a + b != num_sv)
+                    throw invalid_file_format_exception(
+                        "The number of positive and negative support vectors doesn't add up to the total number: " +
+                        std::to_string(a) + " + " + std::to_string(b) + " != " + std::to_string(num_sv) + "!");
+                nr_sv = { (int64_t) a, (int64_t) b };
+                nr_sv_set = true;
+            } else if (line == "sv") {
+                break;
             } else {
-                throw invalid_file_format_exception("Unrecognized header entry '" + key + "'! Maybe SV is missing?");
+                throw invalid_file_format_exception("Unrecognized header entry '" + std::string(raw) +
+                                                    "'! Maybe SV is missing?");
             }
         }
-        if (!have_kernel) throw invalid_file_format_exception("Missing kernel_type!");
-        if (!have_rho) throw invalid_file_format_exception("Missing rho value!");
-        const rows_t pr = parse_rows(content, pos);
+        if (num_sv == 0) throw invalid_file_format_exception("Missing total number of support vectors!");
+        if (label_first == 0 || label_second == 0) throw invalid_file_format_exception("Missing labels!");
+        if (!nr_sv_set) throw invalid_file_format_exception("Missing number of support vectors per class!");
+        if (!rho_set) throw invalid_file_format_exception("Missing rho value!");
+        if (header + 1 >= lines.size())
+            throw invalid_file_format_exception("Can't parse file: no support vectors are given or SV is missing!");
+        if (lines.size() - header - 1 < num_sv)
+            throw invalid_file_format_exception("total_sv is " + std::to_string(num_sv) + ", but only " +
+                                                std::to_string(lines.size() - header - 1) +
+                                                " support vectors are given!");
+        // the support vector lines: exactly total_sv of them (parse_libsvm_content(f, header + 1, data(num_sv), ...))
+        const std::size_t sv_begin = (std::size_t) (lines[header + 1].data() - content.data());
+        const std::size_t sv_end = header + 1 + num_sv < lines.size()
+                                       ? (std::size_t) (lines[header + 1 + num_sv].data() - content.data())
+                                       : content.size();
+        const rows_t pr = parse_rows(content.substr(0, sv_end), sv_begin);
         if (!pr.has_first || pr.first.size() != pr.rows.size())
             throw invalid_file_format_exception("Every support vector needs an alpha value!");
         set_rows(pr, keep_sparse, min_features);

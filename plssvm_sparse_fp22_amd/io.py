@@ -31,6 +31,14 @@ def _lines(path):
             yield s.rstrip("\n")
 
 
+def _convert_token(tok, dtype):
+    """A whole token as a real of dtype (InvalidFileFormat with the reference's message otherwise)."""
+    try:
+        return float(tok)
+    except ValueError:
+        raise InvalidFileFormat(f"Can't convert '{tok.strip()}' to a value of type {_type_name(dtype)}!") from None
+
+
 def parse_libsvm(path, dtype=np.float64, sparse=False):
     """Returns (X, y) with X dense [n][d] (or (rowptr, col, val, n, d) when sparse) and y in {-1,+1}
     (None when the file carries no labels)."""
@@ -43,7 +51,7 @@ def parse_libsvm(path, dtype=np.float64, sparse=False):
         if pos == -1:
             pos = len(line)
         if colon == -1 or colon >= pos:
-            labels.append(float(line[:pos]))
+            labels.append(_convert_token(line[:pos], dtype))
             rest = line[pos:]
             has_label = True if has_label is None else has_label
         else:
@@ -54,8 +62,10 @@ def parse_libsvm(path, dtype=np.float64, sparse=False):
             if ":" not in tok:
                 break  # trailing comment or garbage after the last feature
             k, v = tok.split(":", 1)
+            if not k.strip().isdigit():
+                raise InvalidFileFormat(f"Can't convert '{k.strip()}' to a value of type unsigned long!")
             cols.append(int(k))
-            vals.append(float(v))
+            vals.append(_convert_token(v, dtype))
         order = np.argsort(np.asarray(cols, dtype=np.int64), kind="stable")
         rows_c.append(np.asarray(cols, dtype=np.int64)[order])
         rows_v.append(np.asarray(vals, dtype=np.float64)[order])
