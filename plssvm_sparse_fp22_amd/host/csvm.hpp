@@ -1,10 +1,11 @@
 // plssvm::mi355x::csvm<T> — the reference's plssvm::csvm<T> / hip::csvm<T> surface over the C ABI
 // (include/plssvm_mi355x.h). Host-only C++17; all compute runs in libplssvm_mi355x.so on the GPU.
 //
-// Mirrors include/plssvm/csvm.hpp:33-278 for the training path: the constructor validates the data
-// like csvm.cpp:43-53, learn() is csvm.cpp:207-267 calling setup_data_on_device / generate_q /
-// solver_CG (the hooks mock_hip_csvm exposes, tests/backends/HIP/mock_hip_csvm.hpp:24-51, are public
-// here too), write_model() writes the LIBSVM model format of csvm.cpp:60-204.
+// Derives from csvm_interface<T> (csvm_interface.hpp: the reference's abstract plssvm::csvm<T>, restated:
+// same pure virtuals, state, constructor checks and learn()) and implements its five pure virtuals on the
+// C ABI — exactly what a maintainer's hip::csvm<T> replacement does. The hooks
+// mock_hip_csvm exposes (tests/backends/HIP/mock_hip_csvm.hpp:24-51) are public here; write_model()
+// writes the LIBSVM model format of csvm.cpp:60-204.
 #pragma once
 
 #include <charconv>
@@ -15,6 +16,7 @@
 #include <vector>
 
 #include "../../include/plssvm_mi355x.h"
+#include "csvm_interface.hpp"
 #include "parameter.hpp"
 
 namespace plssvm::mi355x {
@@ -25,27 +27,26 @@ struct backend_exception : std::runtime_error {  // plssvm::hip::backend_excepti
 };
 
 template <typename T>
-class csvm {
+class csvm : public csvm_interface<T> {
+    using base = csvm_interface<T>;
+
   public:
     using real_type = T;
+    using base::learn;  // learn() (imax = num_features) and learn(imax)
 
-    explicit csvm(const parameter<T> &params, int device = 0) : params_(params) {
-        if (params.num_data_points == 0) throw std::invalid_argument("Data set is empty!");
-        if (params.num_features == 0) throw std::invalid_argument("No features provided for the data points!");
-        const int rc = plssvm_mi_create((int) sizeof(T), (int) params.kernel, params.degree, (double) params.gamma,
-                                        (double) params.coef0, (double) params.cost, device, &ctx_);
+    explicit csvm(const parameter<T> &params, int device = 0) : base(params) {
+        const int rc = plssvm_mi_create((int) sizeof(T), (int) this->kernel_, this->degree_, (double) this->gamma_,
+                                        (double) this->coef0_, (double) this->cost_, device, &ctx_);
         if (rc != PLSSVM_MI_OK) throw backend_exception(rc, plssvm_mi_last_error(nullptr));
     }
-    ~csvm() { plssvm_mi_destroy(ctx_); }
-    csvm(const csvm &) = delete;
-    csvm &operator=(const csvm &) = delete;
+    ~csvm() override { plssvm_mi_destroy(ctx_); }
 
     // one process per GPU: join a row-block group before setup (rank 0 creates the id)
     void join_group(int rank, int world, const void *unique_id) { check(plssvm_mi_comm_init(ctx_, rank, world, unique_id)); }
 
-    // ---- gpu_csvm hot-path surface ----
-    void setup_data_on_device() {
-        const auto &p = params_;
+    // ---- the reference's pure virtuals (csvm.hpp:188-214), public here like mock_hip_csvm's hooks ----
+    void setup_data_on_device() override {
+        const auto &p = this->params_;
         if (p.sparse) {
             const bool f22 = !p.val22.empty() && sizeof(T) == 4;  // packed FP22 input stays packed
             check(plssvm_mi_setup_csr(ctx_, p.rowptr.data(), p.col.data(), f22 ? (const void *) p.val22.data() : p.val.data(),
@@ -53,16 +54,17 @@ class csvm {
         } else {
             check(plssvm_mi_setup_dense(ctx_, p.dense.data(), p.num_data_points, p.num_features));
         }
+        on_device_ = true;
     }
-    std::vector<T> generate_q() {
-        std::vector<T> q((std::size_t) std::max<int64_t>(params_.num_data_points - 1, 1));
+    [[nodiscard]] std::vector<T> generate_q() override {
+        std::vector<T> q(std::max<std::size_t>(this->num_data_points_ - 1, 1));
         double qa = 0;
         check(plssvm_mi_generate_q(ctx_, q.data(), &qa));
-        QA_cost_ = (T) qa;
-        q.resize((std::size_t) (params_.num_data_points - 1));
+        q.resize(this->num_data_points_ - 1);
         return q;
     }
-    std::vector<T> solver_CG(const std::vector<T> &b, std::size_t imax, T eps, const std::vector<T> &q) {
+    std::vector<T> solver_CG(const std::vector<T> &b, std::size_t imax, T eps, const std::vector<T> &q) override {
+        check(plssvm_mi_set_qa_cost(ctx_, (double) this->QA_cost_));  // learn() computed it on the host
         std::vector<T> x(std::max<std::size_t>(b.size(), 1));
         trace_.assign(imax + 1, 0.0);
         int64_t it = 0;
@@ -72,40 +74,48 @@ class csvm {
         x.resize(b.size());
         return x;
     }
+    // gpu_csvm::update_w (gpu_csvm.cpp:327-350): w_ = sum_i alpha_i x_i (linear model vector)
+    void update_w() override {
+        need_model();
+        this->w_.assign(std::max<std::size_t>(this->num_features_, 1), T(0));
+        check(plssvm_mi_update_w(ctx_, this->alpha_ptr_->data(), this->w_.data()));
+        this->w_.resize(this->num_features_);
+    }
+    // gpu_csvm::predict (gpu_csvm.cpp:52-127): decision values bias + sum_i alpha_i k(x_i, z) of dense points
+    [[nodiscard]] std::vector<T> predict(const std::vector<std::vector<T>> &points) override {
+        need_model();
+        if (points.empty()) return {};
+        std::vector<T> Z;
+        Z.reserve(points.size() * points[0].size());
+        for (const auto &z : points) {
+            if (z.size() != points[0].size()) throw exception{ "All points in the data vector must have the same number of features!" };
+            Z.insert(Z.end(), z.begin(), z.end());
+        }
+        std::vector<T> out(points.size());
+        check(plssvm_mi_predict_dense(ctx_, this->alpha_ptr_->data(), (double) this->bias_, Z.data(), (int64_t) points.size(),
+                                      (int64_t) points[0].size(), out.data()));
+        return out;
+    }
+
+    // ---- run_device_kernel + the mock_hip_csvm setters (tests/backends/HIP/mock_hip_csvm.hpp:24-51) ----
     void run_device_kernel(const std::vector<T> &q, std::vector<T> &ret, const std::vector<T> &d, T add) {
         check(plssvm_mi_kp(ctx_, q.data(), d.data(), ret.data(), (double) add));
     }
-    void set_cost(T c) { check(plssvm_mi_set_cost(ctx_, (double) c)); }
+    void set_cost(T c) {
+        check(plssvm_mi_set_cost(ctx_, (double) c));
+        this->cost_ = c;
+    }
     void set_QA_cost(T qa) {
         check(plssvm_mi_set_qa_cost(ctx_, (double) qa));
-        QA_cost_ = qa;
-    }
-
-    // csvm<T>::learn (src/plssvm/csvm.cpp:207-267); imax < 0 = num_features (csvm.cpp:256)
-    void learn(int64_t imax = -1) {
-        const auto &y = params_.labels;
-        if (y.empty()) throw std::invalid_argument("No labels given for training! Maybe the data is only usable for prediction?");
-        if ((int64_t) y.size() != params_.num_data_points)
-            throw std::invalid_argument("Number of labels must match the number of data points!");
-        setup_data_on_device();
-        on_device_ = true;
-        const std::vector<T> q = generate_q();
-        const std::size_t m = (std::size_t) params_.num_data_points - 1;
-        std::vector<T> b(y.begin(), y.begin() + (std::ptrdiff_t) m);
-        for (T &v : b) v -= y.back();
-        std::vector<T> alpha = solver_CG(b, (std::size_t) (imax < 0 ? params_.num_features : imax), params_.epsilon, q);
-        T s = 0, qa = 0;
-        for (std::size_t i = 0; i < m; ++i) s += alpha[i];
-        for (std::size_t i = 0; i < m; ++i) qa = std::fma(q[i], alpha[i], qa);
-        bias_ = y.back() + QA_cost_ * s - qa;
-        alpha.push_back(-s);
-        alpha_ = std::move(alpha);
+        this->QA_cost_ = qa;
     }
 
     // csvm<T>::write_model (src/plssvm/csvm.cpp:60-204): positive-label support vectors first
     void write_model(const std::string &filename) const {
-        if (alpha_.empty()) throw std::invalid_argument("No alphas given! Maybe a call to 'learn()' is missing?");
-        const auto &p = params_;
+        if (this->alpha_ptr_ == nullptr) throw exception{ "No alphas given! Maybe a call to 'learn()' is missing?" };
+        const auto &p = this->params_;
+        const auto &alpha_ = *this->alpha_ptr_;
+        const T bias_ = this->bias_;
         std::size_t npos = 0, nneg = 0;
         for (const T v : p.labels) (v > 0 ? npos : nneg) += 1;
         std::string out = "svm_type c_svc\nkernel_type ";
@@ -146,29 +156,24 @@ class csvm {
     // model use (csvm.hpp:123-178; gpu_csvm::update_w / predict, gpu_csvm.cpp:52-127,327-350). Without a
     // preceding learn(), set_model() supplies the alphas and rho of a model file.
     void set_model(std::vector<T> alpha, T rho) {
-        if ((int64_t) alpha.size() != params_.num_data_points)
-            throw std::invalid_argument("Number of alphas must match the number of support vectors!");
-        alpha_ = std::move(alpha);
-        bias_ = -rho;
-        on_device_ = false;
+        if (alpha.size() != this->num_data_points_)
+            throw exception{ "Number of weights (" + std::to_string(alpha.size()) + ") must match the number of data points (" +
+                             std::to_string(this->num_data_points_) + ")!" };
+        this->alpha_ptr_ = std::make_shared<const std::vector<T>>(std::move(alpha));
+        this->bias_ = -rho;
+        this->w_.clear();
     }
-    std::vector<T> update_w() {
-        need_model();
-        std::vector<T> w((std::size_t) std::max<int64_t>(params_.num_features, 1));
-        check(plssvm_mi_update_w(ctx_, alpha_.data(), w.data()));
-        w.resize((std::size_t) params_.num_features);
-        return w;
-    }
-    // decision values bias + sum_i alpha_i k(sv_i, z) of the points held by `points`
+    // decision values bias + sum_i alpha_i k(sv_i, z) of the points held by `points` (dense or CSR)
     std::vector<T> predict(const parameter<T> &points) {
         need_model();
         std::vector<T> out((std::size_t) std::max<int64_t>(points.num_data_points, 1));
+        const T *alpha = this->alpha_ptr_->data();
         if (points.sparse)
-            check(plssvm_mi_predict_csr(ctx_, alpha_.data(), (double) bias_, points.rowptr.data(), points.col.data(),
+            check(plssvm_mi_predict_csr(ctx_, alpha, (double) this->bias_, points.rowptr.data(), points.col.data(),
                                         points.val.data(), PLSSVM_MI_VAL_REAL, points.num_data_points,
                                         points.num_features, out.data()));
         else
-            check(plssvm_mi_predict_dense(ctx_, alpha_.data(), (double) bias_, points.dense.data(), points.num_data_points,
+            check(plssvm_mi_predict_dense(ctx_, alpha, (double) this->bias_, points.dense.data(), points.num_data_points,
                                           points.num_features, out.data()));
         out.resize((std::size_t) points.num_data_points);
         return out;
@@ -181,19 +186,20 @@ class csvm {
     }
     // csvm::accuracy(points, correct_labels)
     T accuracy(const parameter<T> &points) {
-        if (points.labels.empty()) throw std::invalid_argument("No labels given for the accuracy calculation!");
+        if (points.labels.empty()) throw exception{ "No labels given for the accuracy calculation!" };
         const std::vector<T> l = predict_label(points);
         if (l.size() != points.labels.size())
-            throw std::invalid_argument("Number of data points to predict and correct labels mismatch!");
+            throw exception{ "Number of data points to predict and correct labels mismatch!" };
         std::size_t ok = 0;
         for (std::size_t i = 0; i < l.size(); ++i) ok += l[i] * points.labels[i] > T(0);
         return (T) ok / (T) l.size();
     }
 
-    const std::vector<T> &alpha() const { return alpha_; }
-    T bias() const { return bias_; }
-    T rho() const { return -bias_; }
-    T QA_cost() const { return QA_cost_; }
+    const std::vector<T> &alpha() const { return *this->alpha_ptr_; }
+    const std::vector<T> &w() const { return this->w_; }
+    T bias() const { return this->bias_; }
+    T rho() const { return -this->bias_; }
+    T QA_cost() const { return this->QA_cost_; }
     int64_t iterations() const { return iterations_; }
     const std::vector<double> &residual_trace() const { return trace_; }
 
@@ -205,19 +211,13 @@ class csvm {
 
   private:
     void need_model() {
-        if (alpha_.empty()) throw std::invalid_argument("No alphas provided for prediction!");
-        if (!on_device_) {
-            setup_data_on_device();
-            on_device_ = true;
-        }
+        if (this->alpha_ptr_ == nullptr) throw exception{ "No alphas provided for prediction!" };
+        if (!on_device_) setup_data_on_device();
     }
     void check(int rc) const {
         if (rc != PLSSVM_MI_OK) throw backend_exception(rc, plssvm_mi_last_error(ctx_));
     }
-    parameter<T> params_;
     plssvm_mi_ctx *ctx_ = nullptr;
-    T QA_cost_ = 0, bias_ = 0;
-    std::vector<T> alpha_;
     std::vector<double> trace_;
     int64_t iterations_ = 0;
     bool on_device_ = false;

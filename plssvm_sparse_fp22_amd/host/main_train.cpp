@@ -97,7 +97,8 @@ int train(const cli &c) {
     const int device = c.opt.count("device") ? std::stoi(c.opt.at("device")) : 0;
     csvm<T> svm(params, device);
     const auto t1 = std::chrono::steady_clock::now();
-    svm.learn(c.opt.count("max_iter") ? std::stoll(c.opt.at("max_iter")) : -1);
+    if (c.opt.count("max_iter")) svm.learn((std::size_t) std::stoll(c.opt.at("max_iter")));
+    else svm.learn();
     const auto t2 = std::chrono::steady_clock::now();
     if (params.print_info) {
         std::printf("Solved minimization problem (r = b - Ax) using CG in %lldms (%lld iterations, residuum %s).\n",
