@@ -10,7 +10,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libplssvm_mi355x.so")
+# PLSSVM_MI_LIB: an alternative build of the same library (A/B measurements of compile-time variants,
+# tools/variants.sh); never a CPU stand-in — every build behind this name is the gfx950 HIP path
+LIB_PATH = os.environ.get("PLSSVM_MI_LIB") or os.path.join(_HERE, "libplssvm_mi355x.so")
 
 OK = 0
 ERR = {-1: "ERR_ARG", -2: "ERR_HIP", -3: "ERR_RCCL", -4: "ERR_OOM", -5: "ERR_UNSUPPORTED", -6: "ERR_STATE",

@@ -182,28 +182,55 @@ __device__ __forceinline__ void store_partials(T v1, T v2, T *red, T *__restrict
     }
 }
 
+// The fused CG kernels are short (a few MB per launch): each thread loads its first CG_PRE grid-stride
+// elements before summing the previous step's partials, so that reduction overlaps the loads; the
+// per-thread element order (and every sum) is unchanged.
+constexpr int CG_PRE = 2;
+
+// slabs != null: raw_i = sum_{k < P} slabs[k * m + i], summed as panel_reduce_kernel does (from 0, in
+// panel order: bitwise the reduced pass output)
 template <typename T>
-__global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__ raw, const T *__restrict__ q,
+__global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__ raw, const T *__restrict__ slabs,
+                                                         int64_t P, const T *__restrict__ q,
                                                          const T *__restrict__ d, const T *__restrict__ psum,
                                                          T QA_cost, T cost_inv, int raw_only, int64_t m,
                                                          T *__restrict__ Ad, T *__restrict__ pdad,
                                                          cg_scalars<T> *sc) {
     if (sc->converged) return;
     __shared__ T red[CG_NT / 64], bc[1];
+    const int64_t i0 = (int64_t) blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t) gridDim.x * blockDim.x;
+    auto load_raw = [&](int64_t i) {
+        if (slabs == nullptr) return raw[i];
+        T rw = 0;
+        for (int64_t k = 0; k < P; ++k) rw += slabs[k * m + i];
+        return rw;
+    };
+    T rw[CG_PRE], qv[CG_PRE], dv[CG_PRE];
+#pragma unroll
+    for (int e = 0; e < CG_PRE; ++e) {
+        const int64_t i = i0 + e * st;
+        if (i < m) rw[e] = load_raw(i), qv[e] = q[i], dv[e] = d[i];
+    }
     T sp, sqp;
     partials_total(psum, red, bc, sp, sqp);
     if (blockIdx.x == 0 && threadIdx.x == 0) sc->sp = sp, sc->sqp = sqp;
     T s1 = 0;
-    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t) gridDim.x * blockDim.x) {
+    auto one = [&](int64_t i, T r_, T q_, T d_) {
         T v;
         {
 #pragma clang fp contract(fast)  // kp_finalize_kernel's expression, contracted as in dense.hip
-            v = raw_only ? raw[i] : raw[i] + (QA_cost - q[i]) * sp - sqp + cost_inv * d[i];
+            v = raw_only ? r_ : r_ + (QA_cost - q_) * sp - sqp + cost_inv * d_;
             v = T(0) + T(1) * v;
         }
         Ad[i] = v;
-        s1 += d[i] * v;
+        s1 += d_ * v;
+    };
+#pragma unroll
+    for (int e = 0; e < CG_PRE; ++e) {
+        const int64_t i = i0 + e * st;
+        if (i < m) one(i, rw[e], qv[e], dv[e]);
     }
+    for (int64_t i = i0 + CG_PRE * st; i < m; i += st) one(i, load_raw(i), q[i], d[i]);
     store_partials(s1, T(0), red, pdad);
 }
 
@@ -214,34 +241,54 @@ __global__ __launch_bounds__(CG_NT) void cg_upd_rr_kernel(T *__restrict__ x, T *
                                                         cg_scalars<T> *sc) {
     if (sc->converged) return;
     __shared__ T red[CG_NT / 64], bc[1];
+    const int64_t i0 = (int64_t) blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t) gridDim.x * blockDim.x;
+    T xv[CG_PRE], dv[CG_PRE], av[CG_PRE], rv[CG_PRE];  // reset: av = b
+#pragma unroll
+    for (int e = 0; e < CG_PRE; ++e) {
+        const int64_t i = i0 + e * st;
+        if (i < m) xv[e] = x[i], dv[e] = d[i], av[e] = reset ? b[i] : Ad[i], rv[e] = reset ? T(0) : r[i];
+    }
     T dAd, unused;
     partials_total(pdad, red, bc, dAd, unused);
     const T delta = sc->delta;
     const T alpha = delta / dAd;
     if (blockIdx.x == 0 && threadIdx.x == 0) sc->dAd = dAd, sc->alpha = alpha, sc->delta_prev = delta;
     T s1 = 0;
-    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t) gridDim.x * blockDim.x) {
-        const T t = alpha * d[i];
-        x[i] = x[i] + t;
+    auto one = [&](int64_t i, T x_, T d_, T a_, T r_) {
+        const T t = alpha * d_;
+        x[i] = x_ + t;
         if (reset) {
-            r[i] = b[i];
+            r[i] = a_;
         } else {
-            const T u = alpha * Ad[i];
-            const T rn = r[i] - u;
+            const T u = alpha * a_;
+            const T rn = r_ - u;
             r[i] = rn;
             s1 += rn * rn;
         }
+    };
+#pragma unroll
+    for (int e = 0; e < CG_PRE; ++e) {
+        const int64_t i = i0 + e * st;
+        if (i < m) one(i, xv[e], dv[e], av[e], rv[e]);
     }
+    for (int64_t i = i0 + CG_PRE * st; i < m; i += st) one(i, x[i], d[i], reset ? b[i] : Ad[i], reset ? T(0) : r[i]);
     if (!reset) store_partials(s1, T(0), red, prr);
 }
 
 template <typename T>
 __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, const T *__restrict__ r,
                                                           const T *__restrict__ q, const T *__restrict__ prr, int init,
-                                                          int64_t run, double *trace, int64_t trace_cap, int64_t m,
+                                                          double *trace, int64_t trace_cap, int64_t m,
                                                           T *__restrict__ psum, cg_scalars<T> *sc) {
     if (sc->converged) return;
     __shared__ T red[CG_NT / 64], bc[1];
+    const int64_t i0 = (int64_t) blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t) gridDim.x * blockDim.x;
+    T dv[CG_PRE], rv[CG_PRE], qv[CG_PRE];
+#pragma unroll
+    for (int e = 0; e < CG_PRE; ++e) {
+        const int64_t i = i0 + e * st;
+        if (i < m) dv[e] = init ? T(0) : d[i], rv[e] = r[i], qv[e] = q[i];
+    }
     T beta = 0;
     if (!init) {
         T rr, unused;
@@ -249,6 +296,8 @@ __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, c
         const bool conv = rr <= sc->eps2delta0;
         beta = rr / sc->delta_prev;
         if (blockIdx.x == 0 && threadIdx.x == 0) {  // FIN_DELTA of dot_final_kernel
+            // the iteration index lives on the device (captured iteration blocks are position-free)
+            const int64_t run = sc->iters;
             sc->delta = rr;
             sc->iters = run + 1;
             if (trace && run + 1 < trace_cap) trace[run + 1] = (double) rr;
@@ -258,28 +307,34 @@ __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, c
         if (conv) return;  // the same decision in every block
     }
     T s1 = 0, s2 = 0;
-    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t) gridDim.x * blockDim.x) {
+    auto one = [&](int64_t i, T d_, T r_, T q_) {
         T dn;
         if (init) {
-            dn = r[i];
+            dn = r_;
         } else {
-            const T t = beta * d[i];
-            dn = t + r[i];
+            const T t = beta * d_;
+            dn = t + r_;
         }
         d[i] = dn;
         s1 += dn;
-        s2 += q[i] * dn;
+        s2 += q_ * dn;
+    };
+#pragma unroll
+    for (int e = 0; e < CG_PRE; ++e) {
+        const int64_t i = i0 + e * st;
+        if (i < m) one(i, dv[e], rv[e], qv[e]);
     }
+    for (int64_t i = i0 + CG_PRE * st; i < m; i += st) one(i, init ? T(0) : d[i], r[i], q[i]);
     store_partials(s1, s2, red, psum);
 }
 
 }  // namespace
 
 template <typename T>
-void launch_cg_fin_dad(const T *raw, const T *q, const T *d, const T *psum, T QA_cost, T cost_inv, int raw_only,
-                       int64_t m, T *Ad, T *pdad, cg_scalars<T> *sc, hipStream_t s) {
-    hipLaunchKernelGGL(cg_fin_dad_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, raw, q, d, psum, QA_cost, cost_inv,
-                       raw_only, m, Ad, pdad, sc);
+void launch_cg_fin_dad(const T *raw, const T *slabs, int64_t P, const T *q, const T *d, const T *psum, T QA_cost,
+                       T cost_inv, int raw_only, int64_t m, T *Ad, T *pdad, cg_scalars<T> *sc, hipStream_t s) {
+    hipLaunchKernelGGL(cg_fin_dad_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, raw, slabs, P, q, d, psum, QA_cost,
+                       cost_inv, raw_only, m, Ad, pdad, sc);
     MI_LAUNCH_CHECK();
 }
 
@@ -291,9 +346,9 @@ void launch_cg_upd_rr(T *x, T *r, const T *d, const T *Ad, const T *b, int reset
 }
 
 template <typename T>
-void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int init, int64_t run, double *trace,
+void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int init, double *trace,
                         int64_t trace_cap, int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s) {
-    hipLaunchKernelGGL(cg_dir_sums_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, d, r, q, prr, init, run, trace,
+    hipLaunchKernelGGL(cg_dir_sums_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, d, r, q, prr, init, trace,
                        trace_cap, m, psum, sc);
     MI_LAUNCH_CHECK();
 }
@@ -353,12 +408,12 @@ void launch_cg_direction(T *d, const T *r, int64_t m, const cg_scalars<T> *sc, h
     template void launch_cg_update<T>(T *, T *, const T *, const T *, const T *, int, int64_t,                    \
                                       const cg_scalars<T> *, hipStream_t);                                        \
     template void launch_cg_direction<T>(T *, const T *, int64_t, const cg_scalars<T> *, hipStream_t);             \
-    template void launch_cg_fin_dad<T>(const T *, const T *, const T *, const T *, T, T, int, int64_t, T *, T *,    \
-                                       cg_scalars<T> *, hipStream_t);                                               \
+    template void launch_cg_fin_dad<T>(const T *, const T *, int64_t, const T *, const T *, const T *, T, T, int,  \
+                                       int64_t, T *, T *, cg_scalars<T> *, hipStream_t);                                               \
     template void launch_cg_upd_rr<T>(T *, T *, const T *, const T *, const T *, int, const T *, int64_t, T *,      \
                                       cg_scalars<T> *, hipStream_t);                                                \
-    template void launch_cg_dir_sums<T>(T *, const T *, const T *, const T *, int, int64_t, double *, int64_t,      \
-                                        int64_t, T *, cg_scalars<T> *, hipStream_t);
+    template void launch_cg_dir_sums<T>(T *, const T *, const T *, const T *, int, double *, int64_t, int64_t,      \
+                                        T *, cg_scalars<T> *, hipStream_t);
 INST(float)
 INST(double)
 #undef INST

@@ -126,7 +126,10 @@ int plssvm_mi_partition(int64_t m, int rank, int world_size, int64_t *out4) {
 
 int plssvm_mi_set_cost(plssvm_mi_ctx *ctx, double cost) {
     if (!ctx || !(cost > 0)) return PLSSVM_MI_ERR_ARG;
-    return ctx->call([&](auto &e) { e.cost = (decltype(e.cost)) cost; });
+    return ctx->call([&](auto &e) {
+        e.cost = (decltype(e.cost)) cost;
+        e.graph_reset();  // a captured CG block holds 1/C
+    });
 }
 
 int plssvm_mi_set_qa_cost(plssvm_mi_ctx *ctx, double qa) {
@@ -135,6 +138,7 @@ int plssvm_mi_set_qa_cost(plssvm_mi_ctx *ctx, double qa) {
         e.need_data();
         e.QA_cost = (decltype(e.QA_cost)) qa;
         e.have_q = true;
+        e.graph_reset();
     });
 }
 

@@ -5,6 +5,7 @@
 // run_device_kernel (:353-363) -> device_reduction (:366-386).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "engine.hpp"
@@ -87,6 +88,7 @@ template <typename T>
 engine<T>::~engine() {
     (void) hipSetDevice(device);
     if (stream) (void) hipStreamSynchronize(stream);
+    graph_reset();
     if (comm) (void) ncclCommDestroy(comm);
     if (blas) (void) rocblas_destroy_handle(blas);
     XT.reset();
@@ -244,6 +246,7 @@ void engine<T>::finish_setup() {
     have_data = true;
     have_q = false;
     cg_active = false;
+    graph_reset();
 }
 
 template <typename T>
@@ -355,6 +358,7 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
     MI_HIP_CHECK(hipMemcpyAsync(sc.get(), &init, sizeof(init), hipMemcpyHostToDevice, stream));
     trace_cap = std::max<int64_t>(trace_len, 1);
     if (trace.size() < trace_cap) trace.alloc(trace_cap, stream);
+    graph_reset();  // QA_cost, trace and the vectors' contents may differ from the captured solve
     if (m > 0) MI_HIP_CHECK(hipMemcpyAsync(b.get(), b_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
     // x = 1; r = b; r -= Q~x   (csvm.cpp:85-90)
     launch_cg_init<T>(b.get(), m, x.get(), r.get(), stream);
@@ -363,9 +367,12 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
     launch_dot2<T>(r.get(), r.get(), nullptr, nullptr, m, red.get(), nullptr, stream);
     launch_dot_final<T>(red.get(), sc.get(), FIN_DELTA0, 0, trace.get(), trace_cap, nullptr, stream);
     // d = r, with sum d / sum q d for the first Q~d
-    launch_cg_dir_sums<T>(dv.get(), r.get(), q.get(), nullptr, 1, 0, nullptr, 0, m, cgp.get(), sc.get(), stream);
+    launch_cg_dir_sums<T>(dv.get(), r.get(), q.get(), nullptr, 1, nullptr, 0, m, cgp.get(), sc.get(), stream);
     run = 0;
     cg_active = true;
+    // a solve that can reach a whole block captures it now (capture launches nothing; the
+    // instantiation stays out of the iterations' time)
+    if (trace_len > CG_RESET && graph_usable()) graph_capture();
     if (delta0_out) {
         cg_scalars<T> h{};
         MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));
@@ -374,28 +381,99 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
     }
 }
 
+// one CG iteration (reset: the every-50th recomputation r = b - Q~x), all launches on the engine stream
+template <typename T>
+void engine<T>::cg_iter(int reset) {
+    const cg_scalars<T> *st = sc.get();
+    T *psum = cgp.get(), *pdad = psum + 2 * RED_BLOCKS, *prr = psum + 4 * RED_BLOCKS;
+    const int raw_only = (sim_world > 0 && sim_rank != 0) ? 1 : 0;
+    // Ad = Q~ d (:111-113); alpha = delta / (d . Ad) (:116) in the next kernel
+    const T *slabs = nullptr;
+    int64_t P = 0;
+    if (sparse && factored() && world == 1 && sim_world == 0 && csr.spmv_csr.P > 1) {
+        // one GPU, factored sparse linear: the CSR pass's panel slabs are summed by cg_fin_dad
+        spmv_pass_csc(dv.get(), st);
+        launch_panel_spmv<T>(csr.spmv_csr, w.get(), d, raw.get(), st, stream, 1, 0, false);
+        slabs = csr.spmv_csr.partial.get();
+        P = csr.spmv_csr.P;
+    } else {
+        kp_raw(dv.get(), st);
+    }
+    launch_cg_fin_dad<T>(raw.get(), slabs, P, q.get(), dv.get(), psum, QA_cost, cost_inv(), raw_only, m, Ad.get(),
+                         pdad, sc.get(), stream);
+    // x += alpha d; r = b - Q~x every 50th iteration, else r -= alpha Ad   (:119-132)
+    launch_cg_upd_rr<T>(x.get(), r.get(), dv.get(), Ad.get(), b.get(), reset, pdad, m, prr, sc.get(), stream);
+    if (reset) {
+        kp_device(x.get(), r.get(), T(-1), false, st);
+        launch_dot2<T>(r.get(), r.get(), nullptr, nullptr, m, prr, st, stream);
+    }
+    // delta = r.r ; stop test ; beta (:135-146); d = beta d + r (:149-151), with sum d / sum q d
+    launch_cg_dir_sums<T>(dv.get(), r.get(), q.get(), prr, 0, trace.get(), trace_cap, m, psum, sc.get(), stream);
+}
+
+// Iteration blocks of CG_RESET (the reset period) starting at a multiple of it are replayed from one
+// captured hipGraph: the launches of a block depend only on the engine's buffers (the iteration
+// index lives on the device), so one capture serves every block of a solve. Host-staged groups
+// synchronise inside the exchange and are never captured; RCCL groups are captured only with
+// PLSSVM_MI_GRAPH=2 (the collectives then run as graph nodes); PLSSVM_MI_GRAPH=0 disables graphs.
+template <typename T>
+bool engine<T>::graph_usable() const {
+    static const int mode = [] {
+        const char *e = std::getenv("PLSSVM_MI_GRAPH");
+        return e == nullptr ? 1 : std::atoi(e);
+    }();
+    if (mode == 0 || xchg != nullptr || m <= 0) return false;
+    return comm == nullptr || mode == 2;
+}
+
+template <typename T>
+void engine<T>::graph_reset() {
+    if (cg_graph != nullptr) {
+        (void) hipGraphExecDestroy(cg_graph);
+        cg_graph = nullptr;
+    }
+}
+
+template <typename T>
+void engine<T>::graph_capture() {
+    if (cg_graph == nullptr) {
+        hipGraph_t g = nullptr;
+        MI_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+        try {
+            for (int k = 0; k < CG_RESET; ++k) cg_iter(k == CG_RESET - 1 ? 1 : 0);
+        } catch (...) {
+            (void) hipStreamEndCapture(stream, &g);
+            if (g) (void) hipGraphDestroy(g);
+            throw;
+        }
+        MI_HIP_CHECK(hipStreamEndCapture(stream, &g));
+        const hipError_t e = hipGraphInstantiate(&cg_graph, g, nullptr, nullptr, 0);
+        (void) hipGraphDestroy(g);
+        MI_HIP_CHECK(e);
+    }
+}
+
+template <typename T>
+void engine<T>::graph_block() {
+    graph_capture();
+    MI_HIP_CHECK(hipGraphLaunch(cg_graph, stream));
+}
+
 template <typename T>
 void engine<T>::cg_step(int64_t nsteps, bool &converged, int64_t &iters) {
     if (!cg_active) throw mi_error(-6, "cg_step without cg_begin");
     MI_HIP_CHECK(hipSetDevice(device));
-    const cg_scalars<T> *st = sc.get();
-    T *psum = cgp.get(), *pdad = psum + 2 * RED_BLOCKS, *prr = psum + 4 * RED_BLOCKS;
-    const int raw_only = (sim_world > 0 && sim_rank != 0) ? 1 : 0;
-    for (int64_t s = 0; s < nsteps; ++s, ++run) {  // m == 0: the kernels see no elements, converge at once
-        // Ad = Q~ d (:111-113); alpha = delta / (d . Ad) (:116) in the next kernel
-        kp_raw(dv.get(), st);
-        launch_cg_fin_dad<T>(raw.get(), q.get(), dv.get(), psum, QA_cost, cost_inv(), raw_only, m, Ad.get(), pdad,
-                             sc.get(), stream);
-        // x += alpha d; r = b - Q~x every 50th iteration, else r -= alpha Ad   (:119-132)
-        const int reset = (run % 50 == 49) ? 1 : 0;
-        launch_cg_upd_rr<T>(x.get(), r.get(), dv.get(), Ad.get(), b.get(), reset, pdad, m, prr, sc.get(), stream);
-        if (reset) {
-            kp_device(x.get(), r.get(), T(-1), false, st);
-            launch_dot2<T>(r.get(), r.get(), nullptr, nullptr, m, prr, st, stream);
+    // m == 0: the kernels see no elements, converge at once
+    for (int64_t s = 0; s < nsteps;) {
+        if (run % CG_RESET == 0 && nsteps - s >= CG_RESET && graph_usable()) {
+            graph_block();
+            s += CG_RESET;
+            run += CG_RESET;
+        } else {
+            cg_iter(run % CG_RESET == CG_RESET - 1 ? 1 : 0);
+            ++s;
+            ++run;
         }
-        // delta = r.r ; stop test ; beta (:135-146); d = beta d + r (:149-151), with sum d / sum q d
-        launch_cg_dir_sums<T>(dv.get(), r.get(), q.get(), prr, 0, run, trace.get(), trace_cap, m, psum, sc.get(),
-                              stream);
     }
     cg_scalars<T> h{};
     MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));
@@ -428,12 +506,14 @@ void engine<T>::solve_cg(const T *b_host, const T *q_host, int64_t imax, T eps, 
     cg_begin(b_host, q_host, eps, false, nullptr, imax + 1);
     bool conv = false;
     int64_t it = 0;
-    // batches of iterations between host polls; kernels after convergence exit at entry
+    // batches of iterations between host polls (kernels after convergence exit at entry): 4, 8, 16,
+    // then up to the first reset, then whole CG_RESET blocks (one captured graph each)
     int64_t batch = 4;
     while (!conv && run < imax) {
-        const int64_t ns = std::min<int64_t>(batch, imax - run);
+        const int64_t ns = std::min<int64_t>(run < CG_RESET ? std::min<int64_t>(batch, CG_RESET - run) : CG_RESET,
+                                             imax - run);
         cg_step(ns, conv, it);
-        batch = std::min<int64_t>(batch * 2, 64);
+        batch *= 2;
     }
     cg_result(x_out, trace_out, imax + 1, iters);
 }

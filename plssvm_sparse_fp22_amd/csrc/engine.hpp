@@ -66,6 +66,8 @@ struct engine : engine_base {
     bool have_q = false;
     int64_t run = 0;
     bool cg_active = false;
+    static constexpr int CG_RESET = 50;  // r = b - Q~x every 50th iteration (csvm.cpp:119-132)
+    hipGraphExec_t cg_graph = nullptr;   // one captured block of CG_RESET iterations (graph_block)
 
     engine(int kernel_, int degree_, double gamma_, double coef0_, double cost_, int device_);
     ~engine() override;
@@ -91,6 +93,11 @@ struct engine : engine_base {
     void kp_host(const T *q_host, const T *p, T *ret_host, T add);
 
     void cg_begin(const T *b_host, const T *q_host, T eps, bool force, double *delta0_out, int64_t trace_len);
+    void cg_iter(int reset);
+    bool graph_usable() const;
+    void graph_capture();
+    void graph_block();
+    void graph_reset();
     void cg_step(int64_t nsteps, bool &converged, int64_t &iters);
     void cg_result(T *x_out, double *trace_out, int64_t trace_len, int64_t *iters);
     void solve_cg(const T *b, const T *q_host, int64_t imax, T eps, T *x_out, double *trace_out, int64_t *iters);

@@ -103,19 +103,19 @@ void launch_cg_direction(T *d, const T *r, int64_t m, const cg_scalars<T> *sc, h
 // between them; dots keep dot2_kernel's grid and order, so the results are bitwise those of the
 // unfused sequence.
 // Ad = Q~ d from raw (kp_finalize arithmetic, add = 1, overwrite), sum d / sum q d from psum;
-// d.Ad partials -> pdad
+// d.Ad partials -> pdad. slabs != null: raw = the P panel slabs [P][m] of an unreduced SpMV pass.
 template <typename T>
-void launch_cg_fin_dad(const T *raw, const T *q, const T *d, const T *psum, T QA_cost, T cost_inv, int raw_only,
-                       int64_t m, T *Ad, T *pdad, cg_scalars<T> *sc, hipStream_t s);
+void launch_cg_fin_dad(const T *raw, const T *slabs, int64_t P, const T *q, const T *d, const T *psum, T QA_cost,
+                       T cost_inv, int raw_only, int64_t m, T *Ad, T *pdad, cg_scalars<T> *sc, hipStream_t s);
 // alpha = delta / d.Ad (pdad); x += alpha d; r -= alpha Ad and r.r partials -> prr (reset: r = b)
 template <typename T>
 void launch_cg_upd_rr(T *x, T *r, const T *d, const T *Ad, const T *b, int reset, const T *pdad, int64_t m, T *prr,
                       cg_scalars<T> *sc, hipStream_t s);
 // delta = r.r (prr), stop test, beta; d = beta d + r (init: d = r, scalars untouched);
-// sum d / sum q d partials -> psum
+// sum d / sum q d partials -> psum. The iteration index is sc->iters (trace[iters + 1] = delta, iters += 1).
 template <typename T>
-void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int init, int64_t run, double *trace,
-                        int64_t trace_cap, int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s);
+void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int init, double *trace, int64_t trace_cap,
+                        int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s);
 
 // ---- sparse (CSR / FP22) ------------------------------------------------------------------------
 // declared in sparse.hpp

@@ -628,7 +628,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         csr.csc_r0 = local ? r0 : 0;
         csr.csc_r1 = local ? r1 : m;
         const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
-        constexpr int64_t blocks = 512;  // two 1024-thread workgroups per CU
+        const int64_t blocks = sell_target_blocks();
         build_spmv_plan<T>(
             csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22,
             [&](auto emit) {
@@ -723,7 +723,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             // the two SELL passes of the kernel expansion (the factored linear path's plans, with K channels):
             // moments over the CSC of all rows, the Horner pass over this rank's CSR rows
             const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
-            constexpr int64_t blocks = 512;
+            const int64_t blocks = sell_target_blocks();
             csr.csc_r0 = 0;
             csr.csc_r1 = m;
             build_spmv_plan<T>(

@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <numeric>
 #include <vector>
 
@@ -38,16 +39,26 @@ namespace plssvm_mi {
 constexpr int SELL_NT = 1024;  // 16 waves per workgroup
 constexpr int SELL_WAVES = SELL_NT / 64;
 #ifndef PLSSVM_MI_SELL_XBYTES
-#define PLSSVM_MI_SELL_XBYTES 65536
+#define PLSSVM_MI_SELL_XBYTES 163840
 #endif
-constexpr int SELL_XBYTES = PLSSVM_MI_SELL_XBYTES;  // LDS panel of the gathered vector (2 workgroups / CU)
+constexpr int SELL_XBYTES = PLSSVM_MI_SELL_XBYTES;  // LDS panel of the gathered vector (all of a CU's LDS)
 constexpr int SELL_SIGMA = 4096;    // sorting window (segments)
 #ifndef PLSSVM_MI_SELL_UNROLL
-#define PLSSVM_MI_SELL_UNROLL 8
+#define PLSSVM_MI_SELL_UNROLL 4
 #endif
 constexpr int SELL_UNROLL = PLSSVM_MI_SELL_UNROLL;  // entries per lane in flight per step
 template <typename T>
 constexpr int sell_width() { return SELL_XBYTES / (int) sizeof(T); }
+// workgroups per pass: equal-cost chunk ranges, a multiple of the 256 CUs (one resident workgroup per
+// CU with a full-LDS panel); PLSSVM_MI_SELL_BLOCKS overrides (measurements)
+inline int64_t sell_target_blocks() {
+    static const int64_t nb = [] {
+        const char *e = std::getenv("PLSSVM_MI_SELL_BLOCKS");
+        const long v = e ? std::atol(e) : 0;
+        return v > 0 ? (int64_t) v : (int64_t) 256;
+    }();
+    return nb;
+}
 
 struct sell_chunk {
     int64_t off;    // first entry (entry j of slot l at off + 64 j + l)
@@ -68,6 +79,7 @@ template <typename T>
 struct spmv_plan {
     bool ldsx = false;
     int64_t P = 0, nseg = 0, W = 0, nnz = 0, slots_total = 0, entries = 0, nchunks = 0, nblocks = 0;
+    int64_t nchp = 0;  // chunks per panel (panel q's chunks are [q nchp, (q + 1) nchp))
     dev_buf<sell_chunk> chunks;
     dev_buf<int32_t> perm;    // [nchunks * 64] slot -> segment (-1: padding slot)
     dev_buf<uint16_t> idx16;  // ldsx: panel-local index
@@ -115,81 +127,98 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
                                                             const typename sell_idx<LDSX>::type *__restrict__ idx,
                                                             vals_t<T> val, const int32_t *__restrict__ bchunk,
                                                             const T *__restrict__ x, int64_t xn, int64_t W,
-                                                            int64_t nseg, T *__restrict__ out,
+                                                            int64_t nseg, int nchp, T *__restrict__ out,
                                                             const cg_scalars<T> *__restrict__ status) {
     constexpr int XC = MODE == 2 ? KC : 1;   // channels of the gathered vector
     constexpr int OC = MODE == 1 ? KC : 1;   // outputs per segment
     constexpr int XW = LDSX ? sell_width<T>() : 1;
+    using idx_t = typename sell_idx<LDSX>::type;
     __shared__ T xs[XW];
     if (status != nullptr && status->converged) return;
     const int tid = threadIdx.x, lane = tid & 63;
     const int c0 = bchunk[blockIdx.x], c1 = bchunk[blockIdx.x + 1];
-    if (c0 >= c1) return;
-    const int q = chunks[c0].q;
-    T *o = out + (int64_t) q * nseg * OC;
-    const T *xg = x + (int64_t) q * W * XC;  // LDSX: panel q gathers x[q W + local]; otherwise W = 0
-    if constexpr (LDSX) {
-        const int xl = (int) min((int64_t) W, xn - (int64_t) q * W) * XC;
-        constexpr int XPER = XW / SELL_NT;
-        T t[XPER];
-#pragma unroll
-        for (int u = 0; u < XPER; ++u) {
-            const int k = tid + u * SELL_NT;
-            t[u] = k < xl ? xg[k] : T(0);
-        }
-#pragma unroll
-        for (int u = 0; u < XPER; ++u) xs[tid + u * SELL_NT] = t[u];
-        __syncthreads();
-    }
-    auto gx = [&](int64_t c) -> T {
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    auto gx = [&](const T *xg, int64_t c) -> T {
         if constexpr (LDSX) return xs[c];
         else return xg[c];
     };
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    for (int c = c0 + wave; c < c1; c += SELL_WAVES) {
-        const sell_chunk ch = chunks[c];
-        const int slot_seg = perm[(int64_t) c * 64 + lane];
-        const int64_t base = ch.off + lane;
-        // steps of SELL_UNROLL entries; a step past the width re-reads the slot's last entry (same
-        // cache line) and masks it, so every step issues all of its loads at once
-        const int last = max(ch.width - 1, 0);
-        T acc[OC];
+    // the block's chunk range may cross panels (blocks are cut by cost over the whole panel-major chunk
+    // sequence): one LDS fill per panel, all waves done with the previous panel first
+    for (int cb = c0; cb < c1;) {
+        const int q = chunks[cb].q;
+        const int ce = min(c1, (q + 1) * nchp);  // chunks of panel q are [q nchp, (q + 1) nchp)
+        T *o = out + (int64_t) q * nseg * OC;
+        const T *xg = x + (int64_t) q * W * XC;  // LDSX: panel q gathers x[q W + local]; otherwise W = 0
+        if constexpr (LDSX) {
+            if (cb != c0) __syncthreads();
+            const int xl = (int) min((int64_t) W, xn - (int64_t) q * W) * XC;
+            // 16-byte loads and LDS stores (XW is a multiple of 16 B per thread); a misaligned panel
+            // start (the CSC pass of a group rank gathers p + r0) or the ragged last panel go per element
+            using V = __attribute__((ext_vector_type(4))) float;
+            constexpr int EV = 16 / (int) sizeof(T);  // elements per vector
+            constexpr int VPER = XW / EV / SELL_NT;
+            static_assert(VPER * EV * SELL_NT == XW, "panel width must be a multiple of 16 B per thread");
+            if (xl == XW && (reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
+                V t[VPER];
 #pragma unroll
-        for (int k = 0; k < OC; ++k) acc[k] = T(0);
-        for (int j = 0; j < ch.width; j += SELL_UNROLL) {
-            typename sell_idx<LDSX>::type ci[SELL_UNROLL];
-            T vi[SELL_UNROLL];
+                for (int u = 0; u < VPER; ++u) t[u] = reinterpret_cast<const V *>(xg)[tid + u * SELL_NT];
 #pragma unroll
-            for (int u = 0; u < SELL_UNROLL; ++u) {
-                const int64_t k = base + (int64_t) min(j + u, last) * 64;
-                ci[u] = __builtin_nontemporal_load(idx + k);
-                vi[u] = sell_val<T, F22>(val, k);
-            }
-#pragma unroll
-            for (int u = 0; u < SELL_UNROLL; ++u) {
-                const T v = j + u < ch.width ? vi[u] : T(0);
-                if constexpr (MODE == 0) {
-                    acc[0] = fma(v, gx((int64_t) ci[u]), acc[0]);
-                } else if constexpr (MODE == 1) {
-                    T t = v * gx((int64_t) ci[u]);
-#pragma unroll
-                    for (int k = 0; k < KC; ++k) {
-                        acc[k] += t;
-                        t *= v;
-                    }
-                } else {
-                    const int64_t cb = (int64_t) ci[u] * KC;
-                    T h = gx(cb + KC - 1);
-#pragma unroll
-                    for (int k = KC - 2; k >= 0; --k) h = fma(h, v, gx(cb + k));
-                    acc[0] = fma(h, v, acc[0]);
+                for (int u = 0; u < VPER; ++u) reinterpret_cast<V *>(xs)[tid + u * SELL_NT] = t[u];
+            } else {
+                constexpr int XPER = XW / SELL_NT;
+                for (int u = 0; u < XPER; ++u) {
+                    const int k = tid + u * SELL_NT;
+                    xs[k] = k < xl ? xg[k] : T(0);
                 }
             }
+            __syncthreads();
         }
-        if (slot_seg >= 0) {
+        for (int c = cb + wave; c < ce; c += SELL_WAVES) {
+            const sell_chunk ch = chunks[c];
+            const int seg = perm[(int64_t) c * 64 + lane];
+            const int64_t base = ch.off + lane;
+            // steps of SELL_UNROLL entries; a step past the width re-reads the slot's last entry (same
+            // cache line) and masks it, so every step issues all of its loads at once
+            const int last = max(ch.width - 1, 0);
+            T acc[OC];
 #pragma unroll
-            for (int k = 0; k < OC; ++k) o[(int64_t) k * nseg + slot_seg] = acc[k];
+            for (int k = 0; k < OC; ++k) acc[k] = T(0);
+            for (int j = 0; j < ch.width; j += SELL_UNROLL) {
+                idx_t ci[SELL_UNROLL];
+                T vi[SELL_UNROLL];
+#pragma unroll
+                for (int u = 0; u < SELL_UNROLL; ++u) {
+                    const int64_t k = base + (int64_t) min(j + u, last) * 64;
+                    ci[u] = __builtin_nontemporal_load(idx + k);
+                    vi[u] = sell_val<T, F22>(val, k);
+                }
+#pragma unroll
+                for (int u = 0; u < SELL_UNROLL; ++u) {
+                    const T v = j + u < ch.width ? vi[u] : T(0);
+                    if constexpr (MODE == 0) {
+                        acc[0] = fma(v, gx(xg, (int64_t) ci[u]), acc[0]);
+                    } else if constexpr (MODE == 1) {
+                        T t = v * gx(xg, (int64_t) ci[u]);
+#pragma unroll
+                        for (int k = 0; k < KC; ++k) {
+                            acc[k] += t;
+                            t *= v;
+                        }
+                    } else {
+                        const int64_t cx = (int64_t) ci[u] * KC;
+                        T h = gx(xg, cx + KC - 1);
+#pragma unroll
+                        for (int k = KC - 2; k >= 0; --k) h = fma(h, v, gx(xg, cx + k));
+                        acc[0] = fma(h, v, acc[0]);
+                    }
+                }
+            }
+            if (seg >= 0) {
+#pragma unroll
+                for (int k = 0; k < OC; ++k) o[(int64_t) k * nseg + seg] = acc[k];
+            }
         }
+        cb = ce;
     }
 }
 
@@ -240,18 +269,20 @@ inline void launch_panel_spmv_t(const spmv_plan<T> &pl, const T *x, int64_t xn, 
     if (pl.ldsx) {
         auto k = f22 ? sell_spmv_kernel<T, true, true, KC, MODE> : sell_spmv_kernel<T, true, false, KC, MODE>;
         hipLaunchKernelGGL(k, grid, block, 0, stream, pl.chunks.get(), pl.perm.get(), pl.idx16.get(), pl.vals(),
-                           pl.bchunk.get(), x, xn, pl.W, pl.nseg, dst, status);
+                           pl.bchunk.get(), x, xn, pl.W, pl.nseg, (int) pl.nchp, dst, status);
     } else {
         auto k = f22 ? sell_spmv_kernel<T, false, true, KC, MODE> : sell_spmv_kernel<T, false, false, KC, MODE>;
         hipLaunchKernelGGL(k, grid, block, 0, stream, pl.chunks.get(), pl.perm.get(), pl.idx32.get(), pl.vals(),
-                           pl.bchunk.get(), x, xn, (int64_t) 0, pl.nseg, dst, status);
+                           pl.bchunk.get(), x, xn, (int64_t) 0, pl.nseg, (int) pl.nchp, dst, status);
     }
     MI_LAUNCH_CHECK();
 }
 
+// reduce = false (mode 0 only): a multi-panel pass leaves its P partial slabs in pl.partial for the
+// consumer to sum in panel order (cg_fin_dad_kernel), out is not written
 template <typename T>
 inline void launch_panel_spmv(const spmv_plan<T> &pl, const T *x, int64_t xn, T *out, const cg_scalars<T> *status,
-                              hipStream_t stream, int kc = 1, int mode = 0) {
+                              hipStream_t stream, int kc = 1, int mode = 0, bool reduce = true) {
     if (pl.nseg <= 0 || pl.nblocks <= 0) return;
     if (mode == 0) {
         launch_panel_spmv_t<T, 1, 0>(pl, x, xn, out, status, stream);
@@ -270,7 +301,7 @@ inline void launch_panel_spmv(const spmv_plan<T> &pl, const T *x, int64_t xn, T 
             default: launch_panel_spmv_t<T, 16, 2>(pl, x, xn, out, status, stream);
         }
     }
-    if (pl.P > 1) {
+    if (pl.P > 1 && reduce) {
         const int64_t ns = pl.nseg * (mode == 1 ? kc : 1);
         const int split = pl.P >= 16 ? 1 : 0;
         hipLaunchKernelGGL(panel_reduce_kernel<T>, dim3((unsigned) ceil_div(ns, split ? 64 : 256)), dim3(256), 0,
@@ -338,6 +369,7 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
     }
     pl.entries = off;
     pl.nchunks = (int64_t) chunks.size();
+    pl.nchp = nch_per_panel;
     pl.slots_total = P * slots_per_panel;
     // fill (zero padding: index 0, value 0 contributes exactly 0) plus a 64-entry zero tail
     const int64_t cap = off + 64;
@@ -364,30 +396,24 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
             vr[t] = (T) v;
         }
     });
-    // blocks: ~target_blocks, each a contiguous chunk range of one panel, balanced by cost
-    // (entries + a per-chunk charge for its descriptor, slot map and output)
+    // blocks: target_blocks contiguous chunk ranges of equal cost (entries + a per-chunk charge for its
+    // descriptor, slot map and output) over the panel-major chunk sequence; a range may cross panels
     constexpr int64_t CHUNK_COST = 8 * 64;
     auto cost = [&](const sell_chunk &c) { return (int64_t) c.width * 64 + CHUNK_COST; };
     int64_t total_cost = 0;
     for (const auto &c : chunks) total_cost += cost(c);
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(target_blocks, (int64_t) chunks.size()));
     std::vector<int32_t> bchunk{ 0 };
-    for (int64_t q = 0; q < P; ++q) {
-        const int64_t i0 = q * nch_per_panel, i1 = i0 + nch_per_panel;
-        if (i1 == i0) continue;
-        int64_t cq = 0;
-        for (int64_t i = i0; i < i1; ++i) cq += cost(chunks[(size_t) i]);
-        int64_t nbq = std::max<int64_t>(1, (int64_t) std::llround((double) target_blocks * (double) cq /
-                                                                  (double) std::max<int64_t>(total_cost, 1)));
-        nbq = std::min(nbq, i1 - i0);
+    {
         int64_t acc = 0, k = 1;
-        for (int64_t i = i0; i < i1; ++i) {
+        for (int64_t i = 0; i < (int64_t) chunks.size(); ++i) {
             acc += cost(chunks[(size_t) i]);
-            if (i + 1 < i1 && k < nbq && acc * nbq >= k * cq) {
+            if (i + 1 < (int64_t) chunks.size() && k < nb && acc * nb >= k * total_cost) {
                 bchunk.push_back((int32_t) (i + 1));
                 ++k;
             }
         }
-        bchunk.push_back((int32_t) i1);
+        bchunk.push_back((int32_t) chunks.size());
     }
     pl.nblocks = (int64_t) bchunk.size() - 1;
     auto up = [&](auto &buf, const auto &vec) {

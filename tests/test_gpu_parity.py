@@ -175,6 +175,38 @@ def test_cg_trace_across_explicit_residual(oracle, kernel, cost, std):
     np.testing.assert_allclose(x, ref_x, rtol=1e-3, atol=1e-3 * np.abs(ref_x).max())
 
 
+@pytest.mark.parametrize("layout,kernel", [("dense", "rbf"), ("dense", "linear"), ("csr", "linear"),
+                                           ("csr", "rbf")])
+def test_cg_graph_blocks_bitwise_equal_to_launches(layout, kernel):
+    """cg_step(130) replays iterations [0, 50) and [50, 100) — each with its explicit-residual
+    iteration — from one captured hipGraph and runs [100, 130) as launches; 130 single cg_step(1)
+    calls never use the graph. Same kernels, same order: x and the delta trace are bitwise equal."""
+    if layout == "csr":
+        csr, y = datagen.sparse_csr(1500, 300, 12, seed=13, dtype=np.float64)
+    else:
+        X, y = datagen.blobs(700, 40, seed=13, cluster_std=3.0)
+    out = []
+    for batched in (True, False):
+        p = pm.Parameter(kernel, gamma=1.0 / (300 if layout == "csr" else 40), cost=100.0, real_type=np.float64)
+        if layout == "csr":
+            p.csr = csr
+        else:
+            p.data = np.ascontiguousarray(X)
+        with pm.CSVM(p) as svm:
+            svm.setup_data_on_device()
+            svm.generate_q()
+            svm.cg_begin((y[:-1] - y[-1]).astype(np.float64), eps=1e-300)
+            if batched:
+                it, _ = svm.cg_step(130)
+            else:
+                for _ in range(130):
+                    it, _ = svm.cg_step(1)
+            out.append(svm.cg_result(131))
+    (xa, ta, ia), (xb, tb, ib) = out
+    assert ia == ib == 130
+    assert np.array_equal(xa, xb) and np.array_equal(ta, tb)
+
+
 @pytest.mark.parametrize("world", [2, 3, 8])
 @pytest.mark.parametrize("kernel,mode", [("rbf", "auto"), ("polynomial", "auto"), ("linear", "factored")])
 def test_simulated_ranks_sum_to_full_kp(oracle, world, kernel, mode):
