@@ -110,17 +110,62 @@ __constant__ double c_exp2_256[256] = {
     1.9571441241754002, 1.9624504802089273, 1.9677712232331759, 1.9731063922552343,
     1.978456026387951, 1.9838201648502194, 1.9891988469672663, 1.9945921121709402
 };
-constexpr double K256 = 369.3299304675746;  // 256 / ln 2
 
+// 32-entry variant (PLSSVM_MI_EXP_TAB = 32, not the default): 2^(i/32) is one 256-B LDS bank row, so its
+// table read is conflict-free for any index pattern, at the price of a degree-5 (or 6) polynomial
+// (Chebyshev fit on [-1/2, 1/2]: worst relative error of the double Horner evaluation 2.5e-16 /
+// 1.1e-16). Measured on config 2: 39.36 / 39.57 ms vs 39.07 ms for the 256-entry
+// table — the table read costs its issue and latency, not bank conflicts.
+#ifndef PLSSVM_MI_EXP_TAB
+#define PLSSVM_MI_EXP_TAB 256
+#endif
+#ifndef PLSSVM_MI_EXP_DEG
+#define PLSSVM_MI_EXP_DEG 5
+#endif
+__constant__ double c_exp2_32[32] = {
+    1.0, 1.0218971486541166, 1.0442737824274138, 1.0671404006768237, 1.0905077326652577, 1.1143867425958924,
+    1.1387886347566916, 1.1637248587775775, 1.189207115002721, 1.215247359980469, 1.241857812073484,
+    1.2690509571917332, 1.2968395546510096, 1.3252366431597413, 1.3542555469368927, 1.383909881963832,
+    1.4142135623730951, 1.4451808069770467, 1.4768261459394993, 1.5091644275934228, 1.5422108254079407,
+    1.5759808451078865, 1.6104903319492543, 1.645755478153965, 1.681792830507429, 1.718619298122478,
+    1.7562521603732995, 1.7947090750031072, 1.8340080864093424, 1.8741676341103, 1.9152065613971474,
+    1.9571441241754002
+};
+constexpr int EXP_TAB = PLSSVM_MI_EXP_TAB;
+constexpr double KEXP = EXP_TAB == 32 ? 46.16624130844683 : 369.3299304675746;  // EXP_TAB / ln 2
+
+#ifndef PLSSVM_MI_ABL_DENSE
+#define PLSSVM_MI_ABL_DENSE 0  // timing ablations only: 1 kv = y (no exp), 2 no table read, 3 no ldexp
+#endif
 __device__ __forceinline__ double exp_scaled_f64(double y, const double *tab) {
+    if constexpr (PLSSVM_MI_ABL_DENSE == 1) return y;
     const double jn = rint(y);
     const double r = y - jn;  // exact
-    double t = fma(2.239395190875157e-12, r, 3.3083026805413713e-09);  // (ln2/256)^k / k!, k = 4..1
-    t = fma(t, r, 3.6655655969101062e-06);
-    t = fma(t, r, 0.0027076061740622863);
-    const double pr = fma(t, r, 1.0);
+    double pr;
+    if constexpr (EXP_TAB == 32 && PLSSVM_MI_EXP_DEG == 6) {
+        double t = fma(1.4345708169159177e-13, r, 3.973729405781781e-11);
+        t = fma(t, r, 9.172562701758912e-09);
+        t = fma(t, r, 1.6938509724129055e-06);
+        t = fma(t, r, 0.0002345961982022468);
+        t = fma(t, r, 0.02166084939249829);
+        pr = fma(t, r, 1.0);
+    } else if constexpr (EXP_TAB == 32) {
+        double t = fma(3.9737266313166245e-11, r, 9.172616498159851e-09);
+        t = fma(t, r, 1.6938509724215757e-06);
+        t = fma(t, r, 0.0002345961981972034);
+        t = fma(t, r, 0.02166084939249829);
+        pr = fma(t, r, 1.0);
+    } else {
+        double t = fma(2.239395190875157e-12, r, 3.3083026805413713e-09);  // (ln2/256)^k / k!, k = 4..1
+        t = fma(t, r, 3.6655655969101062e-06);
+        t = fma(t, r, 0.0027076061740622863);
+        pr = fma(t, r, 1.0);
+    }
     const int j = (int) jn;  // saturates for huge |y|: the ldexp below then returns 0
-    return ldexp(tab[j & 255] * pr, j >> 8);
+    constexpr int SH = EXP_TAB == 32 ? 5 : 8;
+    if constexpr (PLSSVM_MI_ABL_DENSE == 2) return ldexp(pr, j >> SH);
+    if constexpr (PLSSVM_MI_ABL_DENSE == 3) return tab[j & (EXP_TAB - 1)] * pr;
+    return ldexp(tab[j & (EXP_TAB - 1)] * pr, j >> SH);
 }
 
 // 16 B per lane global -> LDS through a buffer descriptor on a wave-uniform base: the per-lane part is
@@ -159,7 +204,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
     constexpr int SMEM = OFF_PAN + (4 * PANEL > RED ? 4 * PANEL : RED);
     __shared__ __attribute__((aligned(16))) T smem[SMEM];
     constexpr bool FAST_EXP = (KERNEL == 2) && sizeof(T) == 8;
-    __shared__ double exp_tab[FAST_EXP ? 256 : 1];
+    __shared__ double exp_tab[FAST_EXP ? EXP_TAB : 1];
 
     if (status != nullptr && status->converged) return;
 
@@ -182,7 +227,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
     const T pin = p[pidx];
     const T nin = (KERNEL == 2) ? norms[pidx] : T(0);
     // fast fp64 RBF: the accumulators start at -n_j / 2 (column j = lane & 15 of every block), so they
-    // end at g_ij - n_j / 2 and y_ij = 2 g K256 (g_ij - n_j / 2) - g K256 n_i is one fma per element
+    // end at g_ij - n_j / 2 and y_ij = 2 g KEXP (g_ij - n_j / 2) - g KEXP n_i is one fma per element
     T acc0[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
@@ -223,7 +268,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
     smem[tid] = pin;
     smem[2 * KP_TILE + tid] = nin;
     if constexpr (FAST_EXP) {
-        exp_tab[tid] = c_exp2_256[tid];  // 256 threads; visible after the first K-loop barrier
+        if (tid < EXP_TAB) exp_tab[tid] = EXP_TAB == 32 ? c_exp2_32[tid] : c_exp2_256[tid];  // visible after the first K-loop barrier
     }
 
     const int64_t nk = d_pad / BK;
@@ -258,7 +303,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
         nj[nt] = (KERNEL == 2 && !FAST_EXP) ? nJ[jl] : T(0);
     }
     T cs[4] = { 0, 0, 0, 0 };
-    const T c2 = FAST_EXP ? T(2) * kf.gamma * T(K256) : T(0);
+    const T c2 = FAST_EXP ? T(2) * kf.gamma * T(KEXP) : T(0);
     // Each row has 32 partials (16 lanes x 2 column-half waves), each column 8 (4 lane groups x 2
     // row-half waves). They are parked in LDS and every thread then sums one half-row and one
     // half-column: ~20 adds per lane instead of a 4-level shuffle tree per row (64 adds + 128
@@ -272,7 +317,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
             const int il = wr * 64 + mt * 16 + M::row(lane, r);
             const T pi = pI[il];
             const T ni = nI[il];
-            const T ai = FAST_EXP ? -kf.gamma * T(K256) * ni : T(0);
+            const T ai = FAST_EXP ? -kf.gamma * T(KEXP) * ni : T(0);
             T s = 0;
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) {
