@@ -267,7 +267,8 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
     kernel, _, _, dtype, layout, _, _ = cfg
     m = n - 1
     s = ms_dom * 1e-3
-    if layout == "dense" and info["kp_mode"] == pm._abi.KP_PAIRWISE:
+    densified = info.get("sparse_algo") == pm._abi.SPARSE_DENSE  # sparse data on the dense MFMA tiles
+    if (layout == "dense" or densified) and info["kp_mode"] == pm._abi.KP_PAIRWISE:
         pairs = m * (m + 1) / 2 * info["tiles_local"] / max(1, info["tiles_total"])
         alg = 2.0 * d * pairs  # Gram-block FLOP of this rank's lower-triangle tiles (GEMM form)
         pk = PEAKS["f64" if dtype == np.float64 else "f32"]

@@ -73,15 +73,20 @@ extern "C" {
 /* K·p algorithm of the pairwise kernels (poly, rbf) on sparse data:
  *   0 = auto: the kernel expansion when it represents the kernel to rounding (poly degree <= 16; rbf
  *       in the factored form with a Taylor degree <= 16 for the data's max |2 g x_if x_jf|), else the
- *       Gram pattern;
+ *       Gram pattern; when the chosen structure's estimated size exceeds the device-memory budget
+ *       (85 % of the free memory; environment PLSSVM_MI_MEM_BUDGET = bytes overrides), or its build
+ *       runs out of memory, the densified path 3;
  *   1 = Gram pattern: every overlapping pair (j < i) with s_ij = x_i . x_j stored at setup, the kernel
  *       function re-evaluated on each per K·p (O(sum_f c_f^2) memory and traffic);
  *   2 = kernel expansion: per-feature column moments + the stored remainder of the pairs sharing two or
- *       more features (O(nnz + #multi-feature pairs)); fails with ERR_UNSUPPORTED when not eligible. */
+ *       more features (O(nnz + #multi-feature pairs)); fails with ERR_UNSUPPORTED when not eligible;
+ *   3 = densified: X densified on the device, the dense MFMA pairwise tiles (O(m d) memory, every pair
+ *       recomputed from the data on each K·p as in the reference); ERR_OOM when m x d does not fit. */
 #define PLSSVM_MI_OPT_SPARSE_ALGO 4
 #define PLSSVM_MI_SPARSE_AUTO 0
 #define PLSSVM_MI_SPARSE_PATTERN 1
 #define PLSSVM_MI_SPARSE_EXPANSION 2
+#define PLSSVM_MI_SPARSE_DENSE 3 /* densified on the device, MFMA pairwise tiles (every pair recomputed per K·p) */
 
 typedef struct plssvm_mi_ctx plssvm_mi_ctx;
 
@@ -229,7 +234,7 @@ typedef struct {
     int64_t spmv_bytes; /* sparse factored linear: HBM bytes both SpMV passes move per K·p (padded SELL
                            stream, slot maps, panel partials) */
     int rbf_small_args; /* sparse factored rbf: 1 = every 2 g |s_ij| is below the short Taylor form's bound */
-    int sparse_algo;    /* sparse poly/rbf: PLSSVM_MI_SPARSE_PATTERN | PLSSVM_MI_SPARSE_EXPANSION (0 otherwise) */
+    int sparse_algo;    /* sparse poly/rbf: PLSSVM_MI_SPARSE_PATTERN | _EXPANSION | _DENSE (0 otherwise) */
     int exp_terms;      /* kernel expansion: polynomial degree K of the per-feature pair function */
     int exp_waves;      /* kernel expansion: waves of the remainder stream */
     int64_t exp_chunks; /* kernel expansion: 8-slot chunks of the remainder stream (this rank's rows) */

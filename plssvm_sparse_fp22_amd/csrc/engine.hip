@@ -296,7 +296,7 @@ void engine<T>::kp_device(const T *p, T *out, T add, bool overwrite, const cg_sc
 template <typename T>
 void engine<T>::kp_raw(const T *p, const cg_scalars<T> *status) {
     if (m <= 0) return;
-    if (sparse) {
+    if (sparse_stored()) {
         sparse_kp_raw(p, status);
     } else if (factored()) {
         launch_gemv_t<T>(XT.get(), n_pad, d, sim_world > 0 ? 0 : r0, sim_world > 0 ? m : r1, p, w.get(), status, stream);
@@ -333,7 +333,8 @@ template <typename T>
 void engine<T>::kp_part(const T *p_host, T *out_host, int part) {
     need_data();
     if (part != 0 && part != 1) throw mi_error(-1, "unknown K·p part");
-    if (part == 1 && !(sparse && !factored())) throw mi_error(-5, "the overlap part exists for sparse poly/rbf only");
+    if (part == 1 && !(sparse_stored() && !factored()))
+        throw mi_error(-5, "the overlap part exists for the stored sparse poly/rbf paths only");
     MI_HIP_CHECK(hipSetDevice(device));
     cg_active = false;
     MI_HIP_CHECK(hipMemsetAsync(sc.get(), 0, sizeof(cg_scalars<T>), stream));
@@ -563,7 +564,7 @@ void engine<T>::time_kp(int reps, double *ms_kp, double *ms_dom) {
     // dominant kernel alone, same stream, same launches
     for (int it = 0; it < reps; ++it) {
         MI_HIP_CHECK(hipEventRecord(d0, stream));
-        if (sparse) {
+        if (sparse_stored()) {
             sparse_dominant(pv.get(), nullptr);
         } else if (factored()) {
             launch_gemv_n<T>(XT.get(), n_pad, d, r0, r1, w.get(), raw.get(), nullptr, stream);

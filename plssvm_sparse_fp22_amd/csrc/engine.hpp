@@ -107,6 +107,12 @@ struct engine : engine_base {
     // sparse paths (sparse.hip)
     void sparse_q();                                              // q, norms, e on CSR data
     void build_gram_blocks(const int64_t *cpos, int64_t max_inc);  // sparse Gram pattern (pairwise kernels)
+    int64_t sparse_mem_budget() const;                             // device bytes for stored sparse structures
+    int64_t estimate_expansion_bytes(const int64_t *rowptr, const int32_t *col, const std::vector<int64_t> &colptr,
+                                     const std::vector<int32_t> &crow, int64_t inc_total) const;
+    void release_sparse_structures();
+    void setup_sparse_dense();                                     // densified fallback (PLSSVM_MI_SPARSE_DENSE)
+    bool sparse_stored() const { return sparse && !csr.dense_on; } // K·p through the CSR structures
     bool expansion_eligible();                                    // expand.hip: K, coefficients; true if usable
     void build_expansion(const int64_t *cpos, int64_t max_inc);   // multi-overlap remainder H, diagonal
     void expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);

@@ -14,6 +14,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -712,39 +713,161 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                                         stream));
         int64_t max_inc = 0;
         for (int64_t I = csr.rb0; I < csr.rb1; ++I) max_inc = std::max(max_inc, inc_rb[I]);
-        // kernel expansion (expand.hip) when it represents the kernel to rounding, else the Gram pattern
+        // kernel expansion (expand.hip) when it represents the kernel to rounding, else the Gram pattern;
+        // either only within the device-memory budget, else the densified MFMA path
         csr.ex.umax = 2.0 * std::fabs((double) gamma) * amax;
         const bool fact_ok = kernel != 2 || std::fabs((double) gamma) * nmax <= (sizeof(T) == 8 ? 300.0 : 40.0);
-        const bool elig = fact_ok && expansion_eligible();
+        const bool elig = sparse_algo != 3 && fact_ok && expansion_eligible();
         if (sparse_algo == 2 && !elig)
             throw mi_error(-5, "the kernel expansion cannot represent this kernel on this data (Taylor degree > 16 or "
                                "the factored rbf form out of range): use the Gram pattern");
-        if (elig && sparse_algo != 1) {
-            // the two SELL passes of the kernel expansion (the factored linear path's plans, with K channels):
-            // moments over the CSC of all rows, the Horner pass over this rank's CSR rows
-            const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
-            const int64_t blocks = sell_target_blocks();
-            csr.csc_r0 = 0;
-            csr.csc_r1 = m;
-            build_spmv_plan<T>(
-                csr.spmv_csc, d, m, nnz, f22,
-                [&](auto emit) {
-                    for (int64_t i = 0; i < m; ++i)
-                        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit((int64_t) col[k], i, (double) hval(k));
-                },
-                blocks, stream, 0, 1, csr.ex.KM);
-            build_spmv_plan<T>(
-                csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22,
-                [&](auto emit) {
-                    for (int64_t i = r0; i < r1; ++i)
-                        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit(i - r0, (int64_t) col[k], (double) hval(k));
-                },
-                blocks, stream, 0, csr.ex.KM, 1);
-            build_expansion(cpos_d.get(), max_inc);
-        } else {
-            build_gram_blocks(cpos_d.get(), max_inc);
+        const int64_t budget = sparse_mem_budget();
+        const bool use_exp = elig && sparse_algo != 1;
+        if (sparse_algo != 3) {
+            int64_t inc_total = 0;
+            for (int64_t I = csr.rb0; I < csr.rb1; ++I) inc_total += inc_rb[I];
+            csr.est_bytes = use_exp ? estimate_expansion_bytes(rowptr, col, colptr, crow, inc_total)
+                                    : csr.pair_bound * (int64_t) (2 * (2 + sizeof(T))) + max_inc * 48;
+        }
+        const bool forced = sparse_algo == 1 || sparse_algo == 2;
+        bool stored = false;
+        if (sparse_algo != 3 && (forced || csr.est_bytes <= budget)) {
+            try {
+                if (use_exp) {
+                    // the two SELL passes of the kernel expansion (the factored linear path's plans, with K channels):
+                    // moments over the CSC of all rows, the Horner pass over this rank's CSR rows (inside the try)
+                    const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
+                    const int64_t blocks = sell_target_blocks();
+                    csr.csc_r0 = 0;
+                    csr.csc_r1 = m;
+                    build_spmv_plan<T>(
+                        csr.spmv_csc, d, m, nnz, f22,
+                        [&](auto emit) {
+                            for (int64_t i = 0; i < m; ++i)
+                                for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit((int64_t) col[k], i, (double) hval(k));
+                        },
+                        blocks, stream, 0, 1, csr.ex.KM);
+                    build_spmv_plan<T>(
+                        csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22,
+                        [&](auto emit) {
+                            for (int64_t i = r0; i < r1; ++i)
+                                for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit(i - r0, (int64_t) col[k], (double) hval(k));
+                        },
+                        blocks, stream, 0, csr.ex.KM, 1);
+                    build_expansion(cpos_d.get(), max_inc);
+                } else {
+                    build_gram_blocks(cpos_d.get(), max_inc);
+                }
+                stored = true;
+            } catch (const mi_error &e) {
+                if (e.code != -4 || forced) throw;
+                MI_HIP_CHECK(hipStreamSynchronize(stream));
+                const int64_t keep = csr.est_bytes;  // the stored structure did not fit after all: drop it
+                release_sparse_structures();
+                csr.est_bytes = keep;
+            }
+        }
+        if (!stored) {
+            cpos_d.reset();
+            setup_sparse_dense();
         }
     }
+}
+
+// device bytes the stored sparse structures may use: 85 % of the free memory (PLSSVM_MI_MEM_BUDGET =
+// bytes overrides it, tests force the densified path with it)
+template <typename T>
+int64_t engine<T>::sparse_mem_budget() const {
+    if (const char *e = std::getenv("PLSSVM_MI_MEM_BUDGET")) {
+        const long long v = std::atoll(e);
+        if (v > 0) return (int64_t) v;
+    }
+    size_t free_b = 0, total_b = 0;
+    MI_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    return (int64_t) ((double) free_b * 0.85);
+}
+
+// peak device bytes of build_expansion: the remainder's symmetric entries (sampled: partners sharing two
+// or more features of up to 64 rows of this rank, capped at ~2^28 column-join incidences) times the
+// bytes its build holds per entry (lower list, symmetric rows, cells, sort keys), plus one sub-block of
+// sort temporaries
+template <typename T>
+int64_t engine<T>::estimate_expansion_bytes(const int64_t *rowptr, const int32_t *col, const std::vector<int64_t> &colptr,
+                                            const std::vector<int32_t> &crow, int64_t inc_total) const {
+    const int64_t R = r1 - r0;
+    if (R <= 0 || m <= 0) return 0;
+    std::vector<int32_t> cnt((size_t) m, 0);
+    std::vector<int32_t> touched;
+    const int64_t S = std::min<int64_t>(R, 64);
+    int64_t sampled = 0, entries = 0, inc = 0;
+    for (int64_t s = 0; s < S && inc < (int64_t(1) << 28); ++s) {
+        const int64_t i = r0 + (s * R) / S;
+        touched.clear();
+        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+            const int32_t f = col[k];
+            for (int64_t t = colptr[f]; t < colptr[f + 1]; ++t) {
+                const int32_t j = crow[t];
+                if (cnt[j]++ == 0) touched.push_back(j);
+            }
+            inc += colptr[f + 1] - colptr[f];
+        }
+        for (const int32_t j : touched) {
+            if (j != i && cnt[j] >= 2) ++entries;
+            cnt[j] = 0;
+        }
+        ++sampled;
+    }
+    const double per_row = sampled ? (double) entries / (double) sampled : 0.0;
+    const double est_entries = per_row * (double) R;
+    const int64_t per_entry = 2 * (4 + 4 + (int64_t) sizeof(T)) + 4 * (4 + (int64_t) sizeof(T)) + 16;
+    const int64_t blk = std::min<int64_t>(inc_total, int64_t(1) << 27);
+    return (int64_t) (est_entries * (double) per_entry) + blk * 80;
+}
+
+// drop every stored sparse K·p structure (a build that ran out of memory)
+template <typename T>
+void engine<T>::release_sparse_structures() {
+    csr.ex = exp_data<T>{};
+    csr.spmv_csc = spmv_plan<T>{};
+    csr.spmv_csr = spmv_plan<T>{};
+    csr.pj.reset(), csr.ps.reset(), csr.rb_base.reset(), csr.rowoff.reset(), csr.cells.reset();
+    csr.slab_row.reset(), csr.slab_col.reset();
+    csr.have_gram = false;
+    csr.pairs = csr.slots = 0;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void csr_densify_kernel(const int64_t *__restrict__ rowptr,
+                                                          const int32_t *__restrict__ col, const T *__restrict__ val,
+                                                          int64_t m, int64_t n_pad, T *__restrict__ XT) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) XT[(int64_t) col[k] * n_pad + i] = val[k];
+}
+
+// the densified path: XT[d_pad][n_pad] from the device CSR, the dense pairwise partial slab; K·p then
+// runs the MFMA tiles of the dense path (every pair recomputed from the data, as the reference does on
+// its densified arrays)
+template <typename T>
+void engine<T>::setup_sparse_dense() {
+    const int64_t dp = round_up(std::max<int64_t>(d, 1), kp_dpad<T>());
+    const int64_t need = (dp * n_pad + std::max<int64_t>(nb, 1) * n_pad) * (int64_t) sizeof(T);
+    size_t free_b = 0, total_b = 0;
+    MI_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    if ((double) need > 0.95 * (double) free_b)
+        throw mi_error(-4, "sparse data: the stored K·p structures exceed the device budget (estimated " +
+                               std::to_string(csr.est_bytes >> 20) + " MiB) and the densified matrix needs " +
+                               std::to_string(need >> 20) + " MiB of " + std::to_string(free_b >> 20) +
+                               " MiB free: use more GPUs or a smaller data set");
+    d_pad = dp;
+    XT.alloc(d_pad * n_pad, stream);
+    partial.alloc(std::max<int64_t>(nb, 1) * n_pad, stream, false);
+    if (m > 0)
+        hipLaunchKernelGGL(csr_densify_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream,
+                           csr.rowptr.get(), csr.col.get(), csr.val.get(), m, n_pad, XT.get());
+    MI_LAUNCH_CHECK();
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    csr.dense_on = true;
 }
 
 template <typename T>

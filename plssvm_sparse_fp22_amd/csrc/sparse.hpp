@@ -101,6 +101,10 @@ struct csr_data {
     dev_buf<T> ssc;       // device scalars: [0] = sum(e p) or sum(p)
 
     exp_data<T> ex;       // kernel expansion path (instead of the Gram pattern)
+    // densified fallback (PLSSVM_MI_SPARSE_DENSE): neither stored structure fits the device budget, so
+    // X is densified into the engine's XT and every K·p recomputes all pairs on the MFMA tiles
+    bool dense_on = false;
+    int64_t est_bytes = 0;  // estimated device bytes of the chosen stored structure (0: not estimated)
 
     vals_t<T> rvals() const { return vals_t<T>{ val.get(), nullptr }; }
     vals_t<T> cvals() const { return vals_t<T>{ cval.get(), nullptr }; }

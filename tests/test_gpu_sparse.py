@@ -92,6 +92,48 @@ def test_sparse_expansion_large_arguments(oracle, kernel, gamma, coef0, dtype):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("kernel", ["rbf", "polynomial"])
+@pytest.mark.parametrize("shape", [(300, 500, 10), (2500, 3000, 20)])
+def test_sparse_densified_path(oracle, kernel, dtype, shape):
+    """PLSSVM_MI_SPARSE_DENSE: X densified on the device, K·p on the dense MFMA tiles."""
+    n, d, k = shape
+    csr, _ = datagen.sparse_csr(n, d, k, seed=n + 7, dtype=dtype)
+    info = check_sparse_kp(oracle, csr, kernel, dtype, algo="dense")
+    assert info["sparse_algo"] == pm._abi.SPARSE_DENSE and info["pair_slots"] == 0
+
+
+@pytest.mark.parametrize("kernel", ["rbf", "polynomial"])
+def test_sparse_over_budget_falls_back_to_densified(oracle, kernel, monkeypatch):
+    """auto: a stored structure estimated above the device budget (PLSSVM_MI_MEM_BUDGET) is never built;
+    the densified path runs instead, with the same results. A forced algorithm ignores the budget."""
+    csr, _ = datagen.sparse_csr(3000, 400, 25, seed=4, dtype=np.float64)
+    monkeypatch.setenv("PLSSVM_MI_MEM_BUDGET", "4096")
+    info = check_sparse_kp(oracle, csr, kernel, np.float64)
+    assert info["sparse_algo"] == pm._abi.SPARSE_DENSE
+    info = check_sparse_kp(oracle, csr, kernel, np.float64, algo="expansion")
+    assert info["sparse_algo"] == pm._abi.SPARSE_EXPANSION
+    monkeypatch.delenv("PLSSVM_MI_MEM_BUDGET")
+    info = check_sparse_kp(oracle, csr, kernel, np.float64)
+    assert info["sparse_algo"] == pm._abi.SPARSE_EXPANSION
+
+
+def test_sparse_densified_learn_and_fp22(oracle):
+    """the densified path through learn() (CG, rank-1 terms, bias) and with packed FP22 input"""
+    csr, y = datagen.sparse_csr(1500, 900, 30, seed=6, dtype=np.float64)
+    svm = sparse_svm(csr, "rbf", np.float64, y=y, coef0=0.0, algo="dense")
+    svm.learn(imax=40)
+    ref = oracle.learn("rbf", oracle_data(oracle, csr, np.float64), y, imax=40, gamma=1.0 / 900)
+    assert abs(svm.iters - ref["iters"]) <= 1
+    n = min(len(svm.trace), len(ref["trace"]), 6)
+    np.testing.assert_allclose(svm.trace[:n], ref["trace"][:n], rtol=1e-6)
+    np.testing.assert_allclose(svm.alpha, ref["alpha"], rtol=1e-6, atol=1e-6 * np.abs(ref["alpha"]).max())
+    svm.close()
+    csr32, _ = datagen.sparse_csr(2000, 1200, 25, seed=5, dtype=np.float32)
+    info = check_sparse_kp(oracle, csr32, "rbf", np.float32, fp22=True, algo="dense")
+    assert info["sparse_algo"] == pm._abi.SPARSE_DENSE
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_sparse_rbf_large_gamma_falls_back_to_direct(oracle, dtype):
     """g max|x|^2 far outside the factored form's range (e_i underflows): auto must pick the direct form."""
     csr, _ = datagen.sparse_csr(2500, 300, 20, seed=11, dtype=dtype)
