@@ -817,7 +817,9 @@ template <typename T>
 void engine<T>::expansion_moments(const T *w, const cg_scalars<T> *status) {
     auto &ex = csr.ex;
     if (d > 0) {  // column moments: one SELL pass over the CSC (mode 1), then the coefficients
-        launch_panel_spmv<T>(csr.spmv_csc, w, m, ex.mom.get(), status, stream, ex.KM, 1);
+        // (a real group: each rank's rows, then one all-reduce of the d x K moments)
+        launch_panel_spmv<T>(csr.spmv_csc, w + csr.csc_r0, csr.csc_r1 - csr.csc_r0, ex.mom.get(), status, stream, ex.KM, 1);
+        if (csr.csc_r1 - csr.csc_r0 < m) allreduce(ex.mom.get(), d * ex.KM);
         coefs cf;
         std::memcpy(cf.c, ex.coef, sizeof(cf.c));
         if (exp_ablate() & 2)

@@ -735,16 +735,19 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             try {
                 if (use_exp) {
                     // the two SELL passes of the kernel expansion (the factored linear path's plans, with K channels):
-                    // moments over the CSC of all rows, the Horner pass over this rank's CSR rows (inside the try)
+                    // column moments over the CSC of this rank's rows in a real group (all-reduced, d x K values)
+                    // or of all rows, the Horner pass over this rank's CSR rows
                     const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
                     const int64_t blocks = sell_target_blocks();
-                    csr.csc_r0 = 0;
-                    csr.csc_r1 = m;
+                    const bool local = world > 1 && sim_world == 0;
+                    csr.csc_r0 = local ? r0 : 0;
+                    csr.csc_r1 = local ? r1 : m;
                     build_spmv_plan<T>(
-                        csr.spmv_csc, d, m, nnz, f22,
+                        csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22,
                         [&](auto emit) {
-                            for (int64_t i = 0; i < m; ++i)
-                                for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit((int64_t) col[k], i, (double) hval(k));
+                            for (int64_t i = csr.csc_r0; i < csr.csc_r1; ++i)
+                                for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k)
+                                    emit((int64_t) col[k], i - csr.csc_r0, (double) hval(k));
                         },
                         blocks, stream, 0, 1, csr.ex.KM);
                     build_spmv_plan<T>(
