@@ -136,7 +136,10 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
     __shared__ T xs[XW];
     if (status != nullptr && status->converged) return;
     const int tid = threadIdx.x, lane = tid & 63;
-    const int c0 = bchunk[blockIdx.x], c1 = bchunk[blockIdx.x + 1];
+    // XCD-aware: consecutive chunk ranges (the blocks of one panel) share an XCD, so a panel of x is
+    // fetched into that XCD's L2 once and the other blocks' fills hit it
+    const int blk = (int) xcd_remap(blockIdx.x, gridDim.x);
+    const int c0 = bchunk[blk], c1 = bchunk[blk + 1];
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     auto gx = [&](const T *xg, int64_t c) -> T {
         if constexpr (LDSX) return xs[c];
@@ -149,7 +152,10 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
         const int ce = min(c1, (q + 1) * nchp);  // chunks of panel q are [q nchp, (q + 1) nchp)
         T *o = out + (int64_t) q * nseg * OC;
         const T *xg = x + (int64_t) q * W * XC;  // LDSX: panel q gathers x[q W + local]; otherwise W = 0
-        if constexpr (LDSX) {
+#ifndef PLSSVM_MI_ABL_SELL
+#define PLSSVM_MI_ABL_SELL 0  // timing ablation only: 1 = skip the panel fill (wrong results)
+#endif
+        if constexpr (LDSX && PLSSVM_MI_ABL_SELL != 1) {
             if (cb != c0) __syncthreads();
             const int xl = (int) min((int64_t) W, xn - (int64_t) q * W) * XC;
             // 16-byte loads and LDS stores (XW is a multiple of 16 B per thread); a misaligned panel
