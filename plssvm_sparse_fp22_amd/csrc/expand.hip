@@ -321,8 +321,8 @@ __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__res
 }
 
 // hs[i] = sum_j H_ij w_j. One 1024-thread workgroup per block of exp_rb rows walks the windows of
-// partners: the window of w (exp_cw values) is staged in LDS (double-buffered: the next window is loaded
-// into registers while the current one is used), each wave streams its rows' 4-slot chunks (one
+// partners: the window of w (exp_cw values) is staged in LDS (the next window is loaded into registers
+// while the current one is used, then stored between two barriers), each wave streams its rows' 4-slot chunks (one
 // contiguous range across all windows, coalesced, nontemporal so the stream does not evict w from L2,
 // software-pipelined one step ahead, also across window boundaries), gathers w_j from LDS and adds its
 // rows' partial sums (segmented shuffle reduction) into an LDS row accumulator only it writes.
@@ -336,7 +336,8 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
                                                                  T *__restrict__ hs,
                                                                  const cg_scalars<T> *__restrict__ status) {
     constexpr int CW = exp_cw<T>(), RB = exp_rb<T>(), NT = EXP_NWV * 64, PER = CW / NT;
-    __shared__ T wl[2][CW];
+    static_assert(CW <= 65536, "window-local partner indices are 16-bit");
+    __shared__ T wl[CW];
     __shared__ T racc[RB];
     if (status != nullptr && status->converged) return;
     const int64_t I = xcd_remap(blockIdx.x, gridDim.x);
@@ -350,9 +351,9 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             reg[q] = idx < m ? w[idx] : T(0);
         }
     };
-    auto store_win = [&](int buf) {
+    auto store_win = [&]() {
 #pragma unroll
-        for (int q = 0; q < PER; ++q) wl[buf][q * NT + tid] = reg[q];
+        for (int q = 0; q < PER; ++q) wl[q * NT + tid] = reg[q];
     };
     const int64_t *wo = woff + (I * EXP_NWV + wave) * (nW + 1);
     const int64_t s_end = wo[nW];
@@ -375,14 +376,13 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
         }
     };
     load_win(0);
-    store_win(0);
+    store_win();
     fetch(wo[0] + lane);
     __syncthreads();
     for (int64_t W = 0; W < nW; ++W) {
-        const int buf = (int) (W & 1);
-        if (W + 1 < nW) load_win(W + 1);  // lands while this window is processed
+        if (W + 1 < nW) load_win(W + 1);  // lands in registers while this window is processed
         const int64_t c_end = wo[W + 1];
-        const T *wb = wl[buf];
+        const T *wb = wl;
         for (int64_t cb = wo[W]; cb < c_end; cb += 64) {  // wave-uniform trip count
             const bool have = cb + lane < c_end;
             const int rl = have ? rl_n : -1;
@@ -407,7 +407,10 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             const int rprev = __shfl_up(rl, 1);
             if (rl >= 0 && (lane == 0 || rprev != rl)) racc[rl] += sacc;  // rows of this wave only
         }
-        if (W + 1 < nW) store_win(buf ^ 1);
+        if (W + 1 < nW) {
+            __syncthreads();  // every wave is done with window W
+            store_win();
+        }
         __syncthreads();
     }
     const int64_t rb0 = I * RB;

@@ -37,9 +37,14 @@ constexpr int EXP_NWV = 16;  // waves per remainder-stream workgroup (one workgr
 // rows per remainder-stream block (one workgroup; exp_rb / EXP_NWV rows per wave)
 template <typename T>
 constexpr int exp_rb() { return sizeof(T) == 4 ? 4096 : 2048; }
-// window of partners j staged in LDS (double-buffered: 2 x 64 KiB + the row accumulator = 144 KiB)
+// window of partners j staged in LDS: one 144 KiB buffer + the row accumulator = 160 KiB (the next
+// window is prefetched into registers). PLSSVM_MI_EXP_CWB = window bytes (build option, measurements);
+// bigger windows = fewer (row, window) groups = less 4-slot padding
+#ifndef PLSSVM_MI_EXP_CWB
+#define PLSSVM_MI_EXP_CWB 147456
+#endif
 template <typename T>
-constexpr int exp_cw() { return sizeof(T) == 4 ? 16384 : 8192; }
+constexpr int exp_cw() { return PLSSVM_MI_EXP_CWB / (int) sizeof(T); }
 
 template <typename T>
 struct exp_data {
