@@ -249,9 +249,8 @@ __global__ __launch_bounds__(256) void exp_mscale_kernel(const T *__restrict__ m
 
 // ---- remainder stream layout (built from the padded symmetric rows) ---------------------------------------
 // count index of (row r, window W): ((I NWV + v) nW + W) RPW + rr,  r = I RB + v RPW + rr
-template <typename T>
-__device__ __forceinline__ int64_t exp_cidx(int64_t r, int64_t W, int64_t nW) {
-    constexpr int64_t RB = exp_rb<T>(), RPW = RB / EXP_NWV;
+__device__ __forceinline__ int64_t exp_cidx(int64_t r, int64_t W, int64_t nW, int64_t RB) {
+    const int64_t RPW = RB / EXP_NWV;
     const int64_t I = r / RB, v = (r % RB) / RPW, rr = r % RPW;
     return ((I * EXP_NWV + v) * nW + W) * RPW + rr;
 }
@@ -260,8 +259,8 @@ __device__ __forceinline__ int64_t exp_cidx(int64_t r, int64_t W, int64_t nW) {
 template <typename T>
 __global__ __launch_bounds__(256) void exp_cell_count_kernel(const int64_t *__restrict__ off8,
                                                              const int32_t *__restrict__ sj, const T *__restrict__ sv,
-                                                             int64_t R, int64_t nW, int64_t *__restrict__ cnt) {
-    constexpr int64_t CW = exp_cw<T>();
+                                                             int64_t R, int64_t nW, int64_t CW, int64_t RB,
+                                                             int64_t *__restrict__ cnt) {
     const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
     int64_t Wc = -1, k = 0;
@@ -269,22 +268,22 @@ __global__ __launch_bounds__(256) void exp_cell_count_kernel(const int64_t *__re
         if (sv[s] == T(0)) continue;                    // pads (and no stored H is exactly 0)
         const int64_t W = sj[s] / CW;
         if (W != Wc) {
-            if (Wc >= 0) cnt[exp_cidx<T>(r, Wc, nW)] = (k + 3) & ~int64_t(3);
+            if (Wc >= 0) cnt[exp_cidx(r, Wc, nW, RB)] = (k + 3) & ~int64_t(3);
             Wc = W;
             k = 0;
         }
         ++k;
     }
-    if (Wc >= 0) cnt[exp_cidx<T>(r, Wc, nW)] = (k + 3) & ~int64_t(3);
+    if (Wc >= 0) cnt[exp_cidx(r, Wc, nW, RB)] = (k + 3) & ~int64_t(3);
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__restrict__ off8,
                                                                const int32_t *__restrict__ sj, const T *__restrict__ sv,
-                                                               int64_t R, int64_t nW, const int64_t *__restrict__ coff,
+                                                               int64_t R, int64_t nW, int64_t CW, int64_t RB,
+                                                               const int64_t *__restrict__ coff,
                                                                uint16_t *__restrict__ hjl, T *__restrict__ hv,
                                                                uint16_t *__restrict__ hrow) {
-    constexpr int64_t CW = exp_cw<T>(), RB = exp_rb<T>();
     const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
     const uint16_t rl = (uint16_t) (r % RB);
@@ -299,7 +298,7 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__
         if (W != Wc) {
             if (Wc >= 0) close();
             Wc = W;
-            base = coff[exp_cidx<T>(r, W, nW)];
+            base = coff[exp_cidx(r, W, nW, RB)];
             k = 0;
         }
         hjl[base + k] = (uint16_t) (sj[s] - W * CW);
@@ -310,24 +309,23 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__
 }
 
 // first chunk of (block I, wave v, window W), W = 0..nW (W = nW: the end of the wave's stream)
-template <typename T>
 __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__restrict__ coff, int64_t nbv, int64_t nW,
-                                                            int64_t *__restrict__ woff) {
-    constexpr int64_t RPW = exp_rb<T>() / EXP_NWV;
+                                                            int64_t RB, int64_t *__restrict__ woff) {
+    const int64_t RPW = RB / EXP_NWV;
     const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nbv * (nW + 1)) return;
     const int64_t bv = t / (nW + 1), W = t % (nW + 1);
     woff[t] = coff[(bv * nW + W) * RPW] >> 2;
 }
 
-// hs[i] = sum_j H_ij w_j. One 1024-thread workgroup per block of exp_rb rows walks the windows of
-// partners: the window of w (exp_cw values) is staged in LDS (the next window is loaded into registers
+// hs[i] = sum_j H_ij w_j. One 1024-thread workgroup per block of RB rows walks the windows of
+// partners: the window of w (CW values) is staged in LDS (the next window is loaded into registers
 // while the current one is used, then stored between two barriers), each wave streams its rows' 4-slot chunks (one
 // contiguous range across all windows, coalesced, nontemporal so the stream does not evict w from L2,
 // software-pipelined one step ahead, also across window boundaries), gathers w_j from LDS and adds its
 // rows' partial sums (segmented shuffle reduction) into an LDS row accumulator only it writes.
 // Fixed order, no atomics: bitwise reproducible.
-template <typename T>
+template <typename T, int RBB>
 __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *__restrict__ woff,
                                                                  const uint16_t *__restrict__ hrow,
                                                                  const uint16_t *__restrict__ hjl,
@@ -335,7 +333,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
                                                                  int64_t m, int64_t r0, int64_t R, int64_t nW,
                                                                  T *__restrict__ hs,
                                                                  const cg_scalars<T> *__restrict__ status) {
-    constexpr int CW = exp_cw<T>(), RB = exp_rb<T>(), NT = EXP_NWV * 64, PER = CW / NT;
+    constexpr int CW = exp_cw_of<T, RBB>(), RB = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64, PER = CW / NT;
     static_assert(CW <= 65536, "window-local partner indices are 16-bit");
     __shared__ T wl[CW];
     __shared__ T racc[RB];
@@ -747,8 +745,28 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
     }
     Li.reset(), Lj.reset(), Lh.reset(), uidx.reset(), ukey.reset(), ukey_s.reset(), uidx_s.reset();
 
-    // ---- cells: blocks of EXP_RB rows x windows of CW partners, rows padded to 4 slots per cell ----
-    constexpr int64_t CW = exp_cw<T>(), RB = exp_rb<T>();
+    // ---- cells: blocks of RB rows x windows of CW partners, rows padded to 4 slots per cell ----
+    // geometry: the largest row block whose block count still covers ~all CUs (PLSSVM_MI_EXP_RBB forces)
+    {
+        int cus = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            cus = prop.multiProcessorCount;
+        ex.RBB = 4096;
+        for (int rbb : { 32768, 16384, 8192 }) {
+            if (ceil_div(std::max<int64_t>(R, 1), rbb / (int64_t) sizeof(T)) * 10 >= (int64_t) cus * 9) {
+                ex.RBB = rbb;
+                break;
+            }
+        }
+        if (const char *e = std::getenv("PLSSVM_MI_EXP_RBB")) {
+            const int v = std::atoi(e);
+            if (v == 4096 || v == 8192 || v == 16384 || v == 32768) ex.RBB = v;
+        }
+        ex.RB = ex.RBB / (int) sizeof(T);
+        ex.CW = exp_cw_host(ex.RBB, (int) sizeof(T));
+    }
+    const int64_t CW = ex.CW, RB = ex.RB;
     ex.nW = ceil_div(std::max<int64_t>(m, 1), CW);
     ex.nblk = ceil_div(R, RB);
     const int64_t nbv = ex.nblk * EXP_NWV, ncnt = ex.nblk * RB * ex.nW;
@@ -758,7 +776,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         coff.alloc(ncnt + 1, stream, false);
         if (R > 0) {
             hipLaunchKernelGGL(exp_cell_count_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                               off8.get(), sj.get(), sv.get(), R, ex.nW, cnt.get());
+                               off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, cnt.get());
             MI_LAUNCH_CHECK();
         }
         size_t tb = 0;
@@ -774,14 +792,14 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
         if (R > 0) {
             hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                               off8.get(), sj.get(), sv.get(), R, ex.nW, coff.get(), ex.hjl.get(), ex.hv.get(),
-                               ex.hrow.get());
+                               off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
+                               ex.hv.get(), ex.hrow.get());
             MI_LAUNCH_CHECK();
         }
         ex.woff.alloc(std::max<int64_t>(nbv * (ex.nW + 1), 1), stream);
         if (nbv > 0) {
-            hipLaunchKernelGGL(exp_cell_woff_kernel<T>, dim3((unsigned) ceil_div(nbv * (ex.nW + 1), 256)), dim3(256), 0,
-                               stream, coff.get(), nbv, ex.nW, ex.woff.get());
+            hipLaunchKernelGGL(exp_cell_woff_kernel, dim3((unsigned) ceil_div(nbv * (ex.nW + 1), 256)), dim3(256), 0,
+                               stream, coff.get(), nbv, ex.nW, RB, ex.woff.get());
             MI_LAUNCH_CHECK();
         }
         MI_HIP_CHECK(hipStreamSynchronize(stream));
@@ -808,8 +826,16 @@ template <typename T>
 void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
     auto &ex = csr.ex;
     if (ex.nblk > 0 && !(exp_ablate() & 1)) {
-        hipLaunchKernelGGL(exp_hcell_kernel<T>, dim3((unsigned) ex.nblk), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
-                           ex.hrow.get(), ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, ex.hs.get(), status);
+        auto launch = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned) ex.nblk), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(), ex.hrow.get(),
+                               ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, ex.hs.get(), status);
+        };
+        switch (ex.RBB) {
+            case 4096: launch(exp_hcell_kernel<T, 4096>); break;
+            case 8192: launch(exp_hcell_kernel<T, 8192>); break;
+            case 32768: launch(exp_hcell_kernel<T, 32768>); break;
+            default: launch(exp_hcell_kernel<T, 16384>);
+        }
         MI_LAUNCH_CHECK();
     } else if (r1 > r0) {
         MI_HIP_CHECK(hipMemsetAsync(ex.hs.get() + r0, 0, sizeof(T) * (size_t) (r1 - r0), stream));

@@ -34,17 +34,17 @@ struct gram_cell {
 // the pairs sharing two or more features (stored, symmetric, rows padded to 8 slots).
 constexpr int EXP_KMAX = 16;
 constexpr int EXP_NWV = 16;  // waves per remainder-stream workgroup (one workgroup per CU)
-// rows per remainder-stream block (one workgroup; exp_rb / EXP_NWV rows per wave)
-template <typename T>
-constexpr int exp_rb() { return sizeof(T) == 4 ? 4096 : 2048; }
-// window of partners j staged in LDS: one 144 KiB buffer + the row accumulator = 160 KiB (the next
-// window is prefetched into registers). PLSSVM_MI_EXP_CWB = window bytes (build option, measurements);
-// bigger windows = fewer (row, window) groups = less 4-slot padding
-#ifndef PLSSVM_MI_EXP_CWB
-#define PLSSVM_MI_EXP_CWB 147456
-#endif
-template <typename T>
-constexpr int exp_cw() { return PLSSVM_MI_EXP_CWB / (int) sizeof(T); }
+// Remainder-stream geometry: one 1024-thread workgroup per block of RB rows (RB / EXP_NWV rows per
+// wave) holds an LDS row accumulator (RB values) and one LDS window of CW partners (the next window is
+// prefetched into registers), together the CU's 160 KiB. RBB = accumulator bytes in {4, 8, 16, 32} KiB;
+// setup picks the largest whose block count still fills the CUs (bigger blocks = w restaged fewer
+// times; a bigger window = fewer (row, window) groups = less 4-slot padding).
+constexpr int EXP_LDS = 163840;
+template <typename T, int RBB>
+constexpr int exp_rb_of() { return RBB / (int) sizeof(T); }
+template <typename T, int RBB>
+constexpr int exp_cw_of() { return (EXP_LDS - RBB) / (int) sizeof(T) / 1024 * 1024; }
+inline int exp_cw_host(int rbb, int es) { return (EXP_LDS - rbb) / es / 1024 * 1024; }
 
 template <typename T>
 struct exp_data {
@@ -59,10 +59,11 @@ struct exp_data {
     dev_buf<T> wv;                    // [n_pad]: w = e p (rbf)
     dev_buf<T> hs;                    // [n_pad]: sum_j H_ij w_j
     int64_t pairs = 0;                // unordered pairs sharing >= 2 features with H != 0 (this rank's rows)
-    // remainder stream: per row block I (exp_rb rows), per wave v (its exp_rb / EXP_NWV rows), per
-    // window W of exp_cw partners j, row by row: the row's entries with j in W, padded to a multiple of 4
+    // remainder stream: per row block I (RB rows), per wave v (its RB / EXP_NWV rows), per
+    // window W of CW partners j, row by row: the row's entries with j in W, padded to a multiple of 4
     // slots (pads: j = 0, H = 0); each wave's stream is one contiguous range across the windows
     int64_t slots = 0, nchunks = 0, nblk = 0, nW = 0;
+    int RBB = 16384, RB = 0, CW = 0;  // geometry (see above): accumulator bytes, rows per block, window
     dev_buf<uint16_t> hjl;            // [slots] j - W * CW
     dev_buf<T> hv;                    // [slots] H_ij
     dev_buf<uint16_t> hrow;           // [nchunks] block-local row of each 4-slot chunk

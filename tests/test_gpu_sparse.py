@@ -133,6 +133,17 @@ def test_sparse_densified_learn_and_fp22(oracle):
     assert info["sparse_algo"] == pm._abi.SPARSE_DENSE
 
 
+@pytest.mark.parametrize("rbb", ["4096", "8192", "32768"])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_sparse_expansion_stream_geometries(oracle, rbb, dtype, monkeypatch):
+    """every remainder-stream geometry (rows per block / window width, PLSSVM_MI_EXP_RBB) against the
+    oracle, on data whose multi-feature pairs span several windows and blocks"""
+    monkeypatch.setenv("PLSSVM_MI_EXP_RBB", rbb)
+    csr, _ = datagen.sparse_csr(42000, 600, 10, seed=21, dtype=dtype)
+    info = check_sparse_kp(oracle, csr, "rbf", dtype, gamma=0.1)
+    assert info["sparse_algo"] == pm._abi.SPARSE_EXPANSION and info["pairs"] > 0
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_sparse_rbf_large_gamma_falls_back_to_direct(oracle, dtype):
     """g max|x|^2 far outside the factored form's range (e_i underflows): auto must pick the direct form."""
