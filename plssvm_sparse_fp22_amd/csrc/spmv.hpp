@@ -47,6 +47,21 @@ constexpr int SELL_SIGMA = 4096;    // sorting window (segments)
 #define PLSSVM_MI_SELL_UNROLL 4
 #endif
 constexpr int SELL_UNROLL = PLSSVM_MI_SELL_UNROLL;  // entries per lane in flight per step
+// IDX2: the 16-bit panel indices of entries 2t, 2t+1 of a slot are adjacent, so one 32-bit load per lane
+// (256 B per wave-instruction) fetches two; chunk widths are padded to even
+#ifndef PLSSVM_MI_SELL_IDX2
+#define PLSSVM_MI_SELL_IDX2 1
+#endif
+constexpr bool SELL_IDX2 = PLSSVM_MI_SELL_IDX2 != 0;
+// VAL2 (with IDX2): the values are stored in the same pair-interleaved order (one 8 / 16-byte load per
+// lane fetches two real values; FP22 streams keep per-entry decoding at the remapped positions)
+#ifndef PLSSVM_MI_SELL_VAL2
+#define PLSSVM_MI_SELL_VAL2 0
+#endif
+constexpr bool SELL_VAL2 = SELL_IDX2 && PLSSVM_MI_SELL_VAL2 != 0;
+// storage position of the entry at value position t = off + 64 j + l (off % 128 == 0 when paired)
+inline int64_t sell_pair_pos(int64_t t) { return (t & ~int64_t(127)) + 2 * (t & 63) + ((t >> 6) & 1); }
+static_assert(!SELL_IDX2 || SELL_UNROLL % 2 == 0, "paired indices need an even step");
 template <typename T>
 constexpr int sell_width() { return SELL_XBYTES / (int) sizeof(T); }
 // workgroups per pass: equal-cost chunk ranges, a multiple of the 256 CUs (one resident workgroup per
@@ -195,8 +210,34 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
 #pragma unroll
                 for (int u = 0; u < SELL_UNROLL; ++u) {
                     const int64_t k = base + (int64_t) min(j + u, last) * 64;
-                    ci[u] = __builtin_nontemporal_load(idx + k);
-                    vi[u] = sell_val<T, F22>(val, k);
+                    if constexpr (!(LDSX && SELL_IDX2)) ci[u] = __builtin_nontemporal_load(idx + k);
+                    if constexpr (!(LDSX && SELL_VAL2)) {
+                        vi[u] = sell_val<T, F22>(val, k);
+                    } else if constexpr (F22) {
+                        const int jj = min(j + u, last);
+                        vi[u] = sell_val<T, F22>(val, ch.off + 128 * (int64_t) (jj >> 1) + 2 * lane + (jj & 1));
+                    }
+                }
+                if constexpr (LDSX && SELL_VAL2 && !F22) {
+                    using V2 = __attribute__((ext_vector_type(2))) T;
+                    const V2 *vp = reinterpret_cast<const V2 *>(val.v) + (ch.off >> 1) + lane;
+                    const int lastp = max((ch.width >> 1) - 1, 0);
+#pragma unroll
+                    for (int u2 = 0; u2 < SELL_UNROLL / 2; ++u2) {
+                        const V2 pr = __builtin_nontemporal_load(vp + (int64_t) min((j >> 1) + u2, lastp) * 64);
+                        vi[2 * u2] = pr.x;
+                        vi[2 * u2 + 1] = pr.y;
+                    }
+                }
+                if constexpr (LDSX && SELL_IDX2) {
+                    const uint32_t *ip = reinterpret_cast<const uint32_t *>(idx) + (ch.off >> 1) + lane;
+                    const int lastp = max((ch.width >> 1) - 1, 0);
+#pragma unroll
+                    for (int u2 = 0; u2 < SELL_UNROLL / 2; ++u2) {
+                        const uint32_t pr = __builtin_nontemporal_load(ip + (int64_t) min((j >> 1) + u2, lastp) * 64);
+                        ci[2 * u2] = (idx_t) (pr & 0xFFFFu);
+                        ci[2 * u2 + 1] = (idx_t) (pr >> 16);
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < SELL_UNROLL; ++u) {
@@ -365,6 +406,7 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
                 const int32_t sgm = perm[(size_t) (q * slots_per_panel + c * 64 + l)];
                 if (sgm >= 0) width = std::max(width, lq[sgm]);
             }
+            if (SELL_IDX2 && ldsx) width = (width + 1) & ~1;  // paired indices: even widths, off % 128 == 0
             chunks[(size_t) (q * nch_per_panel + c)] = sell_chunk{ off, width, (int32_t) q };
             for (int l = 0; l < 64; ++l) {
                 const int32_t sgm = perm[(size_t) (q * slots_per_panel + c * 64 + l)];
@@ -388,18 +430,24 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
         int64_t &p = pos[(size_t) (q * nseg + s)];
         const int64_t t = p;
         p += 64;
-        if (ldsx) i16[t] = (uint16_t) (g - q * W);
+        if (ldsx) {
+            // IDX2: entry j of slot l (value position t = off + 64 j + l) keeps its index at
+            // off + 128 (j >> 1) + 2 l + (j & 1)
+            const int64_t ti = SELL_IDX2 ? sell_pair_pos(t) : t;
+            i16[ti] = (uint16_t) (g - q * W);
+        }
         else i32[t] = (int32_t) g;
+        const int64_t tv = (SELL_VAL2 && ldsx) ? sell_pair_pos(t) : t;  // value position
         if (fp22) {
             const uint64_t code = fp22_encode_host((float) v);
-            const int64_t gg = t >> 4;
-            const int bit = 22 * (int) (t & 15);
+            const int64_t gg = tv >> 4;
+            const int bit = 22 * (int) (tv & 15);
             const int64_t wi = gg * 11 + (bit >> 5);
             const int sh = bit & 31;
             v22[wi] |= (uint32_t) (code << sh);
             if (sh > 10) v22[wi + 1] |= (uint32_t) (code >> (32 - sh));
         } else {
-            vr[t] = (T) v;
+            vr[tv] = (T) v;
         }
     });
     // blocks: target_blocks contiguous chunk ranges of equal cost (entries + a per-chunk charge for its
