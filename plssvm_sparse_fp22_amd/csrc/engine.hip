@@ -391,7 +391,13 @@ void engine<T>::cg_iter(int reset) {
     // Ad = Q~ d (:111-113); alpha = delta / (d . Ad) (:116) in the next kernel
     const T *slabs = nullptr;
     int64_t P = 0;
-    if (sparse && factored() && world == 1 && sim_world == 0 && csr.spmv_csr.P > 1) {
+    if (sparse_stored() && factored() && world == 1 && sim_world == 0 && csr.rb_csr.nblk > 0) {
+        // one GPU, factored sparse linear: CSC pass, then the row-block CSR pass with the finalize and
+        // the d.Ad partials fused (spmv.hpp)
+        spmv_pass_csc(dv.get(), st);
+        launch_rowblock_fin<T>(csr.rb_csr, w.get(), d, q.get(), dv.get(), psum, QA_cost, cost_inv(), Ad.get(), pdad, st,
+                               stream);
+    } else if (sparse && factored() && world == 1 && sim_world == 0 && csr.spmv_csr.P > 1) {
         // one GPU, factored sparse linear: the CSR pass's panel slabs are summed by cg_fin_dad
         spmv_pass_csc(dv.get(), st);
         launch_panel_spmv<T>(csr.spmv_csr, w.get(), d, raw.get(), st, stream, 1, 0, false);
@@ -400,8 +406,9 @@ void engine<T>::cg_iter(int reset) {
     } else {
         kp_raw(dv.get(), st);
     }
-    launch_cg_fin_dad<T>(raw.get(), slabs, P, q.get(), dv.get(), psum, QA_cost, cost_inv(), raw_only, m, Ad.get(),
-                         pdad, sc.get(), stream);
+    if (!(sparse_stored() && factored() && world == 1 && sim_world == 0 && csr.rb_csr.nblk > 0))
+        launch_cg_fin_dad<T>(raw.get(), slabs, P, q.get(), dv.get(), psum, QA_cost, cost_inv(), raw_only, m, Ad.get(),
+                             pdad, sc.get(), stream);
     // x += alpha d; r = b - Q~x every 50th iteration, else r -= alpha Ad   (:119-132)
     launch_cg_upd_rr<T>(x.get(), r.get(), dv.get(), Ad.get(), b.get(), reset, pdad, m, prr, sc.get(), stream);
     if (reset) {

@@ -644,6 +644,14 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                     for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit(i - r0, (int64_t) col[k], (double) hval(k));
             },
             blocks, stream);
+        if (world == 1 && sim_world == 0 && rowblock_fused_enabled())  // CG iterations: CSR pass + finalize in one launch
+            build_rowblock_plan<T>(
+                csr.rb_csr, m, d, f22,
+                [&](auto emit) {
+                    for (int64_t i = 0; i < m; ++i)
+                        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit(i, (int64_t) col[k], (double) hval(k));
+                },
+                blocks, stream);
         return;
     }
 

@@ -88,6 +88,7 @@ struct csr_data {
     // this rank's rows in a real group) and raw[r0, r1) = X w, both as panelled SELL SpMVs
     int64_t csc_r0 = 0, csc_r1 = 0;
     spmv_plan<T> spmv_csc, spmv_csr;
+    rb_plan<T> rb_csr;  // one GPU: the CSR pass as row blocks with the CG finalize fused (spmv.hpp)
     dev_buf<T> e;                     // rbf separable factor exp(-gamma n_i)
 
     // Gram pattern
@@ -116,7 +117,7 @@ struct csr_data {
     vals_t<T> cvals() const { return vals_t<T>{ cval.get(), nullptr }; }
     int64_t bytes() const {
         return rowptr.bytes() + col.bytes() + val.bytes() + colptr.bytes() + crow.bytes() +
-               cval.bytes() + spmv_csc.bytes() + spmv_csr.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
+               cval.bytes() + spmv_csc.bytes() + spmv_csr.bytes() + rb_csr.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
                rb_base.bytes() + rowoff.bytes() + cells.bytes() + slab_row.bytes() + slab_col.bytes() + ex.bytes();
     }
 };

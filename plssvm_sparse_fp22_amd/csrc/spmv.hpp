@@ -487,4 +487,265 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
     MI_HIP_CHECK(hipStreamSynchronize(stream));
 }
 
+// ---- row-block CSR pass with the CG finalize fused (factored sparse linear, one GPU) ------------------
+// raw = X w for a block of RBK rows owned by one 1024-thread workgroup: for each panel q of w (LDS), the
+// block's rows sorted by their panel-q length (descending) are dealt 64 per chunk to the waves, and each
+// lane adds its row's panel-q sum into an LDS row accumulator (every row once per panel, panels in
+// order: bitwise the (0 + slab0) + slab1 + ... of the panelled pass). The epilogue is cg_fin_dad's:
+// Ad_i = raw_i + (QA - q_i) sum(d) - sum(q d) + d_i / C, one d.Ad partial per block — no panel slabs,
+// no separate finalize launch.
+template <typename T>
+constexpr int rb_rows() { return 16384 / (int) sizeof(T); }  // row accumulator: 16 KiB
+template <typename T>
+constexpr int rb_width() { return (163840 - 16384) / (int) sizeof(T) / 1024 * 1024; }  // panel: the rest
+
+// PLSSVM_MI_ROWBLOCK=0 disables the fused row-block pass (measurements)
+inline bool rowblock_fused_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("PLSSVM_MI_ROWBLOCK");
+        return e == nullptr || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+template <typename T>
+struct rb_plan {
+    int64_t P = 0, W = 0, RBK = 0, nblk = 0, nrows = 0, entries = 0;
+    dev_buf<sell_chunk> chunks;  // ordered (block, panel, chunk)
+    dev_buf<int32_t> perm;       // [nchunks * 64] slot -> block-local row (-1: padding)
+    dev_buf<uint16_t> idx16;     // panel-local index, IDX2 pair layout
+    dev_buf<T> val;
+    dev_buf<uint32_t> val22;
+    dev_buf<int32_t> bpc;        // [nblk * P + 1]: chunk range of (block, panel)
+    vals_t<T> vals() const { return vals_t<T>{ val.get(), val22.get() }; }
+    int64_t bytes() const {
+        return chunks.bytes() + perm.bytes() + idx16.bytes() + val.bytes() + val22.bytes() + bpc.bytes();
+    }
+    int64_t stream_bytes() const {
+        const int64_t vb = val22.get() ? fp22_words(entries) * 4 : entries * (int64_t) sizeof(T);
+        return entries * 2 + vb + perm.bytes() + chunks.bytes();
+    }
+};
+
+template <typename T, bool F22>
+__global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
+    const sell_chunk *__restrict__ chunks, const int32_t *__restrict__ perm, const uint16_t *__restrict__ idx,
+    vals_t<T> val, const int32_t *__restrict__ bpc, int64_t P, int64_t W, int64_t RBK, const T *__restrict__ x,
+    int64_t xn, int64_t nrows, const T *__restrict__ q, const T *__restrict__ d, const T *__restrict__ psum,
+    T QA_cost, T cost_inv, T *__restrict__ Ad, T *__restrict__ pdad, const cg_scalars<T> *__restrict__ status) {
+    constexpr int XW = rb_width<T>(), RB = rb_rows<T>();
+    __shared__ T xs[XW];
+    __shared__ T racc[RB];
+    T *red = racc, *bc = racc + SELL_WAVES;  // block-reduction scratch (before / after the accumulator's use)
+    if (status != nullptr && status->converged) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int blk = (int) blockIdx.x;
+    const int64_t row0 = (int64_t) blk * RBK;
+    const int rows = (int) min<int64_t>(RBK, nrows - row0);
+    // sum(d), sum(q d) from the previous step's RED_BLOCKS partial pairs, in dot_final_kernel's order
+    T sp, sqp;
+    {
+        T s1 = 0, s2 = 0;
+        for (int i = tid; i < RED_BLOCKS; i += SELL_NT) {
+            s1 += psum[i];
+            s2 += psum[RED_BLOCKS + i];
+        }
+        auto bsum = [&](T v) {
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+            if (lane == 0) red[wave] = v;
+            __syncthreads();
+            if (tid == 0) {
+                T t = 0;
+                for (int w2 = 0; w2 < SELL_WAVES; ++w2) t += red[w2];
+                bc[0] = t;
+            }
+            __syncthreads();
+            const T out = bc[0];
+            __syncthreads();
+            return out;
+        };
+        sp = bsum(s1);
+        sqp = bsum(s2);
+    }
+    for (int t = tid; t < RB; t += SELL_NT) racc[t] = T(0);  // visible after the first panel fill's barrier
+    for (int64_t qq = 0; qq < P; ++qq) {
+        const T *xg = x + qq * W;
+        {
+            if (qq > 0) __syncthreads();  // every wave is done with panel qq - 1
+            const int xl = (int) min((int64_t) W, xn - qq * W);
+            using V = __attribute__((ext_vector_type(4))) float;
+            constexpr int EV = 16 / (int) sizeof(T);
+            constexpr int VPER = XW / EV / SELL_NT;
+            static_assert(VPER * EV * SELL_NT == XW, "panel width must be a multiple of 16 B per thread");
+            if (xl == XW && (reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
+                V t[VPER];
+#pragma unroll
+                for (int u = 0; u < VPER; ++u) t[u] = reinterpret_cast<const V *>(xg)[tid + u * SELL_NT];
+#pragma unroll
+                for (int u = 0; u < VPER; ++u) reinterpret_cast<V *>(xs)[tid + u * SELL_NT] = t[u];
+            } else {
+                for (int k = tid; k < XW; k += SELL_NT) xs[k] = k < xl ? xg[k] : T(0);
+            }
+            __syncthreads();
+        }
+        const int cb = bpc[blk * P + qq], ce = bpc[blk * P + qq + 1];
+        for (int c = cb + wave; c < ce; c += SELL_WAVES) {
+            const sell_chunk ch = chunks[c];
+            const int seg = perm[(int64_t) c * 64 + lane];
+            const int64_t base = ch.off + lane;
+            const int last = max(ch.width - 1, 0);
+            const int lastp = max((ch.width >> 1) - 1, 0);
+            const uint32_t *ip = reinterpret_cast<const uint32_t *>(idx) + (ch.off >> 1) + lane;
+            T acc = T(0);
+            for (int j = 0; j < ch.width; j += SELL_UNROLL) {
+                uint16_t ci[SELL_UNROLL];
+                T vi[SELL_UNROLL];
+#pragma unroll
+                for (int u = 0; u < SELL_UNROLL; ++u) vi[u] = sell_val<T, F22>(val, base + (int64_t) min(j + u, last) * 64);
+#pragma unroll
+                for (int u2 = 0; u2 < SELL_UNROLL / 2; ++u2) {
+                    const uint32_t pr = __builtin_nontemporal_load(ip + (int64_t) min((j >> 1) + u2, lastp) * 64);
+                    ci[2 * u2] = (uint16_t) (pr & 0xFFFFu);
+                    ci[2 * u2 + 1] = (uint16_t) (pr >> 16);
+                }
+#pragma unroll
+                for (int u = 0; u < SELL_UNROLL; ++u) {
+                    const T v = j + u < ch.width ? vi[u] : T(0);
+                    acc = fma(v, xs[ci[u]], acc);
+                }
+            }
+            if (seg >= 0) racc[seg] += acc;  // each row once per panel
+        }
+    }
+    __syncthreads();
+    T s1 = 0;
+    for (int t = tid; t < rows; t += SELL_NT) {
+        const int64_t i = row0 + t;
+        const T rw = racc[t], qi = q[i], di = d[i];
+        T v;
+        {
+#pragma clang fp contract(fast)  // cg_fin_dad_kernel's expression
+            v = rw + (QA_cost - qi) * sp - sqp + cost_inv * di;
+            v = T(0) + T(1) * v;
+        }
+        Ad[i] = v;
+        s1 += di * v;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s1 += __shfl_xor(s1, o);
+    __syncthreads();  // every row of the accumulator has been read: reuse it as scratch
+    if (lane == 0) red[wave] = s1;
+    __syncthreads();
+    if (tid == 0) {
+        T t = 0;
+        for (int w2 = 0; w2 < SELL_WAVES; ++w2) t += red[w2];
+        pdad[blk] = t;
+    }
+    // the consumer sums RED_BLOCKS partials: the slots past this launch's blocks are zero
+    if (blk == 0)
+        for (int b = (int) gridDim.x + tid; b < RED_BLOCKS; b += SELL_NT) pdad[b] = T(0);
+}
+
+template <typename T>
+inline void launch_rowblock_fin(const rb_plan<T> &pl, const T *w, int64_t xn, const T *q, const T *d, const T *psum,
+                                T QA_cost, T cost_inv, T *Ad, T *pdad, const cg_scalars<T> *status,
+                                hipStream_t stream) {
+    if (pl.nblk <= 0) return;
+    auto k = pl.val22.get() ? sell_rowblock_fin_kernel<T, true> : sell_rowblock_fin_kernel<T, false>;
+    hipLaunchKernelGGL(k, dim3((unsigned) pl.nblk), dim3(SELL_NT), 0, stream, pl.chunks.get(), pl.perm.get(),
+                       pl.idx16.get(), pl.vals(), pl.bpc.get(), pl.P, pl.W, pl.RBK, w, xn, pl.nrows, q, d, psum,
+                       QA_cost, cost_inv, Ad, pdad, status);
+    MI_LAUNCH_CHECK();
+}
+
+// Host construction (rows = segments s in [0, nrows), gathered vector of length xn); gen as for
+// build_spmv_plan. Returns false (plan left empty) when the rows need more than RED_BLOCKS blocks.
+template <typename T, typename Gen>
+bool build_rowblock_plan(rb_plan<T> &pl, int64_t nrows, int64_t xn, bool fp22, Gen gen, int64_t target_blocks,
+                         hipStream_t stream) {
+    pl = rb_plan<T>{};
+    if (nrows <= 0) return false;
+    const int64_t W = rb_width<T>(), P = std::max<int64_t>(1, ceil_div(std::max<int64_t>(xn, 1), W));
+    const int64_t RBK = std::min<int64_t>(rb_rows<T>(), round_up(ceil_div(nrows, target_blocks), 64));
+    const int64_t nblk = ceil_div(nrows, RBK);
+    if (nblk > RED_BLOCKS) return false;
+    pl.P = P, pl.W = W, pl.RBK = RBK, pl.nblk = nblk, pl.nrows = nrows;
+    std::vector<int32_t> len((size_t) (P * nrows), 0);
+    gen([&](int64_t s, int64_t g, double) { ++len[(size_t) ((g / W) * nrows + s)]; });
+    const int64_t cpb = RBK / 64;  // chunks per (block, panel)
+    std::vector<sell_chunk> chunks((size_t) (nblk * P * cpb));
+    std::vector<int32_t> perm(chunks.size() * 64, -1);
+    std::vector<int64_t> pos((size_t) (P * nrows));
+    std::vector<int32_t> bpc{ 0 };
+    std::vector<int32_t> order;
+    int64_t off = 0, c = 0;
+    for (int64_t b = 0; b < nblk; ++b) {
+        const int64_t r0 = b * RBK, r1 = std::min(nrows, r0 + RBK);
+        for (int64_t qq = 0; qq < P; ++qq) {
+            const int32_t *lq = len.data() + qq * nrows;
+            order.resize((size_t) (r1 - r0));
+            std::iota(order.begin(), order.end(), (int32_t) r0);
+            std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b2) { return lq[a] > lq[b2]; });
+            for (int64_t k = 0; k < cpb; ++k, ++c) {
+                int32_t width = 0;
+                for (int l = 0; l < 64; ++l) {
+                    const int64_t t = k * 64 + l;
+                    if (t < (int64_t) order.size()) width = std::max(width, lq[order[(size_t) t]]);
+                }
+                width = (width + 1) & ~1;  // IDX2 pairs
+                chunks[(size_t) c] = sell_chunk{ off, width, (int32_t) qq };
+                for (int l = 0; l < 64; ++l) {
+                    const int64_t t = k * 64 + l;
+                    if (t < (int64_t) order.size()) {
+                        const int32_t row = order[(size_t) t];
+                        perm[(size_t) (c * 64 + l)] = (int32_t) (row - r0);
+                        pos[(size_t) (qq * nrows + row)] = off + l;
+                    }
+                }
+                off += (int64_t) width * 64;
+            }
+            bpc.push_back((int32_t) c);
+        }
+    }
+    pl.entries = off;
+    const int64_t cap = off + 128;
+    std::vector<uint16_t> i16((size_t) cap, 0);
+    std::vector<T> vr(fp22 ? 0 : (size_t) cap, T(0));
+    std::vector<uint32_t> v22(fp22 ? fp22_words(cap) + 1 : 0, 0u);
+    gen([&](int64_t s, int64_t g, double v) {
+        const int64_t qq = g / W;
+        int64_t &p = pos[(size_t) (qq * nrows + s)];
+        const int64_t t = p;
+        p += 64;
+        i16[(size_t) sell_pair_pos(t)] = (uint16_t) (g - qq * W);
+        if (fp22) {
+            const uint64_t code = fp22_encode_host((float) v);
+            const int64_t gg = t >> 4;
+            const int bit = 22 * (int) (t & 15);
+            const int64_t wi = gg * 11 + (bit >> 5);
+            const int sh = bit & 31;
+            v22[(size_t) wi] |= (uint32_t) (code << sh);
+            if (sh > 10) v22[(size_t) wi + 1] |= (uint32_t) (code >> (32 - sh));
+        } else {
+            vr[(size_t) t] = (T) v;
+        }
+    });
+    auto up = [&](auto &buf, const auto &vec) {
+        using E = typename std::decay_t<decltype(vec)>::value_type;
+        if (vec.empty()) return;
+        buf.alloc((int64_t) vec.size(), stream, false);
+        MI_HIP_CHECK(hipMemcpyAsync(buf.get(), vec.data(), sizeof(E) * vec.size(), hipMemcpyHostToDevice, stream));
+    };
+    up(pl.chunks, chunks);
+    up(pl.perm, perm);
+    up(pl.idx16, i16);
+    up(pl.val, vr);
+    up(pl.val22, v22);
+    up(pl.bpc, bpc);
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    return true;
+}
+
 }  // namespace plssvm_mi

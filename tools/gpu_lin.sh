@@ -4,8 +4,8 @@ set -e
 export TMPDIR=/tmp
 root=$(pwd)
 out=$root/gpurun_out/lin; mkdir -p $out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_sparse.py > $out/pytest.log 2>&1
-for nb in 256 512; do
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_sparse.py tests/test_gpu_golden.py -k "not geometries" > $out/pytest.log 2>&1
+for nb in 256 128; do
 PLSSVM_MI_SELL_BLOCKS=$nb timeout -k 10 200 python bench.py --config csr_linear_1m --no-cpu --steps 300 --warmup 3 > $out/lin$nb.json 2> $out/lin$nb.err
 done
 cd /tmp
