@@ -331,12 +331,13 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
                                                                  const uint16_t *__restrict__ hjl,
                                                                  const T *__restrict__ hv, const T *__restrict__ w,
                                                                  int64_t m, int64_t r0, int64_t R, int64_t nW,
-                                                                 T *__restrict__ hs,
+                                                                 int64_t RB, T *__restrict__ hs,
                                                                  const cg_scalars<T> *__restrict__ status) {
-    constexpr int CW = exp_cw_of<T, RBB>(), RB = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64, PER = CW / NT;
+    // RB (rows per block, a multiple of 16) <= RBC, the accumulator's capacity
+    constexpr int CW = exp_cw_of<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64, PER = CW / NT;
     static_assert(CW <= 65536, "window-local partner indices are 16-bit");
     __shared__ T wl[CW];
-    __shared__ T racc[RB];
+    __shared__ T racc[RBC];
     if (status != nullptr && status->converged) return;
     const int64_t I = xcd_remap(blockIdx.x, gridDim.x);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -746,25 +747,30 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
     Li.reset(), Lj.reset(), Lh.reset(), uidx.reset(), ukey.reset(), ukey_s.reset(), uidx_s.reset();
 
     // ---- cells: blocks of RB rows x windows of CW partners, rows padded to 4 slots per cell ----
-    // geometry: the largest row block whose block count still covers ~all CUs (PLSSVM_MI_EXP_RBB forces)
+    // geometry: rows per block RB = the rank's rows spread evenly over the CUs (a multiple of 16: one
+    // round of blocks, every CU busy), in the smallest accumulator class that holds it (the rest of the
+    // LDS is the window); past the largest class, blocks of that size in several rounds.
+    // PLSSVM_MI_EXP_RBB forces a class (RB = its capacity).
     {
         int cus = 256;
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             cus = prop.multiProcessorCount;
-        ex.RBB = 4096;
-        for (int rbb : { 32768, 16384, 8192 }) {
-            if (ceil_div(std::max<int64_t>(R, 1), rbb / (int64_t) sizeof(T)) * 10 >= (int64_t) cus * 9) {
+        const int es = (int) sizeof(T);
+        const int64_t want = round_up(ceil_div(std::max<int64_t>(R, 1), (int64_t) cus), (int64_t) EXP_NWV);
+        ex.RBB = 32768;
+        for (int rbb : { 4096, 8192, 16384, 32768 }) {
+            if (want * es <= rbb) {
                 ex.RBB = rbb;
                 break;
             }
         }
+        ex.RB = (int) std::min<int64_t>(want, ex.RBB / es);
         if (const char *e = std::getenv("PLSSVM_MI_EXP_RBB")) {
             const int v = std::atoi(e);
-            if (v == 4096 || v == 8192 || v == 16384 || v == 32768) ex.RBB = v;
+            if (v == 4096 || v == 8192 || v == 16384 || v == 32768) ex.RBB = v, ex.RB = v / es;
         }
-        ex.RB = ex.RBB / (int) sizeof(T);
-        ex.CW = exp_cw_host(ex.RBB, (int) sizeof(T));
+        ex.CW = exp_cw_host(ex.RBB, es);
     }
     const int64_t CW = ex.CW, RB = ex.RB;
     ex.nW = ceil_div(std::max<int64_t>(m, 1), CW);
@@ -828,7 +834,8 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
     if (ex.nblk > 0 && !(exp_ablate() & 1)) {
         auto launch = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned) ex.nblk), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(), ex.hrow.get(),
-                               ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, ex.hs.get(), status);
+                               ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, (int64_t) ex.RB, ex.hs.get(),
+                               status);
         };
         switch (ex.RBB) {
             case 4096: launch(exp_hcell_kernel<T, 4096>); break;
