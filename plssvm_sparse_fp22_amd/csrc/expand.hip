@@ -331,15 +331,21 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
                                                                  const uint16_t *__restrict__ hjl,
                                                                  const T *__restrict__ hv, const T *__restrict__ w,
                                                                  int64_t m, int64_t r0, int64_t R, int64_t nW,
-                                                                 int64_t RB, T *__restrict__ hs,
+                                                                 int64_t RB, int64_t nI, int G, T *__restrict__ hs,
+                                                                 T *__restrict__ hslab,
                                                                  const cg_scalars<T> *__restrict__ status) {
-    // RB (rows per block, a multiple of 16) <= RBC, the accumulator's capacity
+    // RB (rows per block, a multiple of 16) <= RBC, the accumulator's capacity. G > 1 window groups:
+    // block (I, g) streams only windows [g nW / G, (g + 1) nW / G) of its rows and writes its row sums
+    // to hslab[g][rows] (summed in g order by exp_hslab_reduce_kernel); the blocks of one XCD share g,
+    // so they share w's windows in L2
     constexpr int CW = exp_cw_of<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64, PER = CW / NT;
     static_assert(CW <= 65536, "window-local partner indices are 16-bit");
     __shared__ T wl[CW];
     __shared__ T racc[RBC];
     if (status != nullptr && status->converged) return;
-    const int64_t I = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t bx = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t I = bx % nI, g = bx / nI;
+    const int64_t W0 = g * nW / G, W1 = (g + 1) * nW / G;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int t = tid; t < RB; t += NT) racc[t] = T(0);
     T reg[PER];
@@ -355,13 +361,13 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
         for (int q = 0; q < PER; ++q) wl[q * NT + tid] = reg[q];
     };
     const int64_t *wo = woff + (I * EXP_NWV + wave) * (nW + 1);
-    const int64_t s_end = wo[nW];
+    const int64_t s_end = wo[W1];
     // one step of the stream in registers: chunk cp (= step start + lane), loads clamped to the stream
     int rl_n = 0;
     u32x2 jj_n = { 0u, 0u };
     T h_n[4] = { T(0), T(0), T(0), T(0) };
     auto fetch = [&](int64_t c) {
-        if (s_end == wo[0]) return;  // empty stream (wave-uniform)
+        if (s_end == wo[W0]) return;  // empty stream (wave-uniform)
         const int64_t cl = c < s_end ? c : s_end - 1;
         rl_n = (int) __builtin_nontemporal_load(hrow + cl);
         jj_n = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hjl + 4 * cl));
@@ -374,12 +380,14 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             h_n[0] = v0.x, h_n[1] = v0.y, h_n[2] = v1.x, h_n[3] = v1.y;
         }
     };
-    load_win(0);
-    store_win();
-    fetch(wo[0] + lane);
+    if (W0 < W1) {
+        load_win(W0);
+        store_win();
+        fetch(wo[W0] + lane);
+    }
     __syncthreads();
-    for (int64_t W = 0; W < nW; ++W) {
-        if (W + 1 < nW) load_win(W + 1);  // lands in registers while this window is processed
+    for (int64_t W = W0; W < W1; ++W) {
+        if (W + 1 < W1) load_win(W + 1);  // lands in registers while this window is processed
         const int64_t c_end = wo[W + 1];
         const T *wb = wl;
         for (int64_t cb = wo[W]; cb < c_end; cb += 64) {  // wave-uniform trip count
@@ -406,7 +414,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             const int rprev = __shfl_up(rl, 1);
             if (rl >= 0 && (lane == 0 || rprev != rl)) racc[rl] += sacc;  // rows of this wave only
         }
-        if (W + 1 < nW) {
+        if (W + 1 < W1) {
             __syncthreads();  // every wave is done with window W
             store_win();
         }
@@ -414,7 +422,23 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     }
     const int64_t rb0 = I * RB;
     const int rows = (int) min<int64_t>(RB, R - rb0);
-    for (int t = tid; t < rows; t += NT) hs[r0 + rb0 + t] = racc[t];
+    if (G == 1) {
+        for (int t = tid; t < rows; t += NT) hs[r0 + rb0 + t] = racc[t];
+    } else {
+        for (int t = tid; t < rows; t += NT) hslab[g * R + rb0 + t] = racc[t];
+    }
+}
+
+// hs[r0 + i] = sum_g hslab[g][i], g in order
+template <typename T>
+__global__ __launch_bounds__(256) void exp_hslab_reduce_kernel(const T *__restrict__ hslab, int64_t R, int G, int64_t r0,
+                                                               T *__restrict__ hs, const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R) return;
+    T a = 0;
+    for (int g = 0; g < G; ++g) a += hslab[g * R + i];
+    hs[r0 + i] = a;
 }
 
 // raw_i for rows [r0, r1) (0 elsewhere), raw holding J_i there (the CSR pass): base + scale (J_i +
@@ -749,32 +773,48 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
     // ---- cells: blocks of RB rows x windows of CW partners, rows padded to 4 slots per cell ----
     // geometry: rows per block RB = the rank's rows spread evenly over the CUs (a multiple of 16: one
     // round of blocks, every CU busy), in the smallest accumulator class that holds it (the rest of the
-    // LDS is the window); past the largest class, blocks of that size in several rounds.
-    // PLSSVM_MI_EXP_RBB forces a class (RB = its capacity).
+    // LDS is the window). Few rows (an 8-GPU rank's share: blocks of less than half the largest class):
+    // the largest class instead, and G window groups per row block to fill the CUs — every row block
+    // restages all of w once, so fewer, bigger row blocks restage less. PLSSVM_MI_EXP_RBB forces a class.
     {
         int cus = 256;
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
             cus = prop.multiProcessorCount;
         const int es = (int) sizeof(T);
-        const int64_t want = round_up(ceil_div(std::max<int64_t>(R, 1), (int64_t) cus), (int64_t) EXP_NWV);
-        ex.RBB = 32768;
-        for (int rbb : { 4096, 8192, 16384, 32768 }) {
-            if (want * es <= rbb) {
-                ex.RBB = rbb;
-                break;
+        const int64_t Rr = std::max<int64_t>(R, 1), cap_max = 32768 / es;
+        const int64_t want = round_up(ceil_div(Rr, (int64_t) cus), (int64_t) EXP_NWV);
+        ex.G = 1;
+        if (want * 2 > cap_max) {
+            ex.RBB = 32768;
+            for (int rbb : { 4096, 8192, 16384, 32768 }) {
+                if (want * es <= rbb) {
+                    ex.RBB = rbb;
+                    break;
+                }
             }
+            ex.RB = (int) std::min<int64_t>(want, ex.RBB / es);
+        } else {
+            ex.RBB = 32768;
+            const int64_t nI = ceil_div(Rr, cap_max);
+            ex.RB = (int) round_up(ceil_div(Rr, nI), (int64_t) EXP_NWV);
+            ex.G = (int) std::max<int64_t>(1, cus / nI);
         }
-        ex.RB = (int) std::min<int64_t>(want, ex.RBB / es);
         if (const char *e = std::getenv("PLSSVM_MI_EXP_RBB")) {
             const int v = std::atoi(e);
-            if (v == 4096 || v == 8192 || v == 16384 || v == 32768) ex.RBB = v, ex.RB = v / es;
+            if (v == 4096 || v == 8192 || v == 16384 || v == 32768) ex.RBB = v, ex.RB = v / es, ex.G = 1;
+        }
+        if (const char *e = std::getenv("PLSSVM_MI_EXP_G")) {  // window groups (tests)
+            const int v = std::atoi(e);
+            if (v >= 1) ex.G = v;
         }
         ex.CW = exp_cw_host(ex.RBB, es);
     }
     const int64_t CW = ex.CW, RB = ex.RB;
     ex.nW = ceil_div(std::max<int64_t>(m, 1), CW);
     ex.nblk = ceil_div(R, RB);
+    ex.G = (int) std::max<int64_t>(1, std::min<int64_t>(ex.G, ex.nW));
+    if (ex.G > 1) ex.hslab.alloc((int64_t) ex.G * R, stream, false);
     const int64_t nbv = ex.nblk * EXP_NWV, ncnt = ex.nblk * RB * ex.nW;
     {
         dev_buf<int64_t> cnt, coff;
@@ -833,9 +873,9 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
     auto &ex = csr.ex;
     if (ex.nblk > 0 && !(exp_ablate() & 1)) {
         auto launch = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3((unsigned) ex.nblk), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(), ex.hrow.get(),
-                               ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, (int64_t) ex.RB, ex.hs.get(),
-                               status);
+            hipLaunchKernelGGL(kern, dim3((unsigned) (ex.nblk * ex.G)), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
+                               ex.hrow.get(), ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, (int64_t) ex.RB,
+                               ex.nblk, ex.G, ex.hs.get(), ex.hslab.get(), status);
         };
         switch (ex.RBB) {
             case 4096: launch(exp_hcell_kernel<T, 4096>); break;
@@ -844,6 +884,11 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
             default: launch(exp_hcell_kernel<T, 16384>);
         }
         MI_LAUNCH_CHECK();
+        if (ex.G > 1 && r1 > r0) {
+            hipLaunchKernelGGL(exp_hslab_reduce_kernel<T>, dim3((unsigned) ceil_div(r1 - r0, 256)), dim3(256), 0, stream,
+                               ex.hslab.get(), r1 - r0, ex.G, r0, ex.hs.get(), status);
+            MI_LAUNCH_CHECK();
+        }
     } else if (r1 > r0) {
         MI_HIP_CHECK(hipMemsetAsync(ex.hs.get() + r0, 0, sizeof(T) * (size_t) (r1 - r0), stream));
     }

@@ -64,13 +64,15 @@ struct exp_data {
     // slots (pads: j = 0, H = 0); each wave's stream is one contiguous range across the windows
     int64_t slots = 0, nchunks = 0, nblk = 0, nW = 0;
     int RBB = 16384, RB = 0, CW = 0;  // geometry (see above): accumulator bytes, rows per block, window
+    int G = 1;                         // window groups per row block (G > 1: row sums via hslab)
+    dev_buf<T> hslab;                  // [G][rows] partial row sums of the window groups
     dev_buf<uint16_t> hjl;            // [slots] j - W * CW
     dev_buf<T> hv;                    // [slots] H_ij
     dev_buf<uint16_t> hrow;           // [nchunks] block-local row of each 4-slot chunk
     dev_buf<int64_t> woff;            // [nblk][EXP_NWV][nW + 1] first chunk of each (block, wave, window)
     int64_t bytes() const {
         return mom.bytes() + M.bytes() + hdiag.bytes() + phin.bytes() + wv.bytes() + hs.bytes() + hjl.bytes() + hv.bytes() +
-               hrow.bytes() + woff.bytes();
+               hrow.bytes() + woff.bytes() + hslab.bytes();
     }
 };
 
