@@ -3,7 +3,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -27,6 +30,19 @@ struct mi_error : std::runtime_error {
     } while (0)
 
 #define MI_LAUNCH_CHECK() MI_HIP_CHECK(hipGetLastError())
+
+// setup phase timer: PLSSVM_MI_TIMING=1 prints "[plssvm_mi] <phase> <seconds>" to stderr (measurements)
+struct phase_timer {
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    phase_timer() : on(std::getenv("PLSSVM_MI_TIMING") != nullptr), t(std::chrono::steady_clock::now()) {}
+    void mark(const char *what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[plssvm_mi] %s %.3f\n", what, std::chrono::duration<double>(now - t).count());
+        t = now;
+    }
+};
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }

@@ -529,6 +529,7 @@ bool engine<T>::expansion_eligible() {
 template <typename T>
 void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
     auto &ex = csr.ex;
+    phase_timer pt;
     const phi_fn phi = make_phi<T>(kernel, degree, gamma, coef0);
     ex.M.alloc(std::max<int64_t>(d, 1) * ex.KM, stream);
     ex.mom.alloc(std::max<int64_t>(d, 1) * ex.KM, stream);
@@ -670,6 +671,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         P += ns;
     }
     keys.reset(), keys_s.reset(), vals.reset(), vals_s.reset(), hp.reset(), hsel.reset(), tmp.reset();
+    pt.mark("expansion: column join (blocks)");
     if (P > INT32_MAX) throw mi_error(-5, "more than 2^31 multi-feature pairs on one rank: use more GPUs");
 
     // ---- symmetric rows [r0, r1), padded to 8 slots ----
@@ -769,6 +771,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         }
     }
     Li.reset(), Lj.reset(), Lh.reset(), uidx.reset(), ukey.reset(), ukey_s.reset(), uidx_s.reset();
+    pt.mark("expansion: symmetric rows");
 
     // ---- cells: blocks of RB rows x windows of CW partners, rows padded to 4 slots per cell ----
     // geometry: rows per block RB = the rank's rows spread evenly over the CUs (a multiple of 16: one
@@ -851,6 +854,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         MI_HIP_CHECK(hipStreamSynchronize(stream));
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
+    pt.mark("expansion: cells");
     csr.pairs = ex.pairs;
     csr.slots = ex.slots;
     csr.rbf_factored = kernel == 2;

@@ -569,6 +569,7 @@ void host_check_csr(const int64_t *rowptr, const int32_t *col, int64_t n, int64_
 template <typename T>
 void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void *val, int val_fmt, int64_t n_,
                           int64_t d_) {
+    phase_timer pt;
     host_check_csr<T>(rowptr, col, n_, d_);
     if (!val && rowptr[n_] > 0) throw mi_error(-1, "CSR values missing");
     if (val_fmt != PLSSVM_MI_VAL_REAL && val_fmt != PLSSVM_MI_VAL_FP22) throw mi_error(-1, "unknown value format");
@@ -620,6 +621,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                            csr.rowptr.get(), csr.rvals(), m, gamma, norms.get(), csr.e.get());
     MI_LAUNCH_CHECK();
     finish_setup();  // row split r0, r1
+    pt.mark("setup_csr: check + upload + norms");
 
     if (factored()) {
         // factored linear: w = X_rows^T p over rows [csc_r0, csc_r1) — all rows for
@@ -693,6 +695,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         MI_HIP_CHECK(hipMemcpyAsync(csr.cval.get(), cval_real.data(), sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice,
                                     stream));
     MI_HIP_CHECK(hipStreamSynchronize(stream));
+    pt.mark("setup_csr: host CSC");
 
     {
         // Gram pattern: row blocks owned by this rank, balanced by column-join incidences
@@ -737,6 +740,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             csr.est_bytes = use_exp ? estimate_expansion_bytes(rowptr, col, colptr, crow, inc_total)
                                     : csr.pair_bound * (int64_t) (2 * (2 + sizeof(T))) + max_inc * 48;
         }
+        pt.mark("setup_csr: incidences + size estimate");
         const bool forced = sparse_algo == 1 || sparse_algo == 2;
         bool stored = false;
         if (sparse_algo != 3 && (forced || csr.est_bytes <= budget)) {
@@ -765,7 +769,9 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                                 for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit(i - r0, (int64_t) col[k], (double) hval(k));
                         },
                         blocks, stream, 0, csr.ex.KM, 1);
+                    pt.mark("setup_csr: SELL plans");
                     build_expansion(cpos_d.get(), max_inc);
+                    pt.mark("setup_csr: expansion");
                 } else {
                     build_gram_blocks(cpos_d.get(), max_inc);
                 }
