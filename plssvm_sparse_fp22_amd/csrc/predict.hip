@@ -100,6 +100,7 @@ __global__ __launch_bounds__(256) void predict_linear_kernel(const T *__restrict
 
 // sparse data: partial[b][lane] = sum_{i in row block b} alpha_i k(x_i, z_lane); ZT = [d][64]
 constexpr int PRED_ROWS = 256;  // rows per workgroup
+constexpr int PRED_STEP = 8;    // CSR entries per wave step (gathers in flight)
 template <typename T>
 __global__ __launch_bounds__(256) void predict_csr_kernel(kfun<T> kf, const int64_t *__restrict__ rowptr,
                                                           const int32_t *__restrict__ col, const T *__restrict__ val,
@@ -113,13 +114,46 @@ __global__ __launch_bounds__(256) void predict_csr_kernel(kfun<T> kf, const int6
     T acc = 0;
     for (int64_t i = r0 + wave; i < r1; i += 4) {
         T s = 0;
-        const int64_t e1 = rowptr[i + 1];
-        for (int64_t k = rowptr[i]; k < e1; ++k) s = fma(val[k], ZT[(int64_t) col[k] * 64 + lane], s);
+        const int64_t e0 = rowptr[i], e1 = rowptr[i + 1];
+        // 8 entries per step: their (wave-uniform) column/value loads, then 8 independent ZT gathers in
+        // flight, then the fma chain in entry order (a masked tail entry adds 0 * ZT = 0 exactly)
+        for (int64_t k = e0; k < e1; k += PRED_STEP) {
+            int32_t c[PRED_STEP];
+            T v[PRED_STEP], g[PRED_STEP];
+#pragma unroll
+            for (int u = 0; u < PRED_STEP; ++u) {
+                const int64_t kk = min(k + u, e1 - 1);
+                c[u] = col[kk];
+                v[u] = k + u < e1 ? val[kk] : T(0);
+            }
+#pragma unroll
+            for (int u = 0; u < PRED_STEP; ++u) g[u] = ZT[(int64_t) c[u] * 64 + lane];
+#pragma unroll
+            for (int u = 0; u < PRED_STEP; ++u) s = fma(v[u], g[u], s);
+        }
         acc = fma(alpha[i], kval(kf, s, norms[i], nz), acc);
     }
     red[wave][lane] = acc;
     __syncthreads();
     if (wave == 0) partial[(int64_t) blockIdx.x * 64 + lane] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+// ZT[col][p] = z_p[col] and |z_p|^2 (sequential fma in column order: the densified chain with its zero
+// terms dropped, exactly) for the chunk's points p < c; lanes >= c get norm 0 (ZT pre-zeroed)
+template <typename T>
+__global__ __launch_bounds__(64) void zt_scatter_kernel(const int64_t *__restrict__ zr, const int32_t *__restrict__ zc,
+                                                       const T *__restrict__ zv, int64_t p0, int64_t c,
+                                                       T *__restrict__ ZT, T *__restrict__ nz) {
+    const int p = threadIdx.x;
+    T v = 0;
+    if (p < c) {
+        for (int64_t e = zr[p0 + p]; e < zr[p0 + p + 1]; ++e) {
+            const T x = zv[e];
+            ZT[(int64_t) zc[e] * 64 + p] = x;
+            v = fma(x, x, v);
+        }
+    }
+    nz[p] = v;
 }
 
 // out[p] = bias + alpha_m k(x_m, z_p) + sum_b partial[b][p] (block order); one workgroup per point
@@ -303,9 +337,38 @@ void engine<T>::predict(const T *alpha_host, T bias, const T *Z, const int64_t *
         return;
     }
 
-    // sparse data: 64 points per launch, feature-major ZT[d][64]
+    // sparse data: the points as one device CSR (host: nonzeros in column order, FP22 decoded, range
+    // checked), then per 64 points the feature-major ZT[d][64] is scattered on the device
+    std::vector<int64_t> zr((size_t) np + 1, 0);
+    std::vector<int32_t> zc;
+    std::vector<T> zv;
+    for (int64_t p = 0; p < np; ++p) {
+        if (Z) {
+            for (int64_t k = 0; k < d; ++k)
+                if (Z[p * d + k] != T(0)) zc.push_back((int32_t) k), zv.push_back(Z[p * d + k]);
+        } else {
+            for (int64_t e = zrowptr[p]; e < zrowptr[p + 1]; ++e) {
+                if (zcol[e] < 0 || zcol[e] >= d) throw mi_error(-1, "CSR column index out of range");
+                zc.push_back(zcol[e]);
+                zv.push_back(zfmt == PLSSVM_MI_VAL_FP22 ? (T) fp22_get(static_cast<const uint32_t *>(zval), e)
+                                                        : static_cast<const T *>(zval)[e]);
+            }
+        }
+        zr[(size_t) p + 1] = (int64_t) zc.size();
+    }
+    const int64_t znnz = (int64_t) zc.size();
+    dev_buf<int64_t> zrd;
+    dev_buf<int32_t> zcd;
+    dev_buf<T> zvd;
+    zrd.alloc(np + 1, stream, false);
+    zcd.alloc(std::max<int64_t>(znnz, 1), stream, false);
+    zvd.alloc(std::max<int64_t>(znnz, 1), stream, false);
+    MI_HIP_CHECK(hipMemcpyAsync(zrd.get(), zr.data(), sizeof(int64_t) * (size_t) (np + 1), hipMemcpyHostToDevice, stream));
+    if (znnz > 0) {
+        MI_HIP_CHECK(hipMemcpyAsync(zcd.get(), zc.data(), sizeof(int32_t) * (size_t) znnz, hipMemcpyHostToDevice, stream));
+        MI_HIP_CHECK(hipMemcpyAsync(zvd.get(), zv.data(), sizeof(T) * (size_t) znnz, hipMemcpyHostToDevice, stream));
+    }
     const int64_t nblk = std::max<int64_t>(1, ceil_div(m, PRED_ROWS));
-    std::vector<T> zt((size_t) (d * 64)), nzh(64);
     dev_buf<T> ztd, nzd, pd, od;
     ztd.alloc(d * 64, stream, false);
     nzd.alloc(64, stream, false);
@@ -313,15 +376,10 @@ void engine<T>::predict(const T *alpha_host, T bias, const T *Z, const int64_t *
     od.alloc(64, stream, false);
     for (int64_t p0 = 0; p0 < np; p0 += 64) {
         const int64_t c = std::min<int64_t>(64, np - p0);
-        std::fill(zt.begin(), zt.end(), T(0));
-        for (int64_t p = 0; p < c; ++p) zget(p0 + p, zt.data() + p, 64);
-        for (int64_t p = 0; p < 64; ++p) {
-            T v = 0;
-            for (int64_t k = 0; k < d; ++k) v = std::fma(zt[k * 64 + p], zt[k * 64 + p], v);
-            nzh[p] = v;
-        }
-        MI_HIP_CHECK(hipMemcpyAsync(ztd.get(), zt.data(), sizeof(T) * (size_t) (d * 64), hipMemcpyHostToDevice, stream));
-        MI_HIP_CHECK(hipMemcpyAsync(nzd.get(), nzh.data(), sizeof(T) * 64, hipMemcpyHostToDevice, stream));
+        MI_HIP_CHECK(hipMemsetAsync(ztd.get(), 0, sizeof(T) * (size_t) (d * 64), stream));
+        hipLaunchKernelGGL(zt_scatter_kernel<T>, dim3(1), dim3(64), 0, stream, zrd.get(), zcd.get(), zvd.get(), p0, c,
+                           ztd.get(), nzd.get());
+        MI_LAUNCH_CHECK();
         if (m > 0)
             hipLaunchKernelGGL(predict_csr_kernel<T>, dim3((unsigned) ceil_div(m, PRED_ROWS)), dim3(256), 0, stream, kf(),
                                csr.rowptr.get(), csr.col.get(), csr.val.get(), m, ztd.get(), nzd.get(), norms.get(),
