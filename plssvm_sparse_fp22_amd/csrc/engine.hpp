@@ -118,6 +118,10 @@ struct engine : engine_base {
     void expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);
     void expansion_dominant(const T *p, const cg_scalars<T> *status);  // the remainder stream
     void expansion_moments(const T *w, const cg_scalars<T> *status);   // column moments (SELL CSC pass)
+    // predict through the expansion (expand.hip); false: not applicable, predict brute force
+    bool expansion_predict(const T *alpha_dev, T alpha_m, T bias, const int64_t *zr_dev, const int32_t *zc_dev,
+                           const T *zv_dev, int64_t np, int64_t max_nnz_z, double zabs_max, double znorm_max, T nlast,
+                           T *out_dev);
     // raw[i] = sum_j k_ij p_j, i < m (with_base = false: only the overlap terms, PLSSVM_MI_PART_OVERLAP)
     void sparse_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base = true);
     void sparse_dominant(const T *p, const cg_scalars<T> *status);  // the dominant sparse kernel

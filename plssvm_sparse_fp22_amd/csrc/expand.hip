@@ -943,12 +943,292 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     allgather_rows(raw.get());
 }
 
+// ---- predict through the expansion (csvm::predict on sparse poly / rbf models) -----------------------
+// sum_{i<m} alpha_i k(x_i, z) = base_z (S + J_z + sum_{i sharing >= 2 features with z} w_i H_iz), with
+// w = alpha e (rbf) / alpha (poly), S = sum w, J_z = sum_{f in z} sum_k coef_k z_f^k M_k(f) from the
+// model's column moments M_k(f) = sum_{i in col f} x_if^k w_i (once per call), and H_iz = phi(s_iz) -
+// sum_{f shared} phi(x_if z_f) for the support vectors sharing two or more features with z: per point,
+// the CSC columns of z's features are walked with an LDS bitmap of rows (seen once / twice), the repeat
+// rows are enumerated in ascending order and their exact s_iz and phi sums formed by merging row i with
+// z. Fixed orders throughout: deterministic. O(nnz_z K + sum_{f in z} c_f) per point instead of O(nnz_X).
+constexpr int PRED_NT = 1024;
+constexpr int PRED_BMW = 24576;             // bitmap words (96 KiB): rows per pass = 786 432
+constexpr int PRED_ZCAP = 2048;             // entries of one point held in LDS
+constexpr int PRED_MCAP = 4096;             // repeat rows per pass
+
+template <typename T>
+__global__ __launch_bounds__(256) void exp_pred_w_kernel(const T *__restrict__ alpha, const T *__restrict__ e, int64_t m,
+                                                         T *__restrict__ w) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) w[i] = e != nullptr ? alpha[i] * e[i] : alpha[i];
+}
+
+// M[f][k] = coef_{k+1} sum_{t in col f} cval[t]^(k+1) w[crow[t]], one wave per column (lane-strided,
+// then a butterfly: fixed order)
+template <typename T>
+__global__ __launch_bounds__(256) void exp_pred_moments_kernel(const int64_t *__restrict__ colptr,
+                                                               const int32_t *__restrict__ crow,
+                                                               const T *__restrict__ cval, const T *__restrict__ w,
+                                                               int64_t d, int K, int KM, coefs cf, T *__restrict__ M) {
+    const int64_t f = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (f >= d) return;
+    double acc[EXP_KMAX];
+#pragma unroll
+    for (int k = 0; k < EXP_KMAX; ++k) acc[k] = 0.0;
+    for (int64_t t = colptr[f] + lane; t < colptr[f + 1]; t += 64) {
+        const double v = (double) cval[t];
+        double pw = v * (double) w[crow[t]];
+#pragma unroll
+        for (int k = 0; k < EXP_KMAX; ++k) {
+            if (k < K) acc[k] += pw;
+            pw *= v;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < EXP_KMAX; ++k) {
+        if (k < K) {  // K is uniform
+            double a = acc[k];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o);
+            if (lane == 0) M[f * KM + k] = (T) (cf.c[k + 1] * a);
+        }
+    }
+    if (lane == 0)
+        for (int k = K; k < KM; ++k) M[f * KM + k] = T(0);
+}
+
+template <typename T>
+__device__ __forceinline__ double pred_block_sum(double v, double *red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int w2 = 0; w2 < PRED_NT / 64; ++w2) s += red[w2];
+    return s;
+}
+
+// one point per workgroup; zr/zc/zv: the points' CSR (columns ascending); S: sum w (device scalar);
+// flag[0] set when a pass held more than PRED_MCAP repeat rows (the caller then recomputes brute force)
+template <typename T>
+__global__ __launch_bounds__(PRED_NT) void exp_pred_point_kernel(
+    const int64_t *__restrict__ zr, const int32_t *__restrict__ zc, const T *__restrict__ zv, const int64_t *__restrict__ colptr,
+    const int32_t *__restrict__ crow, const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const T *__restrict__ val, const T *__restrict__ w, const T *__restrict__ M, int KM, phi_fn phi, int64_t m,
+    const T *__restrict__ S, const T *__restrict__ xlast, T nlast, T alpha_m, kfun<T> kf, T kappa, T bias,
+    T *__restrict__ out, int *__restrict__ flag) {
+    __shared__ uint32_t bm[PRED_BMW];
+    __shared__ int32_t zcol_s[PRED_ZCAP];
+    __shared__ T zval_s[PRED_ZCAP];
+    __shared__ int32_t multi[PRED_MCAP];
+    __shared__ int64_t zoff[PRED_ZCAP + 1];
+    __shared__ double red[PRED_NT / 64];
+    __shared__ int nmulti, wcnt[PRED_NT];
+    const int tid = threadIdx.x;
+    const int64_t p = blockIdx.x;
+    const int64_t e0 = zr[p];
+    const int nz = (int) (zr[p + 1] - e0);
+    for (int e = tid; e < nz; e += PRED_NT) zcol_s[e] = zc[e0 + e], zval_s[e] = zv[e0 + e];
+    __syncthreads();
+    // |z|^2 (column order) and x_m . z (entry order), thread 0
+    if (tid == 0) {
+        T nzz = 0, dl = 0;
+        for (int e = 0; e < nz; ++e) {
+            nzz = fma(zval_s[e], zval_s[e], nzz);
+            dl = fma(xlast[zcol_s[e]], zval_s[e], dl);
+        }
+        red[0] = (double) nzz;
+        red[1] = (double) dl;
+        // CSC offsets of z's columns (flattened incidences)
+        int64_t acc = 0;
+        for (int e = 0; e < nz; ++e) {
+            zoff[e] = acc;
+            acc += colptr[zcol_s[e] + 1] - colptr[zcol_s[e]];
+        }
+        zoff[nz] = acc;
+    }
+    __syncthreads();
+    const T nzz = (T) red[0], dl = (T) red[1];
+    const int64_t inc = zoff[nz];
+    // J_z = sum_e z_e (M0 + z_e (M1 + ...)) in the real type's Horner order
+    double js = 0.0;
+    for (int e = tid; e < nz; e += PRED_NT) {
+        const T z = zval_s[e];
+        const T *Mf = M + (int64_t) zcol_s[e] * KM;
+        T h = Mf[KM - 1];
+        for (int k = KM - 2; k >= 0; --k) h = fma(h, z, Mf[k]);
+        js += (double) (h * z);
+    }
+    const double J = pred_block_sum<T>(js, red);
+    double hs = 0.0;
+    const int64_t BMBITS = (int64_t) PRED_BMW * 32;
+    for (int64_t R0 = 0; R0 < m; R0 += BMBITS) {
+        const int64_t R1 = min(m, R0 + BMBITS);
+        for (int q = tid; q < PRED_BMW; q += PRED_NT) bm[q] = 0u;
+        if (tid == 0) nmulti = 0;
+        __syncthreads();
+        // rows seen once -> bit set; seen again -> appended (duplicates for 3+ shared features)
+        for (int64_t t = tid; t < inc; t += PRED_NT) {
+            int lo = 0, hi = nz - 1;  // entry e with zoff[e] <= t < zoff[e + 1]
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (zoff[mid] <= t) lo = mid;
+                else hi = mid - 1;
+            }
+            const int64_t i = crow[colptr[zcol_s[lo]] + (t - zoff[lo])];
+            if (i < R0 || i >= R1) continue;
+            const uint32_t bit = 1u << ((i - R0) & 31);
+            const uint32_t old = atomicOr(&bm[(i - R0) >> 5], bit);
+            if (old & bit) {
+                const int q = atomicAdd(&nmulti, 1);
+                if (q < PRED_MCAP) multi[q] = (int32_t) i;
+            }
+        }
+        __syncthreads();
+        const int nm = nmulti;
+        if (nm > PRED_MCAP) {
+            if (tid == 0) flag[0] = 1;
+            return;  // uniform: every thread read the same nmulti
+        }
+        // the repeat rows as a set in the bitmap, then enumerated in ascending row order
+        for (int q = tid; q < PRED_BMW; q += PRED_NT) bm[q] = 0u;
+        __syncthreads();
+        for (int q = tid; q < nm; q += PRED_NT) {
+            const int64_t i = multi[q] - R0;
+            atomicOr(&bm[i >> 5], 1u << (i & 31));
+        }
+        __syncthreads();
+        constexpr int WPT = PRED_BMW / PRED_NT;
+        int c = 0;
+        for (int q = 0; q < WPT; ++q) c += __popc(bm[tid * WPT + q]);
+        wcnt[tid] = c;
+        __syncthreads();
+        if (tid == 0) {  // exclusive scan of the 1024 counts
+            int a = 0;
+            for (int q = 0; q < PRED_NT; ++q) {
+                const int v = wcnt[q];
+                wcnt[q] = a;
+                a += v;
+            }
+            nmulti = a;
+        }
+        __syncthreads();
+        {
+            int pos = wcnt[tid];
+            for (int q = 0; q < WPT; ++q) {
+                uint32_t word = bm[tid * WPT + q];
+                while (word) {
+                    const int b = __ffs(word) - 1;
+                    word &= word - 1;
+                    multi[pos++] = (int32_t) (R0 + (int64_t) (tid * WPT + q) * 32 + b);
+                }
+            }
+        }
+        __syncthreads();
+        const int U = nmulti;
+        // H_iz = phi(s) - sum phi(x_if z_f) over the shared features (fp64), times w_i
+        for (int q = tid; q < U; q += PRED_NT) {
+            const int64_t i = multi[q];
+            double sdot = 0.0, sphi = 0.0;
+            for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+                const int32_t f = col[k];
+                int lo = 0, hi = nz - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (zcol_s[mid] < f) lo = mid + 1;
+                    else hi = mid;
+                }
+                if (nz > 0 && zcol_s[lo] == f) {
+                    const double a = (double) val[k] * (double) zval_s[lo];
+                    sdot += a;
+                    sphi += phi(a);
+                }
+            }
+            hs += (double) w[i] * (phi(sdot) - sphi);
+        }
+        __syncthreads();
+    }
+    const double H = pred_block_sum<T>(hs, red);
+    if (tid == 0) {
+        double v;
+        if (phi.rbf) {
+            const double ez = exp(-(double) kf.gamma * (double) nzz);
+            v = ez * ((double) S[0] + J + H);
+        } else {
+            v = (double) kappa * (double) S[0] + J + H;
+        }
+        // the last training point (kept apart, as the reference's data_last)
+        T kl;
+        if (kf.kernel == 1) {
+            const T base = fma(kf.gamma, dl, kf.coef0);
+            kl = T(1);
+            for (int e = 0; e < kf.degree; ++e) kl *= base;
+        } else {
+            T dist = nlast + nzz - T(2) * dl;
+            dist = dist > T(0) ? dist : T(0);
+            kl = exp(-kf.gamma * dist);
+        }
+        out[p] = (T) (v + (double) (alpha_m * kl)) + bias;
+    }
+}
+
+// predict through the expansion; false when it does not apply (the caller predicts brute force)
+template <typename T>
+bool engine<T>::expansion_predict(const T *alpha_dev, T alpha_m, T bias, const int64_t *zr_dev, const int32_t *zc_dev,
+                                  const T *zv_dev, int64_t np, int64_t max_nnz_z, double zabs_max, double znorm_max,
+                                  T nlast, T *out_dev) {
+    auto &ex = csr.ex;
+    if (!ex.on || kernel == 0 || m <= 0 || max_nnz_z > PRED_ZCAP) return false;
+    if (std::getenv("PLSSVM_MI_PRED_BRUTE") != nullptr) return false;
+    // the model's Taylor degree covers |2 g x z| up to umax; the factored rbf form |z|^2 in range
+    const double xabs = std::sqrt(ex.umax / std::max(2.0 * std::fabs((double) gamma), 1e-300));
+    if (kernel == 2 && 2.0 * std::fabs((double) gamma) * xabs * zabs_max > ex.umax) return false;
+    if (kernel == 2 && std::fabs((double) gamma) * znorm_max > (sizeof(T) == 8 ? 300.0 : 40.0)) return false;
+    const phi_fn phi = make_phi<T>(kernel, degree, gamma, coef0);
+    dev_buf<T> wv, Md, Sd;
+    wv.alloc(std::max<int64_t>(m, 1), stream, false);
+    Md.alloc(std::max<int64_t>(d, 1) * ex.KM, stream, false);
+    Sd.alloc(2, stream);
+    hipLaunchKernelGGL(exp_pred_w_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream, alpha_dev,
+                       kernel == 2 ? csr.e.get() : nullptr, m, wv.get());
+    MI_LAUNCH_CHECK();
+    launch_dot2<T>(wv.get(), nullptr, nullptr, nullptr, m, red.get(), nullptr, stream);
+    launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, Sd.get(), stream);
+    coefs cf;
+    std::memcpy(cf.c, ex.coef, sizeof(cf.c));
+    if (d > 0)
+        hipLaunchKernelGGL(exp_pred_moments_kernel<T>, dim3((unsigned) ceil_div(d, 4)), dim3(256), 0, stream,
+                           csr.colptr.get(), csr.crow.get(), csr.cval.get(), wv.get(), d, ex.K, ex.KM, cf, Md.get());
+    MI_LAUNCH_CHECK();
+    T kappa = 0;
+    if (kernel == 1) {
+        kappa = 1;
+        for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
+    }
+    dev_buf<int> flag;
+    flag.alloc(1, stream);
+    hipLaunchKernelGGL(exp_pred_point_kernel<T>, dim3((unsigned) np), dim3(PRED_NT), 0, stream, zr_dev, zc_dev, zv_dev,
+                       csr.colptr.get(), csr.crow.get(), csr.rowptr.get(), csr.col.get(), csr.val.get(), wv.get(),
+                       Md.get(), ex.KM, phi, m, Sd.get(), xlast.get(), nlast, alpha_m, kf(), kappa, bias, out_dev,
+                       flag.get());
+    MI_LAUNCH_CHECK();
+    int hf = 0;
+    MI_HIP_CHECK(hipMemcpyAsync(&hf, flag.get(), sizeof(int), hipMemcpyDeviceToHost, stream));
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    return hf == 0;
+}
+
 #define INST(T)                                                                              \
     template bool engine<T>::expansion_eligible();                                           \
     template void engine<T>::build_expansion(const int64_t *, int64_t);                      \
     template void engine<T>::expansion_dominant(const T *, const cg_scalars<T> *);           \
     template void engine<T>::expansion_moments(const T *, const cg_scalars<T> *);            \
-    template void engine<T>::expansion_kp_raw(const T *, const cg_scalars<T> *, bool);
+    template void engine<T>::expansion_kp_raw(const T *, const cg_scalars<T> *, bool);      \
+    template bool engine<T>::expansion_predict(const T *, T, T, const int64_t *, const int32_t *, const T *, int64_t, \
+                                               int64_t, double, double, T, T *);
 INST(float)
 INST(double)
 #undef INST

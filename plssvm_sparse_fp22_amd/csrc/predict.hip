@@ -18,6 +18,7 @@
 #include <rocblas/rocblas.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -357,6 +358,30 @@ void engine<T>::predict(const T *alpha_host, T bias, const T *Z, const int64_t *
         zr[(size_t) p + 1] = (int64_t) zc.size();
     }
     const int64_t znnz = (int64_t) zc.size();
+    // columns ascending per point (the expansion's merge), and the points' magnitudes
+    int64_t max_nnz_z = 0;
+    double zabs_max = 0.0, znorm_max = 0.0;
+    {
+        std::vector<std::pair<int32_t, T>> tmp;
+        for (int64_t p = 0; p < np; ++p) {
+            const int64_t a0 = zr[(size_t) p], a1 = zr[(size_t) p + 1];
+            max_nnz_z = std::max(max_nnz_z, a1 - a0);
+            bool sorted = true;
+            double nrm = 0.0;
+            for (int64_t e = a0; e < a1; ++e) {
+                if (e > a0 && zc[(size_t) e] <= zc[(size_t) e - 1]) sorted = false;
+                zabs_max = std::max(zabs_max, std::fabs((double) zv[(size_t) e]));
+                nrm += (double) zv[(size_t) e] * (double) zv[(size_t) e];
+            }
+            znorm_max = std::max(znorm_max, nrm);
+            if (!sorted) {
+                tmp.clear();
+                for (int64_t e = a0; e < a1; ++e) tmp.emplace_back(zc[(size_t) e], zv[(size_t) e]);
+                std::stable_sort(tmp.begin(), tmp.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+                for (int64_t e = a0; e < a1; ++e) zc[(size_t) e] = tmp[(size_t) (e - a0)].first, zv[(size_t) e] = tmp[(size_t) (e - a0)].second;
+            }
+        }
+    }
     dev_buf<int64_t> zrd;
     dev_buf<int32_t> zcd;
     dev_buf<T> zvd;
@@ -367,6 +392,16 @@ void engine<T>::predict(const T *alpha_host, T bias, const T *Z, const int64_t *
     if (znnz > 0) {
         MI_HIP_CHECK(hipMemcpyAsync(zcd.get(), zc.data(), sizeof(int32_t) * (size_t) znnz, hipMemcpyHostToDevice, stream));
         MI_HIP_CHECK(hipMemcpyAsync(zvd.get(), zv.data(), sizeof(T) * (size_t) znnz, hipMemcpyHostToDevice, stream));
+    }
+    if (kernel != 0 && csr.ex.on) {  // sparse poly / rbf model: through the kernel expansion (expand.hip)
+        dev_buf<T> oall;
+        oall.alloc(np, stream, false);
+        if (expansion_predict(a.get(), alpha_host[m], bias, zrd.get(), zcd.get(), zvd.get(), np, max_nnz_z, zabs_max,
+                              znorm_max, nlast, oall.get())) {
+            MI_HIP_CHECK(hipMemcpyAsync(out, oall.get(), sizeof(T) * (size_t) np, hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            return;
+        }
     }
     const int64_t nblk = std::max<int64_t>(1, ceil_div(m, PRED_ROWS));
     dev_buf<T> ztd, nzd, pd, od;

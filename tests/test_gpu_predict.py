@@ -132,3 +132,27 @@ def test_predict_edge_cases():
         one = svm.predict_values(X[:1])
         many = svm.predict_values(X)
         np.testing.assert_allclose(one[0], many[0], rtol=1e-13)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("kernel", ["rbf", "polynomial"])
+def test_predict_sparse_expansion_matches_brute_force(kernel, dtype, monkeypatch):
+    """sparse poly / rbf predict through the kernel expansion (moments + the support vectors sharing two or
+    more features with the point) against the brute-force kernel (PLSSVM_MI_PRED_BRUTE): 800k support
+    vectors (two passes of the per-point row bitmap) and a dense-ish set whose repeat rows overflow the
+    per-pass list (the path then falls back to brute force by itself)"""
+    rng = np.random.default_rng(4)
+    for n, d, k, npts in [(800_000, 20_000, 10, 200), (6000, 60, 20, 50)]:
+        csr, _ = datagen.sparse_csr(n, d, k, seed=31, dtype=dtype)
+        zc, _ = datagen.sparse_csr(npts, d, k, seed=32, dtype=dtype)
+        alpha = rng.standard_normal(n).astype(dtype)
+        p = pm.Parameter(kernel, gamma=1.0 / d, coef0=0.5, real_type=dtype)
+        p.csr = csr
+        with pm.CSVM(p) as svm:
+            svm.setup_data_on_device()
+            assert svm.info()["sparse_algo"] == pm._abi.SPARSE_EXPANSION
+            got = svm.predict_values(zc, alpha=alpha, bias=0.25)
+            monkeypatch.setenv("PLSSVM_MI_PRED_BRUTE", "1")
+            want = svm.predict_values(zc, alpha=alpha, bias=0.25)
+            monkeypatch.delenv("PLSSVM_MI_PRED_BRUTE")
+        np.testing.assert_allclose(got, want, rtol=0, atol=TOL[dtype] * np.abs(want).max(), err_msg=f"n={n}")
