@@ -557,7 +557,12 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
                                         stream));
         MI_HIP_CHECK(hipStreamSynchronize(stream));
     }
-    constexpr int64_t CAP = int64_t(1) << 27;      // incidences per sub-block (48 B each in flight)
+    // incidences per sub-block (≈ 80 B each in flight); PLSSVM_MI_EXP_CAPLOG = log2 (measurements)
+    const int64_t CAP = int64_t(1) << [] {
+        const char *e = std::getenv("PLSSVM_MI_EXP_CAPLOG");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 20 && v <= 31 ? v : 27;
+    }();
     constexpr int64_t ROWS_MAX = 65536;            // rows per sub-block (one workgroup per row)
     std::vector<std::pair<int64_t, int64_t>> blocks;
     {
@@ -630,6 +635,14 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         Lh = std::move(nh);
         cap = nc;
     };
+    double st_gen = 0, st_sort = 0, st_red = 0, st_sel = 0;  // PLSSVM_MI_TIMING: stage seconds
+    auto stage = [&](double &acc) {
+        if (!pt.on) return;
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        const auto now = std::chrono::steady_clock::now();
+        acc += std::chrono::duration<double>(now - pt.t).count();
+        pt.t = now;
+    };
     for (auto &b : blocks) {
         const int64_t i0 = b.first, rows = b.second - b.first;
         int64_t total = 0;
@@ -644,16 +657,19 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
                            csr.val.get(), cpos, csr.colptr.get(), csr.crow.get(), csr.cval.get(), i0, off.get(),
                            keys.get(), vals.get(), phi);
         MI_LAUNCH_CHECK();
+        stage(st_gen);
         const int end_bit = 32 + std::max(1, (int) std::ceil(std::log2((double) rows + 1.0)));
         size_t t1s = tmp_sort;
         MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp.get(), t1s, keys.get(), keys_s.get(), vals.get(),
                                                         vals_s.get(), (int) total, 0, end_bit, stream));
+        stage(st_sort);
         size_t t2s = tmp_red;
         MI_HIP_CHECK(hipcub::DeviceReduce::ReduceByKey(tmp.get(), t2s, keys_s.get(), keys.get(), vals_s.get(),
                                                        vals.get(), nruns.get(), d2sum(), (int) total, stream));
         hipLaunchKernelGGL(exp_h_kernel, dim3((unsigned) ceil_div(total, 256)), dim3(256), 0, stream, keys.get(),
                            vals.get(), nruns.get(), phi, hp.get());
         MI_LAUNCH_CHECK();
+        stage(st_red);
         int64_t nu = 0;
         MI_HIP_CHECK(hipMemcpyAsync(&nu, nruns.get(), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
         MI_HIP_CHECK(hipStreamSynchronize(stream));
@@ -669,7 +685,11 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
                            nsel.get(), i0, Li.get() + P, Lj.get() + P, Lh.get() + P);
         MI_LAUNCH_CHECK();
         P += ns;
+        stage(st_sel);
     }
+    if (pt.on)
+        std::fprintf(stderr, "[plssvm_mi] column join: %zu blocks, gen %.3f sort %.3f reduce %.3f select+append %.3f\n",
+                     blocks.size(), st_gen, st_sort, st_red, st_sel);
     keys.reset(), keys_s.reset(), vals.reset(), vals_s.reset(), hp.reset(), hsel.reset(), tmp.reset();
     pt.mark("expansion: column join (blocks)");
     if (P > INT32_MAX) throw mi_error(-5, "more than 2^31 multi-feature pairs on one rank: use more GPUs");
