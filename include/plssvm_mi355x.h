@@ -75,18 +75,23 @@ extern "C" {
  *       in the factored form with a Taylor degree <= 16 for the data's max |2 g x_if x_jf|), else the
  *       Gram pattern; when the chosen structure's estimated size exceeds the device-memory budget
  *       (85 % of the free memory; environment PLSSVM_MI_MEM_BUDGET = bytes overrides), or its build
- *       runs out of memory, the densified path 3;
+ *       runs out of memory, the on-the-fly path 4 or the densified path 3, whichever the setup's
+ *       estimate makes faster (the on-the-fly path below a few percent density);
  *   1 = Gram pattern: every overlapping pair (j < i) with s_ij = x_i . x_j stored at setup, the kernel
  *       function re-evaluated on each per K·p (O(sum_f c_f^2) memory and traffic);
  *   2 = kernel expansion: per-feature column moments + the stored remainder of the pairs sharing two or
  *       more features (O(nnz + #multi-feature pairs)); fails with ERR_UNSUPPORTED when not eligible;
  *   3 = densified: X densified on the device, the dense MFMA pairwise tiles (O(m d) memory, every pair
- *       recomputed from the data on each K·p as in the reference); ERR_OOM when m x d does not fit. */
+ *       recomputed from the data on each K·p as in the reference); ERR_OOM when m x d does not fit;
+ *   4 = on the fly: nothing stored per pair; every K·p re-forms s_ij for the pairs sharing a feature
+ *       from the CSR rows and the CSC columns (O(nnz) memory + a d x m / 1024 window-offset table,
+ *       O(sum_f c_f^2) work per K·p, as the reference recomputes every pair). */
 #define PLSSVM_MI_OPT_SPARSE_ALGO 4
 #define PLSSVM_MI_SPARSE_AUTO 0
 #define PLSSVM_MI_SPARSE_PATTERN 1
 #define PLSSVM_MI_SPARSE_EXPANSION 2
 #define PLSSVM_MI_SPARSE_DENSE 3 /* densified on the device, MFMA pairwise tiles (every pair recomputed per K·p) */
+#define PLSSVM_MI_SPARSE_ONTHEFLY 4 /* s_ij re-formed from the CSR / CSC per K·p, nothing stored per pair */
 
 typedef struct plssvm_mi_ctx plssvm_mi_ctx;
 

@@ -163,7 +163,7 @@ class CSVM:
         if rbf_form:  # 1 = direct RBF pair form on sparse data, see PLSSVM_MI_OPT_RBF_FORM
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_RBF_FORM, rbf_form))
         algo = {"auto": _abi.SPARSE_AUTO, "pattern": _abi.SPARSE_PATTERN, "expansion": _abi.SPARSE_EXPANSION,
-                "dense": _abi.SPARSE_DENSE}[sparse_algo]
+                "dense": _abi.SPARSE_DENSE, "onthefly": _abi.SPARSE_ONTHEFLY}[sparse_algo]
         if algo != _abi.SPARSE_AUTO:  # sparse poly/rbf K·p algorithm, see PLSSVM_MI_OPT_SPARSE_ALGO
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_SPARSE_ALGO, algo))
         if sim_rank is not None:  # (rank, world): single-GPU test hook, see PLSSVM_MI_OPT_SIM_RANK

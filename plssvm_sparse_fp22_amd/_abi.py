@@ -36,7 +36,7 @@ EXPORTS = (
 OPT_SIM_RANK = 2
 OPT_RBF_FORM = 3
 OPT_SPARSE_ALGO = 4
-SPARSE_AUTO, SPARSE_PATTERN, SPARSE_EXPANSION, SPARSE_DENSE = 0, 1, 2, 3
+SPARSE_AUTO, SPARSE_PATTERN, SPARSE_EXPANSION, SPARSE_DENSE, SPARSE_ONTHEFLY = 0, 1, 2, 3, 4
 PART_KERNEL, PART_OVERLAP = 0, 1
 XCHG_ALLREDUCE, XCHG_ALLGATHER = 0, 1
 # int fn(void *buf, int64_t count, int real_bytes, int op, void *user)   (plssvm_mi_exchange_fn)

@@ -105,7 +105,7 @@ int plssvm_mi_set_option(plssvm_mi_ctx *ctx, int key, int64_t value) {
             e.sim_world = w;
         } else if (key == PLSSVM_MI_OPT_RBF_FORM && value >= 0 && value <= 1) {
             e.rbf_form = (int) value;
-        } else if (key == PLSSVM_MI_OPT_SPARSE_ALGO && value >= 0 && value <= 3) {
+        } else if (key == PLSSVM_MI_OPT_SPARSE_ALGO && value >= 0 && value <= 4) {
             e.sparse_algo = (int) value;
         } else {
             throw mi_error(PLSSVM_MI_ERR_ARG, "bad option");
@@ -375,6 +375,7 @@ int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
         info->spmv_bytes = e.csr.spmv_csc.stream_bytes() + e.csr.spmv_csr.stream_bytes();
         info->rbf_small_args = e.csr.rbf_small ? 1 : 0;
         info->sparse_algo = e.csr.dense_on ? PLSSVM_MI_SPARSE_DENSE
+                            : e.csr.otf_on ? PLSSVM_MI_SPARSE_ONTHEFLY
                             : e.csr.ex.on  ? PLSSVM_MI_SPARSE_EXPANSION
                                            : (e.csr.have_gram ? PLSSVM_MI_SPARSE_PATTERN : 0);
         info->exp_terms = e.csr.ex.on ? e.csr.ex.K : 0;

@@ -31,7 +31,7 @@ struct engine : engine_base {
     hipStream_t stream = nullptr;
     int kp_mode = 0;  // PLSSVM_MI_KP_*
     int rbf_form = 0;  // PLSSVM_MI_OPT_RBF_FORM
-    int sparse_algo = 0;  // PLSSVM_MI_OPT_SPARSE_ALGO (0 auto, 1 Gram pattern, 2 kernel expansion)
+    int sparse_algo = 0;  // PLSSVM_MI_OPT_SPARSE_ALGO (0 auto, 1 Gram pattern, 2 kernel expansion, 3 dense, 4 on the fly)
 
     // ---- multi-GPU row-block group ----
     int rank = 0, world = 1;
@@ -112,6 +112,11 @@ struct engine : engine_base {
                                      const std::vector<int32_t> &crow, int64_t inc_total) const;
     void release_sparse_structures();
     void setup_sparse_dense();                                     // densified fallback (PLSSVM_MI_SPARSE_DENSE)
+    // on-the-fly path (otf.hip, PLSSVM_MI_SPARSE_ONTHEFLY): estimated seconds per K·p share, setup, K·p
+    double otf_estimate_s(const int64_t *rowptr, const int32_t *col, const std::vector<int64_t> &colptr) const;
+    void setup_otf(int rbf_fact_ok);
+    void otf_dominant(const T *p, const cg_scalars<T> *status);
+    void otf_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);
     bool sparse_stored() const { return sparse && !csr.dense_on; } // K·p through the CSR structures
     bool expansion_eligible();                                    // expand.hip: K, coefficients; true if usable
     void build_expansion(const int64_t *cpos, int64_t max_inc);   // multi-overlap remainder H, diagonal

@@ -1,0 +1,260 @@
+// Sparse polynomial / RBF K·p recomputed on the fly from the CSR rows: nothing per pair
+// is stored, every call re-forms s_ij = x_i . x_j for the pairs that share a feature, as the reference
+// recomputes every k(x_i, x_j) per call (include/plssvm/backends/HIP/svm_kernel.hip.hpp:206-268;
+// src/plssvm/backends/OpenMP/svm_kernel.cpp:21-47). The fallback when neither stored structure (the kernel
+// expansion's remainder, the Gram pattern) fits the device, below the density where the densified MFMA
+// tiles win.
+//
+// One wave owns one row i and an LDS row of CW partner accumulators. For each window of CW partners it
+// walks the CSC segments of row i's features restricted to that window (row-local window offsets cwo),
+// lanes over the segment's entries (a column holds distinct rows, so the lanes of one feature never
+// collide): s[j] = fma(x_if, x_jf, s[j]) feature by feature in ascending order — the same fma chain as
+// the dense dot product over the densified rows. Then the window is scanned once: every non-zero s_ij,
+// j != i, contributes the pair part c_ij p_j (c_ij = k_ij - kappa_ij, the separable part kappa_ij is
+// added in O(m) by gram_base_kernel, with the diagonal). Waves are independent (no barriers, no atomics),
+// all sums in fixed orders: bitwise reproducible.
+#include <algorithm>
+#include <cmath>
+
+#include "../../include/plssvm_mi355x.h"
+#include "engine.hpp"
+
+namespace plssvm_mi {
+
+namespace {
+
+constexpr int OTF_NT = 256;   // 4 waves (rows) per workgroup; 5 workgroups per CU by LDS
+constexpr int OTF_U = 8;      // features whose segment loads are in flight together
+constexpr int OTF_BINMAX = 16;
+
+template <typename T>
+constexpr int otf_cw() { return 8192 / (int) sizeof(T); }  // 8 KiB of partner accumulators per wave
+
+// pair part c_ij = k_ij - kappa_ij for s_ij != 0 (the Gram pattern's forms, sparse.hip)
+template <typename T>
+struct otf_pair {
+    int kernel;  // 0 linear (pairwise mode), 1 poly, 2 rbf
+    int form;    // rbf: 0 factored e_i e_j expm1(2 g s), 1 direct; poly: 0 binomial, 1 direct
+    int deg;
+    T g, c0, kappa;
+    T bin[OTF_BINMAX + 1];  // poly binomial form: c = sum_k bin[k] s^k, bin[k] = C(deg,k) c0^(deg-k) g^k
+};
+
+template <typename T>
+__device__ __forceinline__ T otf_c(const otf_pair<T> &pf, T s, T ni, T nj, T ei, T ej) {
+    if (pf.kernel == 0) return s;
+    if (pf.kernel == 2) {
+        if (pf.form == 0) return ei * ej * expm1(T(2) * pf.g * s);
+        T dist = ni + nj - T(2) * s;
+        dist = dist > T(0) ? dist : T(0);
+        return exp(-pf.g * dist) - ei * ej;
+    }
+    if (pf.form == 0) {
+        T h = T(0);
+        for (int k = pf.deg; k >= 1; --k) h = (h + pf.bin[k]) * s;
+        return h;
+    }
+    const T base = fma(pf.g, s, pf.c0);
+    T r = T(1);
+    for (int e = 0; e < pf.deg; ++e) r *= base;
+    return r - pf.kappa;
+}
+
+__device__ __forceinline__ int rl32(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ int64_t rl64(int64_t x, int l) {
+    const int lo = __builtin_amdgcn_readlane((int) (uint32_t) x, l);
+    const int hi = __builtin_amdgcn_readlane((int) (x >> 32), l);
+    return (int64_t) (((uint64_t) (uint32_t) hi << 32) | (uint32_t) lo);
+}
+__device__ __forceinline__ float rlT(float x, int l) { return __int_as_float(rl32(__float_as_int(x), l)); }
+__device__ __forceinline__ double rlT(double x, int l) { return __longlong_as_double(rl64(__double_as_longlong(x), l)); }
+
+// cwo[W][f] = #{ t in column f : crow[t] < W CW }  (W = 0..nW; CSC rows ascending inside a column)
+__global__ __launch_bounds__(256) void otf_cwo_kernel(const int64_t *__restrict__ colptr,
+                                                      const int32_t *__restrict__ crow, int64_t d, int64_t nW,
+                                                      int64_t CW, int32_t *__restrict__ cwo) {
+    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (nW + 1) * d) return;
+    const int64_t W = t / d, f = t - W * d;
+    const int64_t a = colptr[f], key = W * CW;
+    int64_t lo = a, hi = colptr[f + 1];
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t) crow[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    cwo[t] = (int32_t) (lo - a);
+}
+
+// raw[i] = sum_{j != i, s_ij != 0} c_ij p_j for this rank's rows i in [r0, r1)
+template <typename T>
+__global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+                                                        const T *__restrict__ val, const int64_t *__restrict__ colptr,
+                                                        const int32_t *__restrict__ crow, const T *__restrict__ cval,
+                                                        const int32_t *__restrict__ cwo, const T *__restrict__ norms,
+                                                        const T *__restrict__ ev, const T *__restrict__ p, int64_t m,
+                                                        int64_t d, int64_t nW, int64_t r0, int64_t r1, otf_pair<T> pf,
+                                                        T *__restrict__ raw, const cg_scalars<T> *__restrict__ status) {
+    constexpr int CW = otf_cw<T>();
+    __shared__ T S[OTF_NT / 64][CW];
+    if (status != nullptr && status->converged) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t i = r0 + (int64_t) blockIdx.x * (OTF_NT / 64) + wave;
+    if (i >= r1) return;  // waves never synchronise: each owns its accumulator row
+    T *s = S[wave];
+    for (int t = lane; t < CW; t += 64) s[t] = T(0);
+    const int64_t b0 = rowptr[i], nz = rowptr[i + 1] - b0;
+    const T ni = norms[i], ei = ev != nullptr ? ev[i] : T(1);
+    double acc = 0.0;
+    for (int64_t W = 0; W < nW; ++W) {
+        const int64_t j0 = W * CW;
+        const int32_t *c_lo = cwo + W * d, *c_hi = c_lo + d;
+        for (int64_t q = 0; q < nz; q += 64) {
+            // lane k: feature q + k of row i, its value and its segment [lo, lo + len) of this window
+            const int64_t k = q + lane;
+            int64_t lo = 0;
+            int len = 0;
+            T v = T(0);
+            if (k < nz) {
+                const int32_t f = col[b0 + k];
+                v = val[b0 + k];
+                const int32_t a = c_lo[f];
+                lo = colptr[f] + a;
+                len = c_hi[f] - a;
+            }
+            const int nk = (int) (nz - q < 64 ? nz - q : 64);
+            for (int u = 0; u < nk; u += OTF_U) {
+                int64_t lo_u[OTF_U];
+                int len_u[OTF_U];
+                T v_u[OTF_U];
+                int mx = 0;
+#pragma unroll
+                for (int x = 0; x < OTF_U; ++x) {
+                    const int src = u + x < 64 ? u + x : 63;
+                    lo_u[x] = rl64(lo, src);
+                    len_u[x] = u + x < nk ? rl32(len, src) : 0;
+                    v_u[x] = rlT(v, src);
+                    mx = len_u[x] > mx ? len_u[x] : mx;
+                }
+                for (int o = 0; o < mx; o += 64) {
+                    int jj[OTF_U];
+                    T vv[OTF_U];
+#pragma unroll
+                    for (int x = 0; x < OTF_U; ++x) {  // every segment load in flight before the first update
+                        const bool ok = o + lane < len_u[x];
+                        const int64_t t = lo_u[x] + o + lane;
+                        jj[x] = ok ? crow[t] - (int) j0 : -1;
+                        vv[x] = ok ? cval[t] : T(0);
+                    }
+#pragma unroll
+                    for (int x = 0; x < OTF_U; ++x)  // features in ascending order (one wave: LDS in program order)
+                        if (jj[x] >= 0) s[jj[x]] = fma(v_u[x], vv[x], s[jj[x]]);
+                }
+            }
+        }
+        // the window's pair terms, lane-strided (fixed order); the accumulators are left zeroed
+        for (int t = lane; t < CW; t += 64) {
+            const T sv = s[t];
+            if (sv != T(0)) {
+                s[t] = T(0);
+                const int64_t j = j0 + t;
+                if (j != i)
+                    acc += (double) otf_c<T>(pf, sv, ni, norms[j], ei, ev != nullptr ? ev[j] : T(1)) * (double) p[j];
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) raw[i] = (T) acc;
+}
+
+}  // namespace
+
+// device bytes and an estimated time (s) of one on-the-fly K·p share, from the host CSR / CSC counts
+template <typename T>
+double engine<T>::otf_estimate_s(const int64_t *rowptr, const int32_t *col, const std::vector<int64_t> &colptr) const {
+    const int64_t CW = otf_cw<T>(), nW = ceil_div(std::max<int64_t>(m, 1), CW);
+    double fill = 0.0;  // column-segment entries walked: sum over the rank's entries of their column length
+    for (int64_t k = rowptr[r0]; k < rowptr[r1]; ++k) fill += (double) (colptr[col[k] + 1] - colptr[col[k]]);
+    const double nnz_r = (double) (rowptr[r1] - rowptr[r0]), R = (double) (r1 - r0);
+    // calibrated on the box: segment entries from L2 / MALL, per-(entry, window) segment
+    // set-up, and the LDS scan of every (row, window)
+    return fill * 2.0e-13 + nnz_r * (double) nW * 3.0e-12 + R * (double) m * 6.0e-14;
+}
+
+template <typename T>
+void engine<T>::setup_otf(int rbf_fact_ok) {
+    const int64_t CW = otf_cw<T>();
+    csr.otf_cw = (int) CW;
+    csr.otf_nw = ceil_div(std::max<int64_t>(m, 1), CW);
+    csr.cwo.alloc((csr.otf_nw + 1) * d, stream, false);
+    const int64_t tot = (csr.otf_nw + 1) * d;
+    if (tot > 0)
+        hipLaunchKernelGGL(otf_cwo_kernel, dim3((unsigned) ceil_div(tot, 256)), dim3(256), 0, stream, csr.colptr.get(),
+                           csr.crow.get(), d, csr.otf_nw, CW, csr.cwo.get());
+    MI_LAUNCH_CHECK();
+    if (csr.ssc.get() == nullptr) csr.ssc.alloc(1, stream);
+    csr.rbf_factored = kernel == 2 && rbf_form != 1 && rbf_fact_ok;
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    csr.otf_on = true;
+}
+
+template <typename T>
+void engine<T>::otf_dominant(const T *p, const cg_scalars<T> *status) {
+    if (r1 <= r0) return;
+    otf_pair<T> pf{};
+    pf.kernel = kernel;
+    pf.deg = degree;
+    pf.g = gamma;
+    pf.c0 = coef0;
+    T kappa = 0;
+    if (kernel == 1) {
+        kappa = 1;
+        for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
+        pf.form = (degree >= 1 && degree <= OTF_BINMAX) ? 0 : 1;
+        if (pf.form == 0) {  // C(deg, k) c0^(deg - k) g^k in double, rounded once
+            for (int k = 1; k <= degree; ++k) {
+                double c = 1.0;
+                for (int t = 0; t < k; ++t) c = c * (double) (degree - t) / (double) (t + 1);
+                pf.bin[k] = (T) (c * std::pow((double) coef0, degree - k) * std::pow((double) gamma, k));
+            }
+        }
+    } else {
+        pf.form = csr.rbf_factored ? 0 : 1;
+    }
+    pf.kappa = kappa;
+    hipLaunchKernelGGL(otf_kp_kernel<T>, dim3((unsigned) ceil_div(r1 - r0, OTF_NT / 64)), dim3(OTF_NT), 0, stream,
+                       csr.rowptr.get(), csr.col.get(), csr.val.get(), csr.colptr.get(), csr.crow.get(), csr.cval.get(),
+                       csr.cwo.get(), norms.get(), kernel == 2 ? csr.e.get() : nullptr, p, m, d, csr.otf_nw, r0, r1, pf,
+                       raw.get(), status);
+    MI_LAUNCH_CHECK();
+}
+
+// raw = sum_j k_ij p_j (with_base: + the separable part and the diagonal, as the Gram pattern's)
+template <typename T>
+void engine<T>::otf_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base) {
+    MI_HIP_CHECK(hipMemsetAsync(raw.get(), 0, sizeof(T) * (size_t) m, stream));
+    otf_dominant(p, status);
+    allgather_rows(raw.get());
+    if (with_base && !(sim_world > 0 && sim_rank != 0)) {
+        launch_dot2<T>(p, kernel == 2 ? csr.e.get() : nullptr, nullptr, nullptr, m, red.get(), status, stream);
+        launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+        T kappa = 0;
+        if (kernel == 1) {
+            kappa = 1;
+            for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
+        }
+        launch_gram_base<T>(kernel, kf(), kappa, csr.ssc.get(), norms.get(), csr.e.get(), p, m, raw.get(), status, stream);
+    }
+}
+
+#define INST(T)                                                                                                        \
+    template double engine<T>::otf_estimate_s(const int64_t *, const int32_t *, const std::vector<int64_t> &) const;   \
+    template void engine<T>::setup_otf(int);                                                                           \
+    template void engine<T>::otf_dominant(const T *, const cg_scalars<T> *);                                           \
+    template void engine<T>::otf_kp_raw(const T *, const cg_scalars<T> *, bool);
+INST(float)
+INST(double)
+#undef INST
+
+}  // namespace plssvm_mi

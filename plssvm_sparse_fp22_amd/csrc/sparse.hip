@@ -14,6 +14,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -734,7 +735,8 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                                "the factored rbf form out of range): use the Gram pattern");
         const int64_t budget = sparse_mem_budget();
         const bool use_exp = elig && sparse_algo != 1;
-        if (sparse_algo != 3) {
+        const bool unstored = sparse_algo == 3 || sparse_algo == 4;  // forced densified / on the fly
+        if (!unstored) {
             int64_t inc_total = 0;
             for (int64_t I = csr.rb0; I < csr.rb1; ++I) inc_total += inc_rb[I];
             csr.est_bytes = use_exp ? estimate_expansion_bytes(rowptr, col, colptr, crow, inc_total)
@@ -743,7 +745,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         pt.mark("setup_csr: incidences + size estimate");
         const bool forced = sparse_algo == 1 || sparse_algo == 2;
         bool stored = false;
-        if (sparse_algo != 3 && (forced || csr.est_bytes <= budget)) {
+        if (!unstored && (forced || csr.est_bytes <= budget)) {
             try {
                 if (use_exp) {
                     // the two SELL passes of the kernel expansion (the factored linear path's plans, with K channels):
@@ -785,8 +787,23 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             }
         }
         if (!stored) {
+            // no stored structure: the on-the-fly path or the densified MFMA tiles, whichever the estimate
+            // makes faster (auto), unless one is forced
             cpos_d.reset();
-            setup_sparse_dense();
+            bool otf = sparse_algo == 4;
+            if (sparse_algo == 0) {
+                const double peak = sizeof(T) == 8 ? 78.6e12 : 157.3e12;
+                const double dp = (double) round_up(std::max<int64_t>(d, 1), kp_dpad<T>());
+                const int eff_world = sim_world > 0 ? sim_world : world;
+                const double t_dense = (double) m * (double) m * dp / (double) eff_world / (0.85 * peak);
+                const double t_otf = otf_estimate_s(rowptr, col, colptr);
+                otf = t_otf < t_dense;
+                if (std::getenv("PLSSVM_MI_TIMING") != nullptr)
+                    std::fprintf(stderr, "[plssvm_mi] unstored sparse K·p: on the fly ~%.3g s, densified ~%.3g s\n", t_otf,
+                                 t_dense);
+            }
+            if (otf) setup_otf(fact_ok ? 1 : 0);
+            else setup_sparse_dense();
         }
     }
 }
@@ -1078,6 +1095,10 @@ void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status, bool with
         allgather_rows(raw.get());
         return;
     }
+    if (csr.otf_on) {
+        otf_kp_raw(p, status, with_base);
+        return;
+    }
     if (csr.ex.on) {
         expansion_kp_raw(p, status, with_base);
         return;
@@ -1107,6 +1128,10 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
     if (factored()) {  // both SpMV passes (the factored K·p without its collectives)
         spmv_pass_csc(p, status);
         spmv_pass_csr(status);
+        return;
+    }
+    if (csr.otf_on) {  // the on-the-fly pair kernel (rows of this rank)
+        otf_dominant(p, status);
         return;
     }
     if (csr.ex.on) {  // timing: the remainder stream (p stands in for w)
@@ -1142,7 +1167,18 @@ void engine<T>::sparse_dominant(const T *p, const cg_scalars<T> *status) {
     MI_LAUNCH_CHECK();
 }
 
+template <typename T>
+void launch_gram_base(int kernel, kfun<T> kf, T kappa, const T *ssc, const T *norms, const T *ev, const T *p, int64_t m,
+                      T *raw, const cg_scalars<T> *status, hipStream_t s) {
+    if (m <= 0) return;
+    hipLaunchKernelGGL(gram_base_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, kernel, kf, kappa, ssc,
+                       norms, ev, p, m, raw, status);
+    MI_LAUNCH_CHECK();
+}
+
 #define INST(T)                                                                                                 \
+    template void launch_gram_base<T>(int, kfun<T>, T, const T *, const T *, const T *, const T *, int64_t, T *, \
+                                      const cg_scalars<T> *, hipStream_t);                                      \
     template void engine<T>::setup_csr(const int64_t *, const int32_t *, const void *, int, int64_t, int64_t); \
     template void engine<T>::build_gram_blocks(const int64_t *, int64_t);                                     \
     template void engine<T>::sparse_q();                                                                      \

@@ -114,14 +114,27 @@ struct csr_data {
     // X is densified into the engine's XT and every K·p recomputes all pairs on the MFMA tiles
     bool dense_on = false;
     int64_t est_bytes = 0;  // estimated device bytes of the chosen stored structure (0: not estimated)
+    // on-the-fly path (PLSSVM_MI_SPARSE_ONTHEFLY, otf.hip): nothing stored per pair; cwo[W][f] = the first
+    // entry of CSC column f (column-local) whose row lies in partner window W (CW rows)
+    bool otf_on = false;
+    int otf_cw = 0;
+    int64_t otf_nw = 0;
+    dev_buf<int32_t> cwo;  // [otf_nw + 1][d]
 
     vals_t<T> rvals() const { return vals_t<T>{ val.get(), nullptr }; }
     vals_t<T> cvals() const { return vals_t<T>{ cval.get(), nullptr }; }
     int64_t bytes() const {
         return rowptr.bytes() + col.bytes() + val.bytes() + colptr.bytes() + crow.bytes() +
                cval.bytes() + spmv_csc.bytes() + spmv_csr.bytes() + rb_csr.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
-               rb_base.bytes() + rowoff.bytes() + cells.bytes() + slab_row.bytes() + slab_col.bytes() + ex.bytes();
+               rb_base.bytes() + rowoff.bytes() + cells.bytes() + slab_row.bytes() + slab_col.bytes() + ex.bytes() +
+               cwo.bytes();
     }
 };
+
+// raw_i += the separable part of sum_j k_ij p_j and the diagonal pair (sparse.hip; Gram pattern and
+// on-the-fly paths, after the group exchange)
+template <typename T>
+void launch_gram_base(int kernel, kfun<T> kf, T kappa, const T *ssc, const T *norms, const T *ev, const T *p, int64_t m,
+                      T *raw, const cg_scalars<T> *status, hipStream_t s);
 
 }  // namespace plssvm_mi
