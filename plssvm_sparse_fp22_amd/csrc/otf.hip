@@ -15,6 +15,7 @@
 // all sums in fixed orders: bitwise reproducible.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "../../include/plssvm_mi355x.h"
 #include "engine.hpp"
@@ -27,8 +28,17 @@ constexpr int OTF_NT = 256;   // 4 waves (rows) per workgroup; 5 workgroups per 
 constexpr int OTF_U = 8;      // features whose segment loads are in flight together
 constexpr int OTF_BINMAX = 16;
 
-template <typename T>
-constexpr int otf_cw() { return 8192 / (int) sizeof(T); }  // 8 KiB of partner accumulators per wave
+// partner accumulators per wave: CWB bytes (8 / 16 / 32 KiB; PLSSVM_MI_OTF_CWB, default 8 KiB)
+template <typename T, int CWB>
+constexpr int otf_cw() { return CWB / (int) sizeof(T); }
+inline int otf_cwb() {
+    static const int v = [] {
+        const char *e = std::getenv("PLSSVM_MI_OTF_CWB");
+        const int b = e != nullptr ? std::atoi(e) : 8192;
+        return (b == 16384 || b == 32768) ? b : 8192;
+    }();
+    return v;
+}
 
 // pair part c_ij = k_ij - kappa_ij for s_ij != 0 (the Gram pattern's forms, sparse.hip)
 template <typename T>
@@ -86,8 +96,57 @@ __global__ __launch_bounds__(256) void otf_cwo_kernel(const int64_t *__restrict_
     cwo[t] = (int32_t) (lo - a);
 }
 
-// raw[i] = sum_{j != i, s_ij != 0} c_ij p_j for this rank's rows i in [r0, r1)
+// One batch of up to 64 features of row i against the partner window [j0, j0 + CW): lane k holds feature
+// k's segment (absolute CSC start lo, length len) and value v. Groups of OTF_U features; the next group's
+// loads (first 64 entries of each segment) are issued before the current group's updates, so one memory
+// latency per group is overlapped with the previous group's LDS work (straight-line: a past-the-end group
+// loads entry 0 with length 0). A longer segment's further entries follow right after its first 64, so
+// every s_ij accumulates its features in ascending order.
 template <typename T>
+__device__ __forceinline__ void otf_batch(T *__restrict__ s, const int32_t *__restrict__ crow,
+                                          const T *__restrict__ cval, int j0, int nk, int64_t lo, int len, T v,
+                                          int lane) {
+    int64_t lo_c[OTF_U], lo_n[OTF_U];
+    int len_c[OTF_U], len_n[OTF_U], jj_c[OTF_U], jj_n[OTF_U];
+    T v_c[OTF_U], v_n[OTF_U], vv_c[OTF_U], vv_n[OTF_U];
+    auto fetch = [&](int u, int64_t *lo_x, int *len_x, T *v_x, int *jj_x, T *vv_x) {
+#pragma unroll
+        for (int x = 0; x < OTF_U; ++x) {
+            const int src = u + x < nk ? u + x : 0;
+            lo_x[x] = rl64(lo, src);
+            len_x[x] = u + x < nk ? rl32(len, src) : 0;
+            v_x[x] = rlT(v, src);
+            const int64_t t = lane < len_x[x] ? lo_x[x] + lane : 0;
+            jj_x[x] = crow[t];  // raw loads: validity is tested at the update, not here (keeps them in flight)
+            vv_x[x] = cval[t];
+        }
+    };
+    fetch(0, lo_c, len_c, v_c, jj_c, vv_c);
+    for (int u = 0; u < nk; u += OTF_U) {
+        fetch(u + OTF_U, lo_n, len_n, v_n, jj_n, vv_n);
+#pragma unroll
+        for (int x = 0; x < OTF_U; ++x) {
+            if (lane < len_c[x]) {
+                const int j = jj_c[x] - j0;
+                s[j] = fma(v_c[x], vv_c[x], s[j]);
+            }
+            for (int o = 64; o < len_c[x]; o += 64) {  // segments longer than a wave (dense columns)
+                if (o + lane < len_c[x]) {
+                    const int64_t t = lo_c[x] + o + lane;
+                    const int j = crow[t] - j0;
+                    s[j] = fma(v_c[x], cval[t], s[j]);
+                }
+            }
+        }
+#pragma unroll
+        for (int x = 0; x < OTF_U; ++x) {
+            lo_c[x] = lo_n[x], len_c[x] = len_n[x], v_c[x] = v_n[x], jj_c[x] = jj_n[x], vv_c[x] = vv_n[x];
+        }
+    }
+}
+
+// raw[i] = sum_{j != i, s_ij != 0} c_ij p_j for this rank's rows i in [r0, r1)
+template <typename T, int CWB>
 __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
                                                         const T *__restrict__ val, const int64_t *__restrict__ colptr,
                                                         const int32_t *__restrict__ crow, const T *__restrict__ cval,
@@ -95,7 +154,7 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
                                                         const T *__restrict__ ev, const T *__restrict__ p, int64_t m,
                                                         int64_t d, int64_t nW, int64_t r0, int64_t r1, otf_pair<T> pf,
                                                         T *__restrict__ raw, const cg_scalars<T> *__restrict__ status) {
-    constexpr int CW = otf_cw<T>();
+    constexpr int CW = otf_cw<T, CWB>();
     __shared__ T S[OTF_NT / 64][CW];
     if (status != nullptr && status->converged) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -107,11 +166,11 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
     const T ni = norms[i], ei = ev != nullptr ? ev[i] : T(1);
     double acc = 0.0;
     for (int64_t W = 0; W < nW; ++W) {
-        const int64_t j0 = W * CW;
+        const int j0 = (int) (W * CW);
         const int32_t *c_lo = cwo + W * d, *c_hi = c_lo + d;
-        for (int64_t q = 0; q < nz; q += 64) {
-            // lane k: feature q + k of row i, its value and its segment [lo, lo + len) of this window
-            const int64_t k = q + lane;
+        for (int64_t q0 = 0; q0 < nz; q0 += 64) {
+            // lane k: feature q0 + k of row i, its value and its segment [lo, lo + len) of this window
+            const int64_t k = q0 + lane;
             int64_t lo = 0;
             int len = 0;
             T v = T(0);
@@ -122,35 +181,7 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
                 lo = colptr[f] + a;
                 len = c_hi[f] - a;
             }
-            const int nk = (int) (nz - q < 64 ? nz - q : 64);
-            for (int u = 0; u < nk; u += OTF_U) {
-                int64_t lo_u[OTF_U];
-                int len_u[OTF_U];
-                T v_u[OTF_U];
-                int mx = 0;
-#pragma unroll
-                for (int x = 0; x < OTF_U; ++x) {
-                    const int src = u + x < 64 ? u + x : 63;
-                    lo_u[x] = rl64(lo, src);
-                    len_u[x] = u + x < nk ? rl32(len, src) : 0;
-                    v_u[x] = rlT(v, src);
-                    mx = len_u[x] > mx ? len_u[x] : mx;
-                }
-                for (int o = 0; o < mx; o += 64) {
-                    int jj[OTF_U];
-                    T vv[OTF_U];
-#pragma unroll
-                    for (int x = 0; x < OTF_U; ++x) {  // every segment load in flight before the first update
-                        const bool ok = o + lane < len_u[x];
-                        const int64_t t = lo_u[x] + o + lane;
-                        jj[x] = ok ? crow[t] - (int) j0 : -1;
-                        vv[x] = ok ? cval[t] : T(0);
-                    }
-#pragma unroll
-                    for (int x = 0; x < OTF_U; ++x)  // features in ascending order (one wave: LDS in program order)
-                        if (jj[x] >= 0) s[jj[x]] = fma(v_u[x], vv[x], s[jj[x]]);
-                }
-            }
+            otf_batch<T>(s, crow, cval, j0, (int) (nz - q0 < 64 ? nz - q0 : 64), lo, len, v, lane);
         }
         // the window's pair terms, lane-strided (fixed order); the accumulators are left zeroed
         for (int t = lane; t < CW; t += 64) {
@@ -173,7 +204,7 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
 // device bytes and an estimated time (s) of one on-the-fly K·p share, from the host CSR / CSC counts
 template <typename T>
 double engine<T>::otf_estimate_s(const int64_t *rowptr, const int32_t *col, const std::vector<int64_t> &colptr) const {
-    const int64_t CW = otf_cw<T>(), nW = ceil_div(std::max<int64_t>(m, 1), CW);
+    const int64_t CW = otf_cwb() / (int64_t) sizeof(T), nW = ceil_div(std::max<int64_t>(m, 1), CW);
     double fill = 0.0;  // column-segment entries walked: sum over the rank's entries of their column length
     for (int64_t k = rowptr[r0]; k < rowptr[r1]; ++k) fill += (double) (colptr[col[k] + 1] - colptr[col[k]]);
     const double nnz_r = (double) (rowptr[r1] - rowptr[r0]), R = (double) (r1 - r0);
@@ -184,7 +215,7 @@ double engine<T>::otf_estimate_s(const int64_t *rowptr, const int32_t *col, cons
 
 template <typename T>
 void engine<T>::setup_otf(int rbf_fact_ok) {
-    const int64_t CW = otf_cw<T>();
+    const int64_t CW = otf_cwb() / (int64_t) sizeof(T);
     csr.otf_cw = (int) CW;
     csr.otf_nw = ceil_div(std::max<int64_t>(m, 1), CW);
     csr.cwo.alloc((csr.otf_nw + 1) * d, stream, false);
@@ -223,10 +254,16 @@ void engine<T>::otf_dominant(const T *p, const cg_scalars<T> *status) {
         pf.form = csr.rbf_factored ? 0 : 1;
     }
     pf.kappa = kappa;
-    hipLaunchKernelGGL(otf_kp_kernel<T>, dim3((unsigned) ceil_div(r1 - r0, OTF_NT / 64)), dim3(OTF_NT), 0, stream,
-                       csr.rowptr.get(), csr.col.get(), csr.val.get(), csr.colptr.get(), csr.crow.get(), csr.cval.get(),
-                       csr.cwo.get(), norms.get(), kernel == 2 ? csr.e.get() : nullptr, p, m, d, csr.otf_nw, r0, r1, pf,
-                       raw.get(), status);
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((unsigned) ceil_div(r1 - r0, OTF_NT / 64)), dim3(OTF_NT), 0, stream,
+                           csr.rowptr.get(), csr.col.get(), csr.val.get(), csr.colptr.get(), csr.crow.get(),
+                           csr.cval.get(), csr.cwo.get(), norms.get(), kernel == 2 ? csr.e.get() : nullptr, p, m, d,
+                           csr.otf_nw, r0, r1, pf, raw.get(), status);
+    };
+    const int cwb = csr.otf_cw * (int) sizeof(T);
+    if (cwb == 32768) launch(otf_kp_kernel<T, 32768>);
+    else if (cwb == 16384) launch(otf_kp_kernel<T, 16384>);
+    else launch(otf_kp_kernel<T, 8192>);
     MI_LAUNCH_CHECK();
 }
 
