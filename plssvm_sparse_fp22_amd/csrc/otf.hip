@@ -6,7 +6,7 @@
 // tiles win.
 //
 // One wave owns one row i and an LDS row of CW partner accumulators. For each window of CW partners it
-// walks the CSC segments of row i's features restricted to that window (row-local window offsets cwo),
+// walks the CSC segments of row i's features restricted to that window (segment table seg[f][W]),
 // lanes over the segment's entries (a column holds distinct rows, so the lanes of one feature never
 // collide): s[j] = fma(x_if, x_jf, s[j]) feature by feature in ascending order — the same fma chain as
 // the dense dot product over the densified rows. Then the window is scanned once: every non-zero s_ij,
@@ -25,17 +25,54 @@ namespace plssvm_mi {
 namespace {
 
 constexpr int OTF_NT = 256;   // 4 waves (rows) per workgroup; 5 workgroups per CU by LDS
-constexpr int OTF_U = 8;      // features whose segment loads are in flight together
+#ifndef OTF_U_DEF
+#define OTF_U_DEF 8
+#endif
+#ifndef OTF_ATOMIC
+#define OTF_ATOMIC 0
+#endif
+constexpr int OTF_U = OTF_U_DEF;  // features whose segment loads are in flight together
 constexpr int OTF_BINMAX = 16;
+constexpr int OTF_SCAN = 8;  // scan steps (64 partners each) whose partner loads are in flight together
 
-// partner accumulators per wave: CWB bytes (8 / 16 / 32 KiB; PLSSVM_MI_OTF_CWB, default 8 KiB)
+// a CSC entry (row j, value) as one aligned vector load: a short column segment touches one contiguous
+// range instead of two (the row and value arrays)
+template <typename T>
+struct alignas(2 * sizeof(T)) otf_jv {
+    int32_t j;
+    T v;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void otf_jv_kernel(const int32_t *__restrict__ crow, const T *__restrict__ cval,
+                                                     int64_t nnz, otf_jv<T> *__restrict__ cjv) {
+    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < nnz) cjv[t] = otf_jv<T>{ crow[t], cval[t] };
+}
+
+// a partner's p_j, |x_j|^2 and e_j packed for one vector load in the window scan (rebuilt per K·p)
+template <typename T>
+struct alignas(4 * sizeof(T)) pne_t {
+    T p, n, e, pad;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void otf_pack_kernel(const T *__restrict__ p, const T *__restrict__ norms,
+                                                       const T *__restrict__ ev, int64_t m, pne_t<T> *__restrict__ pne,
+                                                       const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    const int64_t j = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < m) pne[j] = pne_t<T>{ p[j], norms[j], ev != nullptr ? ev[j] : T(1), T(0) };
+}
+
+// partner accumulators per wave: CWB bytes (4 / 8 / 16 / 32 KiB; PLSSVM_MI_OTF_CWB, default 8 KiB)
 template <typename T, int CWB>
 constexpr int otf_cw() { return CWB / (int) sizeof(T); }
 inline int otf_cwb() {
     static const int v = [] {
         const char *e = std::getenv("PLSSVM_MI_OTF_CWB");
         const int b = e != nullptr ? std::atoi(e) : 8192;
-        return (b == 16384 || b == 32768) ? b : 8192;
+        return (b == 4096 || b == 16384 || b == 32768) ? b : 8192;
     }();
     return v;
 }
@@ -79,21 +116,45 @@ __device__ __forceinline__ int64_t rl64(int64_t x, int l) {
 __device__ __forceinline__ float rlT(float x, int l) { return __int_as_float(rl32(__float_as_int(x), l)); }
 __device__ __forceinline__ double rlT(double x, int l) { return __longlong_as_double(rl64(__double_as_longlong(x), l)); }
 
-// cwo[W][f] = #{ t in column f : crow[t] < W CW }  (W = 0..nW; CSC rows ascending inside a column)
-__global__ __launch_bounds__(256) void otf_cwo_kernel(const int64_t *__restrict__ colptr,
+// seg[f][W] = (first entry of column f with row >= W CW, column-local; #entries with row in window W), so one
+// aligned 8-byte load gives a feature's segment of a window (CSC rows ascending inside a column)
+__global__ __launch_bounds__(256) void otf_seg_kernel(const int64_t *__restrict__ colptr,
                                                       const int32_t *__restrict__ crow, int64_t d, int64_t nW,
-                                                      int64_t CW, int32_t *__restrict__ cwo) {
+                                                      int64_t CW, int2 *__restrict__ seg) {
     const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (nW + 1) * d) return;
-    const int64_t W = t / d, f = t - W * d;
-    const int64_t a = colptr[f], key = W * CW;
-    int64_t lo = a, hi = colptr[f + 1];
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int64_t) crow[mid] < key) lo = mid + 1;
-        else hi = mid;
-    }
-    cwo[t] = (int32_t) (lo - a);
+    if (t >= nW * d) return;
+    const int64_t f = t / nW, W = t - f * nW;
+    const int64_t a = colptr[f], b = colptr[f + 1];
+    auto first_at_least = [&](int64_t key) {
+        int64_t lo = a, hi = b;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t) crow[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    const int64_t lo = first_at_least(W * CW), hi = first_at_least((W + 1) * CW);
+    seg[t] = make_int2((int) (lo - a), (int) (hi - lo));
+}
+
+// ecb[k] = colptr[col[k]]: the CSC start of each CSR entry's column (read coalesced with the row)
+__global__ __launch_bounds__(256) void otf_ecb_kernel(const int64_t *__restrict__ colptr, const int32_t *__restrict__ col,
+                                                      int64_t nnz, int64_t *__restrict__ ecb) {
+    const int64_t k = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nnz) ecb[k] = colptr[col[k]];
+}
+
+// s += a in LDS: read-add-write (the lanes of one feature never share a j; one wave's LDS operations
+// complete in issue order). OTF_ATOMIC = 1 uses no-return LDS atomic adds instead: measured 1.4x (1 %
+// density) to 2.7x (5 %) slower on gfx950.
+template <typename T>
+__device__ __forceinline__ void otf_add(T *a, T v) {
+#if OTF_ATOMIC
+    __hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#else
+    *a += v;
+#endif
 }
 
 // One batch of up to 64 features of row i against the partner window [j0, j0 + CW): lane k holds feature
@@ -103,8 +164,8 @@ __global__ __launch_bounds__(256) void otf_cwo_kernel(const int64_t *__restrict_
 // loads entry 0 with length 0). A longer segment's further entries follow right after its first 64, so
 // every s_ij accumulates its features in ascending order.
 template <typename T>
-__device__ __forceinline__ void otf_batch(T *__restrict__ s, const int32_t *__restrict__ crow,
-                                          const T *__restrict__ cval, int j0, int nk, int64_t lo, int len, T v,
+__device__ __forceinline__ void otf_batch(T *__restrict__ s, const otf_jv<T> *__restrict__ cjv, int j0, int nk,
+                                          int64_t lo, int len, T v,
                                           int lane) {
     int64_t lo_c[OTF_U], lo_n[OTF_U];
     int len_c[OTF_U], len_n[OTF_U], jj_c[OTF_U], jj_n[OTF_U];
@@ -117,8 +178,9 @@ __device__ __forceinline__ void otf_batch(T *__restrict__ s, const int32_t *__re
             len_x[x] = u + x < nk ? rl32(len, src) : 0;
             v_x[x] = rlT(v, src);
             const int64_t t = lane < len_x[x] ? lo_x[x] + lane : 0;
-            jj_x[x] = crow[t];  // raw loads: validity is tested at the update, not here (keeps them in flight)
-            vv_x[x] = cval[t];
+            const otf_jv<T> e = cjv[t];  // raw load: validity is tested at the update, not here (keeps it in flight)
+            jj_x[x] = e.j;
+            vv_x[x] = e.v;
         }
     };
     fetch(0, lo_c, len_c, v_c, jj_c, vv_c);
@@ -126,15 +188,12 @@ __device__ __forceinline__ void otf_batch(T *__restrict__ s, const int32_t *__re
         fetch(u + OTF_U, lo_n, len_n, v_n, jj_n, vv_n);
 #pragma unroll
         for (int x = 0; x < OTF_U; ++x) {
-            if (lane < len_c[x]) {
-                const int j = jj_c[x] - j0;
-                s[j] = fma(v_c[x], vv_c[x], s[j]);
-            }
+            if (lane < len_c[x]) otf_add(s + (jj_c[x] - j0), v_c[x] * vv_c[x]);
             for (int o = 64; o < len_c[x]; o += 64) {  // segments longer than a wave (dense columns)
                 if (o + lane < len_c[x]) {
                     const int64_t t = lo_c[x] + o + lane;
-                    const int j = crow[t] - j0;
-                    s[j] = fma(v_c[x], cval[t], s[j]);
+                    const otf_jv<T> e = cjv[t];
+                    otf_add(s + (e.j - j0), v_c[x] * e.v);
                 }
             }
         }
@@ -148,11 +207,10 @@ __device__ __forceinline__ void otf_batch(T *__restrict__ s, const int32_t *__re
 // raw[i] = sum_{j != i, s_ij != 0} c_ij p_j for this rank's rows i in [r0, r1)
 template <typename T, int CWB>
 __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
-                                                        const T *__restrict__ val, const int64_t *__restrict__ colptr,
-                                                        const int32_t *__restrict__ crow, const T *__restrict__ cval,
-                                                        const int32_t *__restrict__ cwo, const T *__restrict__ norms,
-                                                        const T *__restrict__ ev, const T *__restrict__ p, int64_t m,
-                                                        int64_t d, int64_t nW, int64_t r0, int64_t r1, otf_pair<T> pf,
+                                                        const T *__restrict__ val, const int64_t *__restrict__ ecb,
+                                                        const otf_jv<T> *__restrict__ cjv, const int2 *__restrict__ seg, const T *__restrict__ norms,
+                                                        const T *__restrict__ ev, const pne_t<T> *__restrict__ pne, int64_t m,
+                                                        int64_t nW, int64_t r0, int64_t r1, otf_pair<T> pf,
                                                         T *__restrict__ raw, const cg_scalars<T> *__restrict__ status) {
     constexpr int CW = otf_cw<T, CWB>();
     __shared__ T S[OTF_NT / 64][CW];
@@ -164,12 +222,22 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
     for (int t = lane; t < CW; t += 64) s[t] = T(0);
     const int64_t b0 = rowptr[i], nz = rowptr[i + 1] - b0;
     const T ni = norms[i], ei = ev != nullptr ? ev[i] : T(1);
+    // the row's first 64 features stay in registers across the windows (feature, value, column start), and
+    // their next window's segments are loaded one window ahead
+    const bool h0 = lane < nz;
+    const int32_t f0 = h0 ? col[b0 + lane] : 0;
+    const T v0 = h0 ? val[b0 + lane] : T(0);
+    const int64_t c0 = h0 ? ecb[b0 + lane] : 0;
+    int2 sg0 = h0 ? seg[(int64_t) f0 * nW] : make_int2(0, 0);
     double acc = 0.0;
     for (int64_t W = 0; W < nW; ++W) {
         const int j0 = (int) (W * CW);
-        const int32_t *c_lo = cwo + W * d, *c_hi = c_lo + d;
-        for (int64_t q0 = 0; q0 < nz; q0 += 64) {
-            // lane k: feature q0 + k of row i, its value and its segment [lo, lo + len) of this window
+        if (nz > 0) {
+            const int2 sg = sg0;
+            sg0 = h0 && W + 1 < nW ? seg[(int64_t) f0 * nW + W + 1] : make_int2(0, 0);
+            otf_batch<T>(s, cjv, j0, (int) (nz < 64 ? nz : 64), c0 + sg.x, sg.y, v0, lane);
+        }
+        for (int64_t q0 = 64; q0 < nz; q0 += 64) {  // further features: reloaded per window
             const int64_t k = q0 + lane;
             int64_t lo = 0;
             int len = 0;
@@ -177,20 +245,32 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
             if (k < nz) {
                 const int32_t f = col[b0 + k];
                 v = val[b0 + k];
-                const int32_t a = c_lo[f];
-                lo = colptr[f] + a;
-                len = c_hi[f] - a;
+                const int2 sg = seg[(int64_t) f * nW + W];
+                lo = ecb[b0 + k] + sg.x;
+                len = sg.y;
             }
-            otf_batch<T>(s, crow, cval, j0, (int) (nz - q0 < 64 ? nz - q0 : 64), lo, len, v, lane);
+            otf_batch<T>(s, cjv, j0, (int) (nz - q0 < 64 ? nz - q0 : 64), lo, len, v, lane);
         }
-        // the window's pair terms, lane-strided (fixed order); the accumulators are left zeroed
-        for (int t = lane; t < CW; t += 64) {
-            const T sv = s[t];
-            if (sv != T(0)) {
-                s[t] = T(0);
+        // the window's pair terms, lane-strided (fixed order); the accumulators are left zeroed. The partners'
+        // (p_j, |x_j|^2, e_j) come as one packed load per lane, OTF_SCAN steps issued before their use (the
+        // loads do not depend on s_ij: one memory latency per OTF_SCAN steps, not per step)
+        for (int t0 = 0; t0 < CW; t0 += 64 * OTF_SCAN) {
+            T sv[OTF_SCAN];
+            pne_t<T> q[OTF_SCAN];
+#pragma unroll
+            for (int u = 0; u < OTF_SCAN; ++u) {
+                const int t = t0 + 64 * u + lane;
+                sv[u] = s[t];
                 const int64_t j = j0 + t;
-                if (j != i)
-                    acc += (double) otf_c<T>(pf, sv, ni, norms[j], ei, ev != nullptr ? ev[j] : T(1)) * (double) p[j];
+                q[u] = pne[j < m ? j : m - 1];
+            }
+#pragma unroll
+            for (int u = 0; u < OTF_SCAN; ++u) {
+                if (sv[u] != T(0)) {
+                    const int t = t0 + 64 * u + lane;
+                    s[t] = T(0);
+                    if (j0 + t != i) acc += (double) otf_c<T>(pf, sv[u], ni, q[u].n, ei, q[u].e) * (double) q[u].p;
+                }
             }
         }
     }
@@ -218,11 +298,22 @@ void engine<T>::setup_otf(int rbf_fact_ok) {
     const int64_t CW = otf_cwb() / (int64_t) sizeof(T);
     csr.otf_cw = (int) CW;
     csr.otf_nw = ceil_div(std::max<int64_t>(m, 1), CW);
-    csr.cwo.alloc((csr.otf_nw + 1) * d, stream, false);
-    const int64_t tot = (csr.otf_nw + 1) * d;
+    const int64_t tot = csr.otf_nw * d;
+    csr.seg.alloc(std::max<int64_t>(tot, 1), stream, false);
     if (tot > 0)
-        hipLaunchKernelGGL(otf_cwo_kernel, dim3((unsigned) ceil_div(tot, 256)), dim3(256), 0, stream, csr.colptr.get(),
-                           csr.crow.get(), d, csr.otf_nw, CW, csr.cwo.get());
+        hipLaunchKernelGGL(otf_seg_kernel, dim3((unsigned) ceil_div(tot, 256)), dim3(256), 0, stream, csr.colptr.get(),
+                           csr.crow.get(), d, csr.otf_nw, CW, csr.seg.get());
+    MI_LAUNCH_CHECK();
+    csr.pne.alloc(4 * std::max<int64_t>(m, 1), stream, false);
+    csr.cjv.alloc(2 * std::max<int64_t>(csr.nnz, 1), stream, false);
+    if (csr.nnz > 0)
+        hipLaunchKernelGGL(otf_jv_kernel<T>, dim3((unsigned) ceil_div(csr.nnz, 256)), dim3(256), 0, stream,
+                           csr.crow.get(), csr.cval.get(), csr.nnz, reinterpret_cast<otf_jv<T> *>(csr.cjv.get()));
+    MI_LAUNCH_CHECK();
+    csr.ecb.alloc(std::max<int64_t>(csr.nnz, 1), stream, false);
+    if (csr.nnz > 0)
+        hipLaunchKernelGGL(otf_ecb_kernel, dim3((unsigned) ceil_div(csr.nnz, 256)), dim3(256), 0, stream,
+                           csr.colptr.get(), csr.col.get(), csr.nnz, csr.ecb.get());
     MI_LAUNCH_CHECK();
     if (csr.ssc.get() == nullptr) csr.ssc.alloc(1, stream);
     csr.rbf_factored = kernel == 2 && rbf_form != 1 && rbf_fact_ok;
@@ -254,15 +345,20 @@ void engine<T>::otf_dominant(const T *p, const cg_scalars<T> *status) {
         pf.form = csr.rbf_factored ? 0 : 1;
     }
     pf.kappa = kappa;
+    pne_t<T> *pne = reinterpret_cast<pne_t<T> *>(csr.pne.get());
+    hipLaunchKernelGGL(otf_pack_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream, p, norms.get(),
+                       kernel == 2 ? csr.e.get() : nullptr, m, pne, status);
+    MI_LAUNCH_CHECK();
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3((unsigned) ceil_div(r1 - r0, OTF_NT / 64)), dim3(OTF_NT), 0, stream,
-                           csr.rowptr.get(), csr.col.get(), csr.val.get(), csr.colptr.get(), csr.crow.get(),
-                           csr.cval.get(), csr.cwo.get(), norms.get(), kernel == 2 ? csr.e.get() : nullptr, p, m, d,
+                           csr.rowptr.get(), csr.col.get(), csr.val.get(), csr.ecb.get(),
+                           reinterpret_cast<const otf_jv<T> *>(csr.cjv.get()), csr.seg.get(), norms.get(), kernel == 2 ? csr.e.get() : nullptr, pne, m,
                            csr.otf_nw, r0, r1, pf, raw.get(), status);
     };
     const int cwb = csr.otf_cw * (int) sizeof(T);
     if (cwb == 32768) launch(otf_kp_kernel<T, 32768>);
     else if (cwb == 16384) launch(otf_kp_kernel<T, 16384>);
+    else if (cwb == 4096) launch(otf_kp_kernel<T, 4096>);
     else launch(otf_kp_kernel<T, 8192>);
     MI_LAUNCH_CHECK();
 }

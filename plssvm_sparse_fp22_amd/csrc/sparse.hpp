@@ -114,12 +114,15 @@ struct csr_data {
     // X is densified into the engine's XT and every K·p recomputes all pairs on the MFMA tiles
     bool dense_on = false;
     int64_t est_bytes = 0;  // estimated device bytes of the chosen stored structure (0: not estimated)
-    // on-the-fly path (PLSSVM_MI_SPARSE_ONTHEFLY, otf.hip): nothing stored per pair; cwo[W][f] = the first
-    // entry of CSC column f (column-local) whose row lies in partner window W (CW rows)
+    // on-the-fly path (PLSSVM_MI_SPARSE_ONTHEFLY, otf.hip): nothing stored per pair; seg[f][W] = (first
+    // entry of CSC column f whose row lies in partner window W (CW rows), column-local; their count)
     bool otf_on = false;
     int otf_cw = 0;
     int64_t otf_nw = 0;
-    dev_buf<int32_t> cwo;  // [otf_nw + 1][d]
+    dev_buf<int2> seg;      // [d][otf_nw]
+    dev_buf<int64_t> ecb;   // [nnz]: colptr[col[k]] per CSR entry
+    dev_buf<T> pne;         // [m][4]: p_j, |x_j|^2, e_j, 0 of the current K·p
+    dev_buf<T> cjv;         // [nnz][2]: CSC (row, value) pairs (the row as int32 bits in the first slot)
 
     vals_t<T> rvals() const { return vals_t<T>{ val.get(), nullptr }; }
     vals_t<T> cvals() const { return vals_t<T>{ cval.get(), nullptr }; }
@@ -127,7 +130,7 @@ struct csr_data {
         return rowptr.bytes() + col.bytes() + val.bytes() + colptr.bytes() + crow.bytes() +
                cval.bytes() + spmv_csc.bytes() + spmv_csr.bytes() + rb_csr.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
                rb_base.bytes() + rowoff.bytes() + cells.bytes() + slab_row.bytes() + slab_col.bytes() + ex.bytes() +
-               cwo.bytes();
+               seg.bytes() + ecb.bytes() + pne.bytes() + cjv.bytes();
     }
 };
 
