@@ -84,8 +84,8 @@ extern "C" {
  *   3 = densified: X densified on the device, the dense MFMA pairwise tiles (O(m d) memory, every pair
  *       recomputed from the data on each K·p as in the reference); ERR_OOM when m x d does not fit;
  *   4 = on the fly: nothing stored per pair; every K·p re-forms s_ij for the pairs sharing a feature
- *       from the CSR rows and the CSC columns (O(nnz) memory + a d x m / 1024 window-offset table,
- *       O(sum_f c_f^2) work per K·p, as the reference recomputes every pair). */
+ *       from the CSR rows and the CSC columns (O(nnz) memory + a d x m / 2048 segment table, O(sum_f
+ *       c_f^2) work per K·p, as the reference recomputes every pair). */
 #define PLSSVM_MI_OPT_SPARSE_ALGO 4
 #define PLSSVM_MI_SPARSE_AUTO 0
 #define PLSSVM_MI_SPARSE_PATTERN 1

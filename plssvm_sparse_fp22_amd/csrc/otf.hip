@@ -288,9 +288,10 @@ double engine<T>::otf_estimate_s(const int64_t *rowptr, const int32_t *col, cons
     double fill = 0.0;  // column-segment entries walked: sum over the rank's entries of their column length
     for (int64_t k = rowptr[r0]; k < rowptr[r1]; ++k) fill += (double) (colptr[col[k] + 1] - colptr[col[k]]);
     const double nnz_r = (double) (rowptr[r1] - rowptr[r0]), R = (double) (r1 - r0);
-    // calibrated on the box: segment entries from L2 / MALL, per-(entry, window) segment
-    // set-up, and the LDS scan of every (row, window)
-    return fill * 2.0e-13 + nnz_r * (double) nW * 3.0e-12 + R * (double) m * 6.0e-14;
+    // fitted on the box (fp32 RBF, 0.1-5 % density): segment entries, per-(entry, window)
+    // segment set-up, and the LDS scan of every (row, window) partner
+    const double es = (double) sizeof(T) / 4.0;
+    return es * (fill * 4.0e-13 + nnz_r * (double) nW * 5.0e-11 + R * (double) m * 1.33e-12);
 }
 
 template <typename T>

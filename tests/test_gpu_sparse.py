@@ -196,6 +196,37 @@ def test_sparse_onthefly_learn_fp22_and_reproducible(oracle):
     np.testing.assert_allclose(outs[2], want, rtol=0, atol=1e-4 * np.abs(want).max())
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_sparse_over_budget_onthefly_sampled(dtype, monkeypatch):
+    """auto over the device budget at 1 % density (60k x 20k, 200 features per row): the setup's estimate
+    picks the on-the-fly path over the densified tiles; 128 sampled rows of sum_j k_ij p_j against a float64
+    recomputation (fp32 1e-4 / fp64 1e-12 of sum_j |k_ij p_j|)"""
+    import scipy.sparse as sp
+
+    n, d, k = 60_000, 20_000, 200
+    rng = np.random.default_rng(31)
+    col = np.concatenate([np.sort(rng.choice(d, k, replace=False)) for _ in range(n)]).astype(np.int32)
+    val = rng.uniform(-1, 1, n * k)
+    rowptr = np.arange(0, (n + 1) * k, k, dtype=np.int64)
+    monkeypatch.setenv("PLSSVM_MI_MEM_BUDGET", "4096")
+    prm = pm.Parameter("rbf", gamma=1.0 / d, real_type=dtype)
+    prm.csr = (rowptr, col, val.astype(dtype), n, d)
+    m = n - 1
+    p = rng.uniform(1, 2, m).astype(dtype)
+    with pm.CSVM(prm) as svm:
+        svm.setup_data_on_device()
+        assert svm.info()["sparse_algo"] == pm._abi.SPARSE_ONTHEFLY
+        got = svm.kp_part(p, "kernel")
+    rows = np.sort(rng.choice(m, 128, replace=False))
+    X = sp.csr_matrix((val.astype(dtype).astype(np.float64), col, rowptr), shape=(n, d))
+    nrm = np.asarray(X.multiply(X).sum(axis=1)).ravel()
+    G = (X[rows] @ X[:m].T).toarray()
+    K = np.exp(-(1.0 / d) * np.maximum(nrm[rows, None] + nrm[None, :m] - 2.0 * G, 0.0))
+    want, scale = K @ p.astype(np.float64), K @ np.abs(p.astype(np.float64))
+    err = np.max(np.abs(got[rows] - want) / scale)
+    assert err <= (1e-4 if dtype == np.float32 else 1e-12), err
+
+
 @pytest.mark.parametrize("kernel", ["rbf", "polynomial"])
 def test_sparse_over_budget_falls_back_to_densified(oracle, kernel, monkeypatch):
     """auto: a stored structure estimated above the device budget (PLSSVM_MI_MEM_BUDGET) is never built;
