@@ -303,7 +303,8 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
         rem = info["pair_slots"] * (2 + es) + info["exp_chunks"] * 2
         return dict(bound="hbm", achieved=rem / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
                     frac=rem / s / PEAKS["hbm"], traffic=None, kernel="exp_hcell_kernel", launch_ms=ms_dom,
-                    alg_bytes=rem, alg_bytes_def="remainder stream: slots x (2 + sizeof(real)) + chunks x 2",
+                    alg_bytes=rem, alg_bytes_def="remainder stream: slots x (2 + sizeof(real)) + chunks x 2 (run layout: chunks = 0, slots = entries + dummies)",
+                    stream_layout="runs" if info["exp_chunks"] == 0 else "4-slot chunks",
                     exp_terms=info["exp_terms"], multi_pairs=info["pairs"], pair_slots=info["pair_slots"],
                     spmv_bytes=info["spmv_bytes"], survey_alg_bytes=survey,
                     survey_effective_GBps=survey / s / 1e9, survey_effective_frac=survey / s / PEAKS["hbm"])

@@ -242,7 +242,7 @@ typedef struct {
     int sparse_algo;    /* sparse poly/rbf: PLSSVM_MI_SPARSE_PATTERN | _EXPANSION | _DENSE (0 otherwise) */
     int exp_terms;      /* kernel expansion: polynomial degree K of the per-feature pair function */
     int exp_waves;      /* kernel expansion: waves of the remainder stream */
-    int64_t exp_chunks; /* kernel expansion: 8-slot chunks of the remainder stream (this rank's rows) */
+    int64_t exp_chunks; /* kernel expansion: 4-slot chunks of the remainder stream (this rank's rows); 0 = run layout */
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
 

@@ -308,6 +308,75 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__
     if (Wc >= 0) close();
 }
 
+// ---- run layout (option, PLSSVM_MI_EXP_RUNS): no padding, no per-chunk row index --------------------
+// Per (row, window) exactly max(count, 1) entries: the first entry of every row carries bit 15 of its
+// window-local j (so CW <= 32768), a row without partners in the window gets one flagged dummy (j = 0,
+// H = 0). A wave's stream of a window then lists its RPW rows in order and the row of an entry is the
+// number of flags up to it: neither the 4-slot padding nor the chunk rows of the chunk layout are stored.
+template <typename T>
+__global__ __launch_bounds__(256) void exp_run_count_kernel(const int64_t *__restrict__ off8,
+                                                            const int32_t *__restrict__ sj, const T *__restrict__ sv,
+                                                            int64_t R, int64_t nW, int64_t CW, int64_t RB,
+                                                            int64_t *__restrict__ cnt,
+                                                            unsigned long long *__restrict__ dummies) {
+    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    for (int64_t W = 0; W < nW; ++W) cnt[exp_cidx(r, W, nW, RB)] = 1;  // the dummy, unless entries follow
+    int64_t Wc = -1, k = 0, filled = 0;
+    for (int64_t s = off8[r]; s < off8[r + 1]; ++s) {
+        if (sv[s] == T(0)) continue;
+        const int64_t W = sj[s] / CW;
+        if (W != Wc) {
+            if (Wc >= 0) cnt[exp_cidx(r, Wc, nW, RB)] = k;
+            Wc = W;
+            k = 0;
+            ++filled;
+        }
+        ++k;
+    }
+    if (Wc >= 0) cnt[exp_cidx(r, Wc, nW, RB)] = k;
+    atomicAdd(dummies, (unsigned long long) (nW - filled));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void exp_run_scatter_kernel(const int64_t *__restrict__ off8,
+                                                              const int32_t *__restrict__ sj, const T *__restrict__ sv,
+                                                              int64_t R, int64_t nW, int64_t CW, int64_t RB,
+                                                              const int64_t *__restrict__ coff,
+                                                              uint16_t *__restrict__ hjl, T *__restrict__ hv) {
+    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    for (int64_t W = 0; W < nW; ++W) {  // dummies (overwritten where the row has entries in W)
+        const int64_t b = coff[exp_cidx(r, W, nW, RB)];
+        hjl[b] = (uint16_t) 0x8000u;
+        hv[b] = T(0);
+    }
+    int64_t Wc = -1, base = 0, k = 0;
+    for (int64_t s = off8[r]; s < off8[r + 1]; ++s) {
+        const T h = sv[s];
+        if (h == T(0)) continue;
+        const int64_t W = sj[s] / CW;
+        if (W != Wc) {
+            Wc = W;
+            base = coff[exp_cidx(r, W, nW, RB)];
+            k = 0;
+        }
+        hjl[base + k] = (uint16_t) ((sj[s] - W * CW) | (k == 0 ? 0x8000 : 0));
+        hv[base + k] = h;
+        ++k;
+    }
+}
+
+// first entry of (block I, wave v, window W), W = 0..nW
+__global__ __launch_bounds__(256) void exp_run_woff_kernel(const int64_t *__restrict__ coff, int64_t nbv, int64_t nW,
+                                                           int64_t RB, int64_t *__restrict__ woff) {
+    const int64_t RPW = RB / EXP_NWV;
+    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nbv * (nW + 1)) return;
+    const int64_t bv = t / (nW + 1), W = t % (nW + 1);
+    woff[t] = coff[(bv * nW + W) * RPW];
+}
+
 // first chunk of (block I, wave v, window W), W = 0..nW (W = nW: the end of the wave's stream)
 __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__restrict__ coff, int64_t nbv, int64_t nW,
                                                             int64_t RB, int64_t *__restrict__ woff) {
@@ -413,6 +482,149 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             }
             const int rprev = __shfl_up(rl, 1);
             if (rl >= 0 && (lane == 0 || rprev != rl)) racc[rl] += sacc;  // rows of this wave only
+        }
+        if (W + 1 < W1) {
+            __syncthreads();  // every wave is done with window W
+            store_win();
+        }
+        __syncthreads();
+    }
+    const int64_t rb0 = I * RB;
+    const int rows = (int) min<int64_t>(RB, R - rb0);
+    if (G == 1) {
+        for (int t = tid; t < rows; t += NT) hs[r0 + rb0 + t] = racc[t];
+    } else {
+        for (int t = tid; t < rows; t += NT) hslab[g * R + rb0 + t] = racc[t];
+    }
+}
+
+// hs[i] = sum_j H_ij w_j over the run layout. Same block / window / prefetch structure as exp_hcell_kernel;
+// each lane takes 4 consecutive entries per step (4-aligned steps of 256 entries; the entries outside the
+// window's range [wo[W], wo[W + 1]) are masked, so a step that straddles two windows is loaded for both).
+// Rows: carry (flags so far) + the flags of the lower lanes (ballots) + the lane's own. A lane's entries
+// span consecutive rows h..t: the rows strictly inside and row h (when h != t, completed with the
+// segmented scan value of the previous lane) end in this lane; row t is summed across lanes by a segmented
+// inclusive scan keyed by t and added where it ends. Each row is written once per step, by this wave only,
+// in a fixed order: bitwise reproducible.
+template <typename T, int RBB>
+__global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *__restrict__ woff,
+                                                                const uint16_t *__restrict__ hjl,
+                                                                const T *__restrict__ hv, const T *__restrict__ w,
+                                                                int64_t m, int64_t r0, int64_t R, int64_t nW,
+                                                                int64_t RB, int64_t nI, int G, T *__restrict__ hs,
+                                                                T *__restrict__ hslab,
+                                                                const cg_scalars<T> *__restrict__ status) {
+    constexpr int CW = exp_cw_run<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64, PER = CW / NT;
+    __shared__ T wl[CW];
+    __shared__ T racc[RBC];
+    if (status != nullptr && status->converged) return;
+    const int64_t bx = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t I = bx % nI, g = bx / nI;
+    const int64_t W0 = g * nW / G, W1 = (g + 1) * nW / G;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int RPW = (int) (RB / EXP_NWV);
+    for (int t = tid; t < RB; t += NT) racc[t] = T(0);
+    T *ra = racc + wave * RPW;
+    T reg[PER];
+    auto load_win = [&](int64_t W) {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) {
+            const int64_t idx = W * CW + q * NT + tid;
+            reg[q] = idx < m ? w[idx] : T(0);
+        }
+    };
+    auto store_win = [&]() {
+#pragma unroll
+        for (int q = 0; q < PER; ++q) wl[q * NT + tid] = reg[q];
+    };
+    const int64_t *wo = woff + (I * EXP_NWV + wave) * (nW + 1);
+    u32x2 jj_n = { 0u, 0u };
+    T h_n[4] = { T(0), T(0), T(0), T(0) };
+    auto fetch = [&](int64_t sb) {  // sb: a multiple of 4 inside the (padded) stream
+        const int64_t e = sb + 4 * lane;
+        jj_n = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hjl + e));
+        if constexpr (sizeof(T) == 4) {
+            const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(hv + e));
+            h_n[0] = v.x, h_n[1] = v.y, h_n[2] = v.z, h_n[3] = v.w;
+        } else {
+            const f64x2 v0 = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(hv + e));
+            const f64x2 v1 = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(hv + e + 2));
+            h_n[0] = v0.x, h_n[1] = v0.y, h_n[2] = v1.x, h_n[3] = v1.y;
+        }
+    };
+    if (W0 < W1) {
+        load_win(W0);
+        store_win();
+        fetch(wo[W0] & ~int64_t(3));
+    }
+    __syncthreads();
+    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));  // lanes below this one
+    for (int64_t W = W0; W < W1; ++W) {
+        if (W + 1 < W1) load_win(W + 1);
+        const int64_t e0 = wo[W], e1 = wo[W + 1];
+        int carry = 0;  // flags (rows started) before this step in window W
+        for (int64_t sb = e0 & ~int64_t(3); sb < e1; sb += 256) {  // wave-uniform trip count
+            const u32x2 jj = jj_n;
+            const T hc[4] = { h_n[0], h_n[1], h_n[2], h_n[3] };
+            fetch(sb + 256 < e1 ? sb + 256 : (e1 & ~int64_t(3)));  // next step (the next window's first at the end)
+            const int64_t e = sb + 4 * lane;
+            const unsigned jr[4] = { jj.x & 0xFFFFu, jj.x >> 16, jj.y & 0xFFFFu, jj.y >> 16 };
+            T a[4];
+            int fl[4];
+            uint64_t nb = 0;  // flags in lower lanes
+            int tot = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool v = e + u >= e0 && e + u < e1;
+                fl[u] = v && (jr[u] & 0x8000u) ? 1 : 0;
+                a[u] = v ? hc[u] * wl[jr[u] & 0x7FFFu] : T(0);
+                const uint64_t b = __ballot(fl[u]);
+                nb += (uint64_t) __popcll(b & lt);
+                tot += __popcll(b);
+            }
+            int r[4];
+            int cum = carry + (int) nb;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                cum += fl[u];
+                r[u] = cum - 1;  // -1: entries before the window's first (masked, a = 0)
+            }
+            carry += tot;
+            const int h = r[0], t = r[3];
+            T ts = T(0), hsum = T(0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (r[u] == t) ts += a[u];
+                else if (r[u] == h) hsum += a[u];
+            }
+            // rows strictly between h and t end in this lane (at most two: 4 entries)
+            if (t - h >= 2 && h + 1 >= 0) {
+                T s1 = T(0);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (r[u] == h + 1) s1 += a[u];
+                ra[h + 1] += s1;
+            }
+            if (t - h >= 3 && h + 2 >= 0) {
+                T s2 = T(0);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (r[u] == h + 2) s2 += a[u];
+                ra[h + 2] += s2;
+            }
+            // segmented inclusive scan of the tail sums keyed by the tail row
+            T sc = ts;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const T so = __shfl_up(sc, off);
+                const int ko = __shfl_up(t, off);
+                if (lane >= off && ko == t) sc += so;
+            }
+            const T sprev = __shfl_up(sc, 1);
+            const int tprev = __shfl_up(t, 1);
+            const int hnext = __shfl_down(h, 1);
+            if (h != t && h >= 0) ra[h] += hsum + ((lane > 0 && tprev == h) ? sprev : T(0));
+            if (t >= 0 && (lane == 63 || hnext != t)) ra[t] += sc;
         }
         if (W + 1 < W1) {
             __syncthreads();  // every wave is done with window W
@@ -833,46 +1045,90 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         }
         ex.CW = exp_cw_host(ex.RBB, es);
     }
-    const int64_t CW = ex.CW, RB = ex.RB;
-    ex.nW = ceil_div(std::max<int64_t>(m, 1), CW);
+    const int64_t RB = ex.RB;
     ex.nblk = ceil_div(R, RB);
-    ex.G = (int) std::max<int64_t>(1, std::min<int64_t>(ex.G, ex.nW));
-    if (ex.G > 1) ex.hslab.alloc((int64_t) ex.G * R, stream, false);
-    const int64_t nbv = ex.nblk * EXP_NWV, ncnt = ex.nblk * RB * ex.nW;
+    const int64_t nbv = ex.nblk * EXP_NWV;
     {
         dev_buf<int64_t> cnt, coff;
-        cnt.alloc(ncnt + 1, stream);
-        coff.alloc(ncnt + 1, stream, false);
-        if (R > 0) {
-            hipLaunchKernelGGL(exp_cell_count_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                               off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, cnt.get());
-            MI_LAUNCH_CHECK();
-        }
-        size_t tb = 0;
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.get(), coff.get(), ncnt + 1, stream));
         dev_buf<unsigned char> t;
-        t.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, cnt.get(), coff.get(), ncnt + 1, stream));
-        MI_HIP_CHECK(hipMemcpyAsync(&ex.slots, coff.get() + ncnt, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-        ex.nchunks = ex.slots / 4;
-        ex.hjl.alloc(std::max<int64_t>(ex.slots, 4), stream);
-        ex.hv.alloc(std::max<int64_t>(ex.slots, 4), stream);
-        ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
-        if (R > 0) {
-            hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                               off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
-                               ex.hv.get(), ex.hrow.get());
+        auto scan = [&](int64_t ncnt) {
+            size_t tb = 0;
+            MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.get(), coff.get(), ncnt + 1, stream));
+            t.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
+            MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, cnt.get(), coff.get(), ncnt + 1, stream));
+            MI_HIP_CHECK(hipMemcpyAsync(&ex.slots, coff.get() + ncnt, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+        };
+        // PLSSVM_MI_EXP_RUNS = 1: the run layout (when its dummies, rows without partners in a window, stay
+        // under 5 % of the entries; = 2 regardless). Off by default: 11-20 % fewer bytes (config 3-RBF 7.87 ->
+        // 6.99 GB, config 5 8.89 -> 7.10 GB) but 2.5x the VALU per 256-entry step (161 vs 64: row numbering,
+        // multi-row lanes, the segmented scan), measured 1.52 vs 1.42 ms (3-RBF) and 1.74 vs 1.67 ms (5)
+        const char *re = std::getenv("PLSSVM_MI_EXP_RUNS");
+        const int runs_opt = re != nullptr ? std::atoi(re) : 0;
+        ex.runs = false;
+        if (runs_opt != 0 && R > 0) {
+            ex.CW = exp_cw_run_host(ex.RBB, (int) sizeof(T));
+            ex.nW = ceil_div(std::max<int64_t>(m, 1), (int64_t) ex.CW);
+            const int64_t ncnt = ex.nblk * RB * ex.nW;
+            cnt.alloc(ncnt + 1, stream);
+            coff.alloc(ncnt + 1, stream, false);
+            dev_buf<unsigned long long> dum;
+            dum.alloc(1, stream);
+            hipLaunchKernelGGL(exp_run_count_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                               off8.get(), sj.get(), sv.get(), R, ex.nW, (int64_t) ex.CW, RB, cnt.get(), dum.get());
             MI_LAUNCH_CHECK();
+            unsigned long long nd = 0;
+            MI_HIP_CHECK(hipMemcpyAsync(&nd, dum.get(), sizeof(nd), hipMemcpyDeviceToHost, stream));
+            scan(ncnt);
+            ex.runs = runs_opt == 2 || (double) nd <= 0.05 * (double) (ex.slots - (int64_t) nd);
+            if (ex.runs) {
+                ex.nchunks = 0;
+                ex.hjl.alloc(ex.slots + 512, stream);  // steps of 256 entries from 4-aligned starts
+                ex.hv.alloc(ex.slots + 512, stream);
+                ex.hrow.reset();
+                hipLaunchKernelGGL(exp_run_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                                   off8.get(), sj.get(), sv.get(), R, ex.nW, (int64_t) ex.CW, RB, coff.get(),
+                                   ex.hjl.get(), ex.hv.get());
+                MI_LAUNCH_CHECK();
+                ex.woff.alloc(std::max<int64_t>(nbv * (ex.nW + 1), 1), stream);
+                hipLaunchKernelGGL(exp_run_woff_kernel, dim3((unsigned) ceil_div(nbv * (ex.nW + 1), 256)), dim3(256),
+                                   0, stream, coff.get(), nbv, ex.nW, RB, ex.woff.get());
+                MI_LAUNCH_CHECK();
+            }
         }
-        ex.woff.alloc(std::max<int64_t>(nbv * (ex.nW + 1), 1), stream);
-        if (nbv > 0) {
-            hipLaunchKernelGGL(exp_cell_woff_kernel, dim3((unsigned) ceil_div(nbv * (ex.nW + 1), 256)), dim3(256), 0,
-                               stream, coff.get(), nbv, ex.nW, RB, ex.woff.get());
-            MI_LAUNCH_CHECK();
+        if (!ex.runs) {
+            ex.CW = exp_cw_host(ex.RBB, (int) sizeof(T));
+            ex.nW = ceil_div(std::max<int64_t>(m, 1), (int64_t) ex.CW);
+            const int64_t CW = ex.CW, ncnt = ex.nblk * RB * ex.nW;
+            cnt.alloc(ncnt + 1, stream);
+            coff.alloc(ncnt + 1, stream, false);
+            if (R > 0) {
+                hipLaunchKernelGGL(exp_cell_count_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                                   off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, cnt.get());
+                MI_LAUNCH_CHECK();
+            }
+            scan(ncnt);
+            ex.nchunks = ex.slots / 4;
+            ex.hjl.alloc(std::max<int64_t>(ex.slots, 4), stream);
+            ex.hv.alloc(std::max<int64_t>(ex.slots, 4), stream);
+            ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
+            if (R > 0) {
+                hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                                   off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
+                                   ex.hv.get(), ex.hrow.get());
+                MI_LAUNCH_CHECK();
+            }
+            ex.woff.alloc(std::max<int64_t>(nbv * (ex.nW + 1), 1), stream);
+            if (nbv > 0) {
+                hipLaunchKernelGGL(exp_cell_woff_kernel, dim3((unsigned) ceil_div(nbv * (ex.nW + 1), 256)), dim3(256),
+                                   0, stream, coff.get(), nbv, ex.nW, RB, ex.woff.get());
+                MI_LAUNCH_CHECK();
+            }
         }
         MI_HIP_CHECK(hipStreamSynchronize(stream));
     }
+    ex.G = (int) std::max<int64_t>(1, std::min<int64_t>(ex.G, ex.nW));
+    if (ex.G > 1) ex.hslab.alloc((int64_t) ex.G * R, stream, false);
     MI_HIP_CHECK(hipStreamSynchronize(stream));
     pt.mark("expansion: cells");
     csr.pairs = ex.pairs;
@@ -901,11 +1157,25 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
                                ex.hrow.get(), ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, (int64_t) ex.RB,
                                ex.nblk, ex.G, ex.hs.get(), ex.hslab.get(), status);
         };
-        switch (ex.RBB) {
-            case 4096: launch(exp_hcell_kernel<T, 4096>); break;
-            case 8192: launch(exp_hcell_kernel<T, 8192>); break;
-            case 32768: launch(exp_hcell_kernel<T, 32768>); break;
-            default: launch(exp_hcell_kernel<T, 16384>);
+        auto launch_run = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned) (ex.nblk * ex.G)), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
+                               ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, (int64_t) ex.RB, ex.nblk, ex.G,
+                               ex.hs.get(), ex.hslab.get(), status);
+        };
+        if (ex.runs) {
+            switch (ex.RBB) {
+                case 4096: launch_run(exp_hrun_kernel<T, 4096>); break;
+                case 8192: launch_run(exp_hrun_kernel<T, 8192>); break;
+                case 32768: launch_run(exp_hrun_kernel<T, 32768>); break;
+                default: launch_run(exp_hrun_kernel<T, 16384>);
+            }
+        } else {
+            switch (ex.RBB) {
+                case 4096: launch(exp_hcell_kernel<T, 4096>); break;
+                case 8192: launch(exp_hcell_kernel<T, 8192>); break;
+                case 32768: launch(exp_hcell_kernel<T, 32768>); break;
+                default: launch(exp_hcell_kernel<T, 16384>);
+            }
         }
         MI_LAUNCH_CHECK();
         if (ex.G > 1 && r1 > r0) {

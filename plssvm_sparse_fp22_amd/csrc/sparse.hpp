@@ -45,6 +45,10 @@ constexpr int exp_rb_of() { return RBB / (int) sizeof(T); }
 template <typename T, int RBB>
 constexpr int exp_cw_of() { return (EXP_LDS - RBB) / (int) sizeof(T) / 1024 * 1024; }
 inline int exp_cw_host(int rbb, int es) { return (EXP_LDS - rbb) / es / 1024 * 1024; }
+// the run layout keeps a flag in bit 15 of the window-local j: windows of at most 32768 partners
+template <typename T, int RBB>
+constexpr int exp_cw_run() { return exp_cw_of<T, RBB>() < 32768 ? exp_cw_of<T, RBB>() : 32768; }
+inline int exp_cw_run_host(int rbb, int es) { return exp_cw_host(rbb, es) < 32768 ? exp_cw_host(rbb, es) : 32768; }
 
 template <typename T>
 struct exp_data {
@@ -65,6 +69,7 @@ struct exp_data {
     int64_t slots = 0, nchunks = 0, nblk = 0, nW = 0;
     int RBB = 16384, RB = 0, CW = 0;  // geometry (see above): accumulator bytes, rows per block, window
     int G = 1;                         // window groups per row block (G > 1: row sums via hslab)
+    bool runs = false;                 // run layout (exp_hrun_kernel): no padding / chunk rows, see expand.hip
     dev_buf<T> hslab;                  // [G][rows] partial row sums of the window groups
     dev_buf<uint16_t> hjl;            // [slots] j - W * CW
     dev_buf<T> hv;                    // [slots] H_ij

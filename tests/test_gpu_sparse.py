@@ -258,14 +258,17 @@ def test_sparse_densified_learn_and_fp22(oracle):
     assert info["sparse_algo"] == pm._abi.SPARSE_DENSE
 
 
+@pytest.mark.parametrize("runs", ["0", "1"])
 @pytest.mark.parametrize("rbb,groups", [("4096", "1"), ("8192", "1"), ("32768", "1"), ("4096", "2"), ("8192", "3")])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_sparse_expansion_stream_geometries(oracle, rbb, groups, dtype, monkeypatch):
+def test_sparse_expansion_stream_geometries(oracle, rbb, groups, dtype, runs, monkeypatch):
     """every remainder-stream geometry (rows per block / window width, PLSSVM_MI_EXP_RBB; window groups
-    with partial row sums, PLSSVM_MI_EXP_G) against the oracle, on data whose multi-feature pairs span
-    several windows and blocks"""
+    with partial row sums, PLSSVM_MI_EXP_G) in both layouts (PLSSVM_MI_EXP_RUNS: 4-slot chunks with a row
+    per chunk / flagged runs with dummies for rows without partners in a window) against the oracle, on
+    data whose multi-feature pairs span several windows and blocks"""
     monkeypatch.setenv("PLSSVM_MI_EXP_RBB", rbb)
     monkeypatch.setenv("PLSSVM_MI_EXP_G", groups)
+    monkeypatch.setenv("PLSSVM_MI_EXP_RUNS", "2" if runs == "1" else "0")
     csr, _ = datagen.sparse_csr(42000, 600, 10, seed=21, dtype=dtype)
     info = check_sparse_kp(oracle, csr, "rbf", dtype, gamma=0.1)
     assert info["sparse_algo"] == pm._abi.SPARSE_EXPANSION and info["pairs"] > 0
