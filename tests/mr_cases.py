@@ -15,7 +15,11 @@ CASES = {
     "sparse_rbf": ("csr", "rbf", "auto", np.float64, 40),
     "sparse_poly": ("csr", "polynomial", "auto", np.float64, 40),
     "sparse_fp22_rbf": ("fp22", "rbf", "auto", np.float32, 10),
+    "sparse_rbf_onthefly": ("csr", "rbf", "auto", np.float64, 40),
+    "sparse_poly_onthefly": ("csr", "polynomial", "auto", np.float64, 40),
 }
+# sparse poly / rbf K·p algorithm per case (default: auto)
+ALGO = {"sparse_rbf_onthefly": "onthefly", "sparse_poly_onthefly": "onthefly"}
 
 
 def case_data(name):

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from mr_cases import make_case  # noqa: E402
+from mr_cases import ALGO, make_case  # noqa: E402
 
 
 def main():
@@ -30,7 +30,8 @@ def main():
     pm._abi.lib()
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     prm, kp_mode, imax = make_case(case)
-    svm = pm.CSVM(prm, device=0, rank=rank, world_size=world, kp_mode=kp_mode, exchange=pm.torch_exchange(dist))
+    svm = pm.CSVM(prm, device=0, rank=rank, world_size=world, kp_mode=kp_mode, exchange=pm.torch_exchange(dist),
+                  sparse_algo=ALGO.get(case, "auto"))
     svm.setup_data_on_device()
     q = svm.generate_q()
     m = svm.m

@@ -23,7 +23,7 @@ import sys
 import numpy as np
 import pytest
 
-from mr_cases import CASES, case_data
+from mr_cases import ALGO, CASES, case_data
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -98,7 +98,7 @@ def test_world2_group_matches_oracle(oracle, case, tmp_path):
     if layout == "dense" and kp_mode != "factored":
         assert sum(int(r["tiles_local"]) for r in res) == int(res[0]["tiles_total"])
         assert all(int(r["tiles_local"]) > 0 for r in res)
-    if layout != "dense" and kernel != "linear":
+    if layout != "dense" and kernel != "linear" and case not in ALGO:  # stored pairs (the on-the-fly path stores none)
         assert all(int(r["pairs"]) > 0 for r in res)
     for rank, r in enumerate(res):
         assert int(r["world"]) == world
