@@ -407,9 +407,9 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     // block (I, g) streams only windows [g nW / G, (g + 1) nW / G) of its rows and writes its row sums
     // to hslab[g][rows] (summed in g order by exp_hslab_reduce_kernel); the blocks of one XCD share g,
     // so they share w's windows in L2
-    constexpr int CW = exp_cw_of<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64, PER = CW / NT;
+    constexpr int CW = exp_cw_of<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64;
     static_assert(CW <= 65536, "window-local partner indices are 16-bit");
-    __shared__ T wl[CW];
+    __shared__ __attribute__((aligned(16))) T wl[CW];
     __shared__ T racc[RBC];
     if (status != nullptr && status->converged) return;
     const int64_t bx = xcd_remap(blockIdx.x, gridDim.x);
@@ -417,17 +417,31 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     const int64_t W0 = g * nW / G, W1 = (g + 1) * nW / G;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int t = tid; t < RB; t += NT) racc[t] = T(0);
-    T reg[PER];
+    // the window of w moves as 16-byte vectors: thread tid takes vectors tid, tid + NT, ... (PV of them)
+    constexpr int VE = 16 / (int) sizeof(T), NV = CW / VE, PV = (NV + NT - 1) / NT;
+    using wvec = __attribute__((ext_vector_type(VE))) T;
+    wvec reg[PV];
     auto load_win = [&](int64_t W) {
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int64_t idx = W * CW + q * NT + tid;
-            reg[q] = idx < m ? w[idx] : T(0);
+        for (int q = 0; q < PV; ++q) {
+            const int v = q * NT + tid;
+            if (NV % NT == 0 || v < NV) {
+                const int64_t idx = W * CW + (int64_t) v * VE;
+                if (idx + VE <= m) {
+                    reg[q] = *reinterpret_cast<const wvec *>(w + idx);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < VE; ++e) reg[q][e] = idx + e < m ? w[idx + e] : T(0);
+                }
+            }
         }
     };
     auto store_win = [&]() {
 #pragma unroll
-        for (int q = 0; q < PER; ++q) wl[q * NT + tid] = reg[q];
+        for (int q = 0; q < PV; ++q) {
+            const int v = q * NT + tid;
+            if (NV % NT == 0 || v < NV) reinterpret_cast<wvec *>(wl)[v] = reg[q];
+        }
     };
     const int64_t *wo = woff + (I * EXP_NWV + wave) * (nW + 1);
     const int64_t s_end = wo[W1];
@@ -514,8 +528,8 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *_
                                                                 int64_t RB, int64_t nI, int G, T *__restrict__ hs,
                                                                 T *__restrict__ hslab,
                                                                 const cg_scalars<T> *__restrict__ status) {
-    constexpr int CW = exp_cw_run<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64, PER = CW / NT;
-    __shared__ T wl[CW];
+    constexpr int CW = exp_cw_run<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64;
+    __shared__ __attribute__((aligned(16))) T wl[CW];
     __shared__ T racc[RBC];
     if (status != nullptr && status->converged) return;
     const int64_t bx = xcd_remap(blockIdx.x, gridDim.x);
@@ -525,17 +539,31 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *_
     const int RPW = (int) (RB / EXP_NWV);
     for (int t = tid; t < RB; t += NT) racc[t] = T(0);
     T *ra = racc + wave * RPW;
-    T reg[PER];
+    // the window of w moves as 16-byte vectors: thread tid takes vectors tid, tid + NT, ... (PV of them)
+    constexpr int VE = 16 / (int) sizeof(T), NV = CW / VE, PV = (NV + NT - 1) / NT;
+    using wvec = __attribute__((ext_vector_type(VE))) T;
+    wvec reg[PV];
     auto load_win = [&](int64_t W) {
 #pragma unroll
-        for (int q = 0; q < PER; ++q) {
-            const int64_t idx = W * CW + q * NT + tid;
-            reg[q] = idx < m ? w[idx] : T(0);
+        for (int q = 0; q < PV; ++q) {
+            const int v = q * NT + tid;
+            if (NV % NT == 0 || v < NV) {
+                const int64_t idx = W * CW + (int64_t) v * VE;
+                if (idx + VE <= m) {
+                    reg[q] = *reinterpret_cast<const wvec *>(w + idx);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < VE; ++e) reg[q][e] = idx + e < m ? w[idx + e] : T(0);
+                }
+            }
         }
     };
     auto store_win = [&]() {
 #pragma unroll
-        for (int q = 0; q < PER; ++q) wl[q * NT + tid] = reg[q];
+        for (int q = 0; q < PV; ++q) {
+            const int v = q * NT + tid;
+            if (NV % NT == 0 || v < NV) reinterpret_cast<wvec *>(wl)[v] = reg[q];
+        }
     };
     const int64_t *wo = woff + (I * EXP_NWV + wave) * (nW + 1);
     u32x2 jj_n = { 0u, 0u };
