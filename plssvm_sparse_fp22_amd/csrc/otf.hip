@@ -211,6 +211,7 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
                                                         const otf_jv<T> *__restrict__ cjv, const int2 *__restrict__ seg, const T *__restrict__ norms,
                                                         const T *__restrict__ ev, const pne_t<T> *__restrict__ pne, int64_t m,
                                                         int64_t nW, int64_t r0, int64_t r1, otf_pair<T> pf,
+                                                        int64_t Wa, int64_t Wb, double *__restrict__ part,
                                                         T *__restrict__ raw, const cg_scalars<T> *__restrict__ status) {
     constexpr int CW = otf_cw<T, CWB>();
     __shared__ T S[OTF_NT / 64][CW];
@@ -228,13 +229,13 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
     const int32_t f0 = h0 ? col[b0 + lane] : 0;
     const T v0 = h0 ? val[b0 + lane] : T(0);
     const int64_t c0 = h0 ? ecb[b0 + lane] : 0;
-    int2 sg0 = h0 ? seg[(int64_t) f0 * nW] : make_int2(0, 0);
+    int2 sg0 = h0 ? seg[(int64_t) f0 * nW + Wa] : make_int2(0, 0);
     double acc = 0.0;
-    for (int64_t W = 0; W < nW; ++W) {
+    for (int64_t W = Wa; W < Wb; ++W) {
         const int j0 = (int) (W * CW);
         if (nz > 0) {
             const int2 sg = sg0;
-            sg0 = h0 && W + 1 < nW ? seg[(int64_t) f0 * nW + W + 1] : make_int2(0, 0);
+            sg0 = h0 && W + 1 < Wb ? seg[(int64_t) f0 * nW + W + 1] : make_int2(0, 0);
             otf_batch<T>(s, cjv, j0, (int) (nz < 64 ? nz : 64), c0 + sg.x, sg.y, v0, lane);
         }
         for (int64_t q0 = 64; q0 < nz; q0 += 64) {  // further features: reloaded per window
@@ -276,7 +277,11 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
-    if (lane == 0) raw[i] = (T) acc;
+    if (lane == 0) {  // windows [Wa, Wb) of a K·p split over launches: partial sums in window order
+        if (Wa > 0) acc += part[i];
+        if (Wb == nW) raw[i] = (T) acc;
+        else part[i] = acc;
+    }
 }
 
 }  // namespace
@@ -306,6 +311,8 @@ void engine<T>::setup_otf(int rbf_fact_ok) {
                            csr.crow.get(), d, csr.otf_nw, CW, csr.seg.get());
     MI_LAUNCH_CHECK();
     csr.pne.alloc(4 * std::max<int64_t>(m, 1), stream, false);
+    csr.otf_part.alloc(std::max<int64_t>(m, 1), stream, false);
+    if (const char *e = std::getenv("PLSSVM_MI_OTF_WPL")) csr.otf_wpl = std::max<long long>(0, std::atoll(e));
     csr.cjv.alloc(2 * std::max<int64_t>(csr.nnz, 1), stream, false);
     if (csr.nnz > 0)
         hipLaunchKernelGGL(otf_jv_kernel<T>, dim3((unsigned) ceil_div(csr.nnz, 256)), dim3(256), 0, stream,
@@ -350,11 +357,20 @@ void engine<T>::otf_dominant(const T *p, const cg_scalars<T> *status) {
     hipLaunchKernelGGL(otf_pack_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream, p, norms.get(),
                        kernel == 2 ? csr.e.get() : nullptr, m, pne, status);
     MI_LAUNCH_CHECK();
+    // windows per launch (PLSSVM_MI_OTF_WPL; default: all in one launch). Splitting the windows over
+    // launches keeps every wave of the GPU on the same partner window (its CSC segments shared through
+    // the L2s / Infinity Cache): measured no gain at 1 % density (1 / 4 / all windows per launch: 0.626 /
+    // 0.605 / 0.610 s), the segment walk is bound by its scattered L2 misses either way
+    const int64_t nW = csr.otf_nw, wpl = csr.otf_wpl > 0 ? csr.otf_wpl : nW;
     auto launch = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3((unsigned) ceil_div(r1 - r0, OTF_NT / 64)), dim3(OTF_NT), 0, stream,
-                           csr.rowptr.get(), csr.col.get(), csr.val.get(), csr.ecb.get(),
-                           reinterpret_cast<const otf_jv<T> *>(csr.cjv.get()), csr.seg.get(), norms.get(), kernel == 2 ? csr.e.get() : nullptr, pne, m,
-                           csr.otf_nw, r0, r1, pf, raw.get(), status);
+        for (int64_t Wa = 0; Wa < nW; Wa += wpl) {
+            const int64_t Wb = std::min(nW, Wa + wpl);
+            hipLaunchKernelGGL(kern, dim3((unsigned) ceil_div(r1 - r0, OTF_NT / 64)), dim3(OTF_NT), 0, stream,
+                               csr.rowptr.get(), csr.col.get(), csr.val.get(), csr.ecb.get(),
+                               reinterpret_cast<const otf_jv<T> *>(csr.cjv.get()), csr.seg.get(), norms.get(),
+                               kernel == 2 ? csr.e.get() : nullptr, pne, m, nW, r0, r1, pf, Wa, Wb, csr.otf_part.get(),
+                               raw.get(), status);
+        }
     };
     const int cwb = csr.otf_cw * (int) sizeof(T);
     if (cwb == 32768) launch(otf_kp_kernel<T, 32768>);

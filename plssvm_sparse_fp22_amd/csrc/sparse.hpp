@@ -124,10 +124,12 @@ struct csr_data {
     bool otf_on = false;
     int otf_cw = 0;
     int64_t otf_nw = 0;
+    int64_t otf_wpl = 0;    // partner windows per launch (0: all; PLSSVM_MI_OTF_WPL at setup)
     dev_buf<int2> seg;      // [d][otf_nw]
     dev_buf<int64_t> ecb;   // [nnz]: colptr[col[k]] per CSR entry
     dev_buf<T> pne;         // [m][4]: p_j, |x_j|^2, e_j, 0 of the current K·p
     dev_buf<T> cjv;         // [nnz][2]: CSC (row, value) pairs (the row as int32 bits in the first slot)
+    dev_buf<double> otf_part;  // [m]: row sums of the windows done so far (K·p split over launches)
 
     vals_t<T> rvals() const { return vals_t<T>{ val.get(), nullptr }; }
     vals_t<T> cvals() const { return vals_t<T>{ cval.get(), nullptr }; }
@@ -135,7 +137,7 @@ struct csr_data {
         return rowptr.bytes() + col.bytes() + val.bytes() + colptr.bytes() + crow.bytes() +
                cval.bytes() + spmv_csc.bytes() + spmv_csr.bytes() + rb_csr.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
                rb_base.bytes() + rowoff.bytes() + cells.bytes() + slab_row.bytes() + slab_col.bytes() + ex.bytes() +
-               seg.bytes() + ecb.bytes() + pne.bytes() + cjv.bytes();
+               seg.bytes() + ecb.bytes() + pne.bytes() + cjv.bytes() + otf_part.bytes();
     }
 };
 

@@ -138,6 +138,22 @@ def test_sparse_onthefly_ragged_and_linear_pairwise(oracle):
     check_sparse_kp(oracle, csr, "linear", np.float64, mode="pairwise", algo="onthefly")
 
 
+def test_sparse_onthefly_windows_over_launches(monkeypatch):
+    """PLSSVM_MI_OTF_WPL: the partner windows split over several launches (row sums carried in fp64 between
+    them) give the one-launch K·p to rounding"""
+    csr, _ = datagen.sparse_csr(9000, 3000, 25, seed=13, dtype=np.float64)
+    m = csr[3] - 1
+    x = np.linspace(1, 2, m)
+    outs = []
+    for wpl in ("0", "3"):
+        monkeypatch.setenv("PLSSVM_MI_OTF_WPL", wpl)
+        svm = sparse_svm(csr, "rbf", np.float64, algo="onthefly")
+        svm.setup_data_on_device()
+        outs.append(svm.kp_part(x, "kernel"))
+        svm.close()
+    np.testing.assert_allclose(outs[1], outs[0], rtol=1e-13, atol=1e-13 * np.abs(outs[0]).max())
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_sparse_onthefly_simulated_ranks(world):
     """rank shares (rows split) sum to the single-rank K·p"""
