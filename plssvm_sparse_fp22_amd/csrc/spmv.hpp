@@ -116,7 +116,9 @@ struct spmv_plan {
     }
 };
 
-// FP22: both words are loaded unconditionally (the packed array carries one word of padding)
+// FP22: the two words holding the value come as one 8-byte load at 4-byte alignment (gfx950 global
+// loads take dword-aligned dwordx2; the packed array carries one word of padding)
+typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 template <typename T, bool F22>
 __device__ __forceinline__ T sell_val(const vals_t<T> &val, int64_t k) {
     if constexpr (F22) {
@@ -124,8 +126,8 @@ __device__ __forceinline__ T sell_val(const vals_t<T> &val, int64_t k) {
         const int bit = 22 * (int) (k & 15);
         const uint32_t *w = val.v22 + g * 11 + (bit >> 5);
         const int sh = bit & 31;
-        const uint64_t lo = __builtin_nontemporal_load(w), hi = __builtin_nontemporal_load(w + 1);
-        return (T) fp22_decode((uint32_t) (((hi << 32) | lo) >> sh));
+        const u32x2_a4 ww = __builtin_nontemporal_load(reinterpret_cast<const u32x2_a4 *>(w));
+        return (T) fp22_decode((uint32_t) ((((uint64_t) ww.y << 32) | ww.x) >> sh));
     } else {
         return __builtin_nontemporal_load(val.v + k);
     }
