@@ -186,7 +186,7 @@ template <typename T, int KERNEL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_per_eu<T, KERNEL>(), kp_waves_per_eu<T, KERNEL>()))) void kp_tile_kernel(kfun<T> kf, const T *__restrict__ XT,
                                                          const T *__restrict__ norms, const T *__restrict__ p,
                                                          T *__restrict__ partial, int64_t n_pad, int64_t d_pad,
-                                                         int64_t nb, int64_t s0,
+                                                         int64_t nb, int64_t s0, int64_t n_full, int rl,
                                                          const cg_scalars<T> *__restrict__ status) {
     using M = mfma16<T>;
     using acc_t = typename M::acc_t;
@@ -208,10 +208,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
 
     if (status != nullptr && status->converged) return;
 
+    // workgroups: 64 per super-block, but only 8 rl per super-block of the ragged last super-block row
+    // (rl tile rows): no empty workgroups bunched at the end of the range, so the XCDs' contiguous
+    // ranges carry equal work (they made the last rank of 8 3.9 % slower than the others)
     const int64_t wg = xcd_remap(blockIdx.x, gridDim.x);
-    int64_t SI, SJ;
-    tri_tile(s0 + wg / (KP_SUPER * KP_SUPER), SI, SJ);
-    const int slot = (int) (wg % (KP_SUPER * KP_SUPER));
+    int64_t SI, SJ, sb;
+    int slot;
+    if (wg < n_full * (KP_SUPER * KP_SUPER)) {
+        sb = s0 + wg / (KP_SUPER * KP_SUPER);
+        slot = (int) (wg % (KP_SUPER * KP_SUPER));
+    } else {
+        const int64_t w2 = wg - n_full * (KP_SUPER * KP_SUPER);
+        sb = s0 + n_full + w2 / (KP_SUPER * rl);
+        slot = (int) (w2 % (KP_SUPER * rl));
+    }
+    tri_tile(sb, SI, SJ);
     const int64_t I = SI * KP_SUPER + slot / KP_SUPER, J = SJ * KP_SUPER + slot % KP_SUPER;
     if (I >= nb || J > I) return;  // uniform per workgroup
     const int64_t I0 = I * KP_TILE, J0 = J * KP_TILE;
@@ -394,6 +405,51 @@ __global__ __launch_bounds__(256) void kp_reduce_kernel(const T *__restrict__ pa
     raw[i] = s;
 }
 
+// one rank's share (s0, s1 not the whole triangle): raw[i] = sum of the slab rows of the rank's own
+// super-blocks. A rank owning the bottom rows of the triangle sees up to nb slab rows per row i, so the
+// column super-blocks are split over the 16 waves of a block (64 rows per block, lanes = rows: coalesced)
+// and the 16 partial sums are added in wave order: a fixed order, deterministic; the critical path per
+// thread is 1/16 of the row (one thread per row made the last rank of 8 4 % slower than the others)
+constexpr int KP_RED_G = 16;
+template <typename T>
+__global__ __launch_bounds__(64 * KP_RED_G) void kp_reduce_share_kernel(const T *__restrict__ partial, int64_t nb,
+                                                                        int64_t n_pad, int64_t m, int64_t s0,
+                                                                        int64_t s1, T *__restrict__ raw,
+                                                                        const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    __shared__ T red[KP_RED_G][64];
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t i = (int64_t) blockIdx.x * 64 + lane;
+    const int64_t ns = (nb + KP_SUPER - 1) / KP_SUPER;
+    T s = 0;
+    if (i < m) {
+        const int64_t RS = (i / KP_TILE) / KP_SUPER;
+        const int64_t cs0 = g * ns / KP_RED_G, cs1 = (g + 1) * ns / KP_RED_G;
+        for (int64_t CS = cs0; CS < cs1; ++CS) {
+            const int64_t sb = (RS >= CS) ? tri_index(RS, CS) : tri_index(CS, RS);
+            if (sb < s0 || sb >= s1) continue;
+            const int64_t c0 = CS * KP_SUPER, c1 = min(nb, c0 + KP_SUPER);
+            if (c1 - c0 == KP_SUPER) {
+                T v[KP_SUPER];
+#pragma unroll
+                for (int u = 0; u < KP_SUPER; ++u) v[u] = partial[(c0 + u) * n_pad + i];
+#pragma unroll
+                for (int u = 0; u < KP_SUPER; ++u) s += v[u];
+            } else {
+                for (int64_t c = c0; c < c1; ++c) s += partial[c * n_pad + i];
+            }
+        }
+    }
+    red[g][lane] = s;
+    __syncthreads();
+    if (g == 0 && i < m) {
+        T a = red[0][lane];
+#pragma unroll
+        for (int h = 1; h < KP_RED_G; ++h) a += red[h][lane];
+        raw[i] = a;
+    }
+}
+
 }  // namespace
 
 template <typename T>
@@ -403,19 +459,21 @@ void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *par
     // 32-bit DMA offsets inside a chunk (kp_tile_kernel): (BK - 1) rows of n_pad plus a tile row
     if ((int64_t) kp_dpad<T>() * n_pad * (int64_t) sizeof(T) >= ((int64_t) 1 << 31))
         throw mi_error(-5, "too many points for the pairwise tile kernel's 32-bit chunk offsets");
-    const dim3 grid((unsigned) (nsuper * KP_SUPER * KP_SUPER)), block(256);
+    const int64_t ns = ceil_div(nb, KP_SUPER), rl = nb - (ns - 1) * KP_SUPER;
+    const int64_t n_full = std::min(nsuper, std::max<int64_t>(0, tri_index(ns - 1, 0) - s0));
+    const dim3 grid((unsigned) (n_full * KP_SUPER * KP_SUPER + (nsuper - n_full) * KP_SUPER * rl)), block(256);
     switch (kf.kernel) {
         case 0:
             hipLaunchKernelGGL((kp_tile_kernel<T, 0>), grid, block, 0, s, kf, XT, norms, p, partial, n_pad, d_pad, nb,
-                               s0, status);
+                               s0, n_full, (int) rl, status);
             break;
         case 1:
             hipLaunchKernelGGL((kp_tile_kernel<T, 1>), grid, block, 0, s, kf, XT, norms, p, partial, n_pad, d_pad, nb,
-                               s0, status);
+                               s0, n_full, (int) rl, status);
             break;
         default:
             hipLaunchKernelGGL((kp_tile_kernel<T, 2>), grid, block, 0, s, kf, XT, norms, p, partial, n_pad, d_pad, nb,
-                               s0, status);
+                               s0, n_full, (int) rl, status);
             break;
     }
     MI_LAUNCH_CHECK();
@@ -426,8 +484,13 @@ void launch_kp_reduce(const T *partial, int64_t nb, int64_t n_pad, int64_t m, in
                       const cg_scalars<T> *status, hipStream_t s) {
     if (m <= 0) return;
     const int64_t ns = ceil_div(nb, KP_SUPER);
-    hipLaunchKernelGGL(kp_reduce_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, partial, nb, n_pad, m,
-                       s0, s1, ns * (ns + 1) / 2, raw, status);
+    if (s0 == 0 && s1 == ns * (ns + 1) / 2) {
+        hipLaunchKernelGGL(kp_reduce_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, partial, nb, n_pad,
+                           m, s0, s1, ns * (ns + 1) / 2, raw, status);
+    } else {
+        hipLaunchKernelGGL(kp_reduce_share_kernel<T>, dim3((unsigned) ceil_div(m, 64)), dim3(64 * KP_RED_G), 0, s,
+                           partial, nb, n_pad, m, s0, s1, raw, status);
+    }
     MI_LAUNCH_CHECK();
 }
 
