@@ -48,6 +48,17 @@ T host_kernel(int kernel, int degree, T gamma, T coef0, const T *a, const T *b, 
 // Balanced contiguous ranges of 8x8-tile super-blocks of the lower triangle (each holds 64 tiles,
 // diagonal ones 36, edge ones fewer): rank r gets the super-blocks whose cumulative tile count
 // crosses [r, r+1) * total / world. Host-only (plssvm_mi_partition exposes it for CPU tests).
+void kp_tile_offsets(int64_t nb, int64_t s0, int64_t nsuper, std::vector<int32_t> &wg_off) {
+    wg_off.assign((size_t) nsuper + 1, 0);
+    for (int64_t k = 0; k < nsuper; ++k) {
+        int64_t SI, SJ;
+        tri_tile(s0 + k, SI, SJ);
+        const int64_t rows = std::min<int64_t>(KP_SUPER, nb - SI * KP_SUPER), cols = std::min<int64_t>(KP_SUPER, nb - SJ * KP_SUPER);
+        const int64_t tiles = SI == SJ ? rows * (rows + 1) / 2 : rows * cols;
+        wg_off[(size_t) k + 1] = (int32_t) (wg_off[(size_t) k] + tiles);
+    }
+}
+
 void partition_superblocks(int64_t nb, int rank, int world, int64_t &s0, int64_t &s1, int64_t &s_total,
                            int64_t &tiles_total, int64_t &tiles_local) {
     const int64_t ns = ceil_div(nb, KP_SUPER);
@@ -232,6 +243,7 @@ void engine<T>::finish_setup() {
     } else {
         partial.reset();
     }
+    tiles_upload();
     q.alloc(vec_len, stream);
     pv.alloc(vec_len, stream);
     ret.alloc(vec_len, stream);
@@ -247,6 +259,17 @@ void engine<T>::finish_setup() {
     have_q = false;
     cg_active = false;
     graph_reset();
+}
+
+// the tile kernel's workgroup table for this rank's super-blocks [t0, t1) (also the densified sparse path)
+template <typename T>
+void engine<T>::tiles_upload() {
+    std::vector<int32_t> off;
+    kp_tile_offsets(nb, t0, t1 - t0, off);
+    kp_wgs = off.back();
+    kp_wgoff.alloc((int64_t) off.size(), stream, false);
+    MI_HIP_CHECK(hipMemcpyAsync(kp_wgoff.get(), off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice, stream));
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
 }
 
 template <typename T>
@@ -304,7 +327,7 @@ void engine<T>::kp_raw(const T *p, const cg_scalars<T> *status) {
         launch_gemv_n<T>(XT.get(), n_pad, d, r0, r1, w.get(), raw.get(), status, stream);
         allgather_rows(raw.get());
     } else {
-        launch_kp_tiles<T>(kf(), XT.get(), norms.get(), p, partial.get(), n_pad, d_pad, nb, t0, t1 - t0, status,
+        launch_kp_tiles<T>(kf(), XT.get(), norms.get(), p, partial.get(), n_pad, d_pad, nb, t0, t1 - t0, kp_wgoff.get(), kp_wgs, status,
                            stream);
         launch_kp_reduce<T>(partial.get(), nb, n_pad, m, t0, t1, raw.get(), status, stream);
         allreduce(raw.get(), m);
@@ -576,7 +599,7 @@ void engine<T>::time_kp(int reps, double *ms_kp, double *ms_dom) {
         } else if (factored()) {
             launch_gemv_n<T>(XT.get(), n_pad, d, r0, r1, w.get(), raw.get(), nullptr, stream);
         } else {
-            launch_kp_tiles<T>(kf(), XT.get(), norms.get(), pv.get(), partial.get(), n_pad, d_pad, nb, t0, t1 - t0,
+            launch_kp_tiles<T>(kf(), XT.get(), norms.get(), pv.get(), partial.get(), n_pad, d_pad, nb, t0, t1 - t0, kp_wgoff.get(), kp_wgs,
                                nullptr, stream);
         }
         MI_HIP_CHECK(hipEventRecord(d1, stream));

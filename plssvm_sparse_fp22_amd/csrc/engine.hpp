@@ -54,6 +54,9 @@ struct engine : engine_base {
     // work split
     int64_t t_total = 0, t0 = 0, t1 = 0;  // pairwise tile super-blocks owned by this rank: [t0, t1) of t_total
     int64_t tiles_total = 0, tiles_local = 0;
+    dev_buf<int32_t> kp_wgoff;  // tile kernel workgroup table (kp_tile_offsets), kp_wgs workgroups
+    int64_t kp_wgs = 0;
+    void tiles_upload();
     int64_t r0 = 0, r1 = 0, chunk = 0;    // rows owned by this rank (factored / sparse row paths)
 
     // ---- vectors (n_pad, zero padded) ----

@@ -1,6 +1,8 @@
 // Launcher declarations for the MI355X PLSSVM hot-path kernels (implemented in *.hip).
 #pragma once
 
+#include <vector>
+
 #include "common.hpp"
 
 namespace plssvm_mi {
@@ -53,9 +55,13 @@ void launch_q_dense(kfun<T> kf, const T *XT, int64_t n_pad, int64_t d, int64_t m
 constexpr int KP_SUPER = 8;
 
 // partial[c][i]: sum_{j in col-block c} k(x_i,x_j) p_j for the tiles of super-blocks [s0, s0+nsuper)
+// wg_off[k] (k = 0..nsuper): first workgroup of super-block s0 + k (one workgroup per real tile: 64 for a
+// full super-block, 36 for a diagonal one, fewer in the ragged last row); wgs = wg_off[nsuper]
+void kp_tile_offsets(int64_t nb, int64_t s0, int64_t nsuper, std::vector<int32_t> &wg_off);
 template <typename T>
 void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *partial, int64_t n_pad, int64_t d_pad,
-                     int64_t nb, int64_t s0, int64_t nsuper, const cg_scalars<T> *status, hipStream_t s);
+                     int64_t nb, int64_t s0, int64_t nsuper, const int32_t *wg_off, int64_t wgs,
+                     const cg_scalars<T> *status, hipStream_t s);
 
 // raw[i] = sum_c partial[c][i] over the tiles whose super-block lies in [s0, s1); i < m
 template <typename T>

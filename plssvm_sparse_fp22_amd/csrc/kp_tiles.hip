@@ -186,7 +186,8 @@ template <typename T, int KERNEL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_per_eu<T, KERNEL>(), kp_waves_per_eu<T, KERNEL>()))) void kp_tile_kernel(kfun<T> kf, const T *__restrict__ XT,
                                                          const T *__restrict__ norms, const T *__restrict__ p,
                                                          T *__restrict__ partial, int64_t n_pad, int64_t d_pad,
-                                                         int64_t nb, int64_t s0, int64_t n_full, int rl,
+                                                         int64_t nb, int64_t s0, int64_t nsuper,
+                                                         const int32_t *__restrict__ wg_off,
                                                          const cg_scalars<T> *__restrict__ status) {
     using M = mfma16<T>;
     using acc_t = typename M::acc_t;
@@ -208,22 +209,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
 
     if (status != nullptr && status->converged) return;
 
-    // workgroups: 64 per super-block, but only 8 rl per super-block of the ragged last super-block row
-    // (rl tile rows): no empty workgroups bunched at the end of the range, so the XCDs' contiguous
-    // ranges carry equal work (they made the last rank of 8 3.9 % slower than the others)
+    // workgroups: one per real tile. wg_off[k] = first workgroup of the rank's super-block s0 + k (a full
+    // super-block has 64 tiles, a diagonal one 36, the ragged last super-block row fewer): no empty
+    // workgroups, so the XCDs' contiguous ranges carry equal work (empty ones bunched at the end of a
+    // range made the last rank of 8 3.9 % slower than the others)
     const int64_t wg = xcd_remap(blockIdx.x, gridDim.x);
-    int64_t SI, SJ, sb;
-    int slot;
-    if (wg < n_full * (KP_SUPER * KP_SUPER)) {
-        sb = s0 + wg / (KP_SUPER * KP_SUPER);
-        slot = (int) (wg % (KP_SUPER * KP_SUPER));
-    } else {
-        const int64_t w2 = wg - n_full * (KP_SUPER * KP_SUPER);
-        sb = s0 + n_full + w2 / (KP_SUPER * rl);
-        slot = (int) (w2 % (KP_SUPER * rl));
+    int lo = 0, hi = (int) nsuper;  // largest k with wg_off[k] <= wg
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t) wg_off[mid] <= wg) lo = mid;
+        else hi = mid;
     }
+    const int64_t sb = s0 + lo, local = wg - wg_off[lo];
+    int64_t SI, SJ;
     tri_tile(sb, SI, SJ);
-    const int64_t I = SI * KP_SUPER + slot / KP_SUPER, J = SJ * KP_SUPER + slot % KP_SUPER;
+    int64_t ta, tb;  // tile row / column inside the super-block
+    if (SI == SJ) {
+        tri_tile(local, ta, tb);  // lower triangle, tb <= ta
+    } else {
+        const int64_t cols = min<int64_t>(KP_SUPER, nb - SJ * KP_SUPER);
+        ta = local / cols;
+        tb = local % cols;
+    }
+    const int64_t I = SI * KP_SUPER + ta, J = SJ * KP_SUPER + tb;
     if (I >= nb || J > I) return;  // uniform per workgroup
     const int64_t I0 = I * KP_TILE, J0 = J * KP_TILE;
     const bool diag = (I == J);
@@ -454,26 +462,25 @@ __global__ __launch_bounds__(64 * KP_RED_G) void kp_reduce_share_kernel(const T 
 
 template <typename T>
 void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *partial, int64_t n_pad, int64_t d_pad,
-                     int64_t nb, int64_t s0, int64_t nsuper, const cg_scalars<T> *status, hipStream_t s) {
-    if (nsuper <= 0 || nb <= 0) return;
+                     int64_t nb, int64_t s0, int64_t nsuper, const int32_t *wg_off, int64_t wgs,
+                     const cg_scalars<T> *status, hipStream_t s) {
+    if (nsuper <= 0 || nb <= 0 || wgs <= 0) return;
     // 32-bit DMA offsets inside a chunk (kp_tile_kernel): (BK - 1) rows of n_pad plus a tile row
     if ((int64_t) kp_dpad<T>() * n_pad * (int64_t) sizeof(T) >= ((int64_t) 1 << 31))
         throw mi_error(-5, "too many points for the pairwise tile kernel's 32-bit chunk offsets");
-    const int64_t ns = ceil_div(nb, KP_SUPER), rl = nb - (ns - 1) * KP_SUPER;
-    const int64_t n_full = std::min(nsuper, std::max<int64_t>(0, tri_index(ns - 1, 0) - s0));
-    const dim3 grid((unsigned) (n_full * KP_SUPER * KP_SUPER + (nsuper - n_full) * KP_SUPER * rl)), block(256);
+    const dim3 grid((unsigned) wgs), block(256);
     switch (kf.kernel) {
         case 0:
             hipLaunchKernelGGL((kp_tile_kernel<T, 0>), grid, block, 0, s, kf, XT, norms, p, partial, n_pad, d_pad, nb,
-                               s0, n_full, (int) rl, status);
+                               s0, nsuper, wg_off, status);
             break;
         case 1:
             hipLaunchKernelGGL((kp_tile_kernel<T, 1>), grid, block, 0, s, kf, XT, norms, p, partial, n_pad, d_pad, nb,
-                               s0, n_full, (int) rl, status);
+                               s0, nsuper, wg_off, status);
             break;
         default:
             hipLaunchKernelGGL((kp_tile_kernel<T, 2>), grid, block, 0, s, kf, XT, norms, p, partial, n_pad, d_pad, nb,
-                               s0, n_full, (int) rl, status);
+                               s0, nsuper, wg_off, status);
             break;
     }
     MI_LAUNCH_CHECK();
@@ -496,7 +503,8 @@ void launch_kp_reduce(const T *partial, int64_t nb, int64_t n_pad, int64_t m, in
 
 #define INST(T)                                                                                                  \
     template void launch_kp_tiles<T>(kfun<T>, const T *, const T *, const T *, T *, int64_t, int64_t, int64_t, \
-                                     int64_t, int64_t, const cg_scalars<T> *, hipStream_t);                    \
+                                     int64_t, int64_t, const int32_t *, int64_t, const cg_scalars<T> *,        \
+                                     hipStream_t);                                                              \
     template void launch_kp_reduce<T>(const T *, int64_t, int64_t, int64_t, int64_t, int64_t, T *,             \
                                       const cg_scalars<T> *, hipStream_t);
 INST(float)
