@@ -802,8 +802,18 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                     std::fprintf(stderr, "[plssvm_mi] unstored sparse K·p: on the fly ~%.3g s, densified ~%.3g s\n", t_otf,
                                  t_dense);
             }
-            if (otf) setup_otf(fact_ok ? 1 : 0);
-            else setup_sparse_dense();
+            if (otf) {
+                try {
+                    setup_otf(fact_ok ? 1 : 0);
+                } catch (const mi_error &e) {  // its tables did not fit either: the densified path decides
+                    if (e.code != -4 || sparse_algo == 4) throw;
+                    MI_HIP_CHECK(hipStreamSynchronize(stream));
+                    csr.seg.reset(), csr.ecb.reset(), csr.pne.reset(), csr.cjv.reset(), csr.otf_part.reset();
+                    csr.otf_on = false;
+                    otf = false;
+                }
+            }
+            if (!otf) setup_sparse_dense();
         }
     }
 }
