@@ -387,6 +387,28 @@ __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__res
     woff[t] = coff[(bv * nW + W) * RPW] >> 2;
 }
 
+#ifndef EXP_DPP
+#define EXP_DPP 1  // remainder stream: segmented row sums by DPP row shifts / broadcasts (0: ds_bpermute shuffles)
+#endif
+
+// one step of a segmented inclusive lane scan keyed by k (keys non-decreasing in lane order): v += the DPP
+// source lane's v when that lane holds the same key (lanes without a source keep v)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_step(float &v, int k) {
+    const float vs = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xF, false));
+    const int ks = __builtin_amdgcn_update_dpp(-2, k, CTRL, ROWS, 0xF, false);
+    if (ks == k) v += vs;
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_step(double &v, int k) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int) (uint32_t) b, CTRL, ROWS, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int) (b >> 32), CTRL, ROWS, 0xF, false);
+    const double vs = __longlong_as_double((long long) (((uint64_t) (uint32_t) hi << 32) | (uint32_t) lo));
+    const int ks = __builtin_amdgcn_update_dpp(-2, k, CTRL, ROWS, 0xF, false);
+    if (ks == k) v += vs;
+}
+
 // hs[i] = sum_j H_ij w_j. One 1024-thread workgroup per block of RB rows walks the windows of
 // partners: the window of w (CW values) is staged in LDS (the next window is loaded into registers
 // while the current one is used, then stored between two barriers), each wave streams its rows' 4-slot chunks (one
@@ -486,6 +508,20 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
                 acc = fma(h2, wb[jj.y & 0xFFFFu], acc);
                 acc = fma(h3, wb[jj.y >> 16], acc);
             }
+#if EXP_DPP
+            // segmented inclusive prefix sums over the lanes by DPP (rows are non-decreasing in lane order):
+            // row_shr 1/2/4/8 inside each 16-lane row, then row_bcast 15 / 31 across rows; the total of a
+            // row's run lands on its last lane, which adds it to the row accumulator
+            T sacc = acc;
+            seg_step<0x111, 0xF>(sacc, rl);  // row_shr:1
+            seg_step<0x112, 0xF>(sacc, rl);  // row_shr:2
+            seg_step<0x114, 0xF>(sacc, rl);  // row_shr:4
+            seg_step<0x118, 0xF>(sacc, rl);  // row_shr:8
+            seg_step<0x142, 0xA>(sacc, rl);  // row_bcast:15 (rows 1, 3)
+            seg_step<0x143, 0xC>(sacc, rl);  // row_bcast:31 (rows 2, 3)
+            const int rnext = __builtin_amdgcn_update_dpp(-2, rl, 0x130, 0xF, 0xF, false);  // wave_shl:1
+            if (rl >= 0 && (lane == 63 || rnext != rl)) racc[rl] += sacc;  // rows of this wave only
+#else
             // segmented suffix sums: rows are non-decreasing in lane order
             T sacc = acc;
 #pragma unroll
@@ -496,6 +532,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             }
             const int rprev = __shfl_up(rl, 1);
             if (rl >= 0 && (lane == 0 || rprev != rl)) racc[rl] += sacc;  // rows of this wave only
+#endif
         }
         if (W + 1 < W1) {
             __syncthreads();  // every wave is done with window W
