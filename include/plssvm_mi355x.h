@@ -192,6 +192,18 @@ PLSSVM_MI_API int plssvm_mi_kp_part(plssvm_mi_ctx *ctx, const void *p, void *out
 PLSSVM_MI_API int plssvm_mi_solve_cg(plssvm_mi_ctx *ctx, const void *b, const void *q, int64_t imax, double eps, void *x_out,
                        double *delta_trace, int64_t *iters);
 
+/* Progress of plssvm_mi_solve_cg / plssvm_mi_learn — the per-iteration output of the reference's
+ * solver_CG when print_info is set (src/plssvm/backends/OpenMP/csvm.cpp:115-117,161-166;
+ * gpu_csvm.cpp:233-321). The CG runs on the device and the host polls it once per batch of
+ * iterations (4, 8, 16, ..., then blocks of 50); after each batch fn(first, count, deltas, target,
+ * batch_ms, user) is called with the batch's iterations [first, first + count) (0-based),
+ * deltas[0..count] = r^T r before iteration `first`, ..., after the batch's last iteration,
+ * target = eps^2 delta0 (the stop bound) and the batch's wall time in ms. fn == NULL: no calls.
+ * The callback must not call back into the context. */
+typedef void (*plssvm_mi_progress_fn)(int64_t first, int64_t count, const double *deltas, double target,
+                                      double batch_ms, void *user);
+PLSSVM_MI_API int plssvm_mi_set_progress(plssvm_mi_ctx *ctx, plssvm_mi_progress_fn fn, void *user);
+
 /* Stepwise CG on the same device state (used by bench.py to time single iterations):
  * begin = x0 = 1, r = b - Q~x, d = r; step runs n iterations (ignores convergence when
  * force != 0); result copies x and the trace out. */

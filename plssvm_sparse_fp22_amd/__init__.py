@@ -50,24 +50,42 @@ def partition(m, rank, world_size):
 def torch_exchange(dist, group=None):
     """Host-staged exchange (plssvm_mi_comm_init_host) over torch.distributed, e.g. gloo: every rank
     all-gathers the buffers and sums them in rank order 0..G-1, so all ranks get the same bits — the
-    reference's device_reduction, which sums devices 0..G-1 on the host (gpu_csvm.cpp:366-386)."""
+    reference's device_reduction, which sums devices 0..G-1 on the host (gpu_csvm.cpp:366-386).
+
+    Failure protocol: each payload carries one status element. A rank whose local step fails still
+    takes part in the collective (sending the failure flag), and then every rank raises, so the whole
+    group returns PLSSVM_MI_ERR_RCCL together instead of the peers waiting forever in the collective."""
     import torch
 
-    def fn(buf, op):
+    def fn(buf, op, local_error=None):
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
-        if op == _abi.XCHG_ALLGATHER:
-            count = buf.size // world
-            parts = [torch.empty(count, dtype=torch.from_numpy(buf[:0]).dtype) for _ in range(world)]
-            dist.all_gather(parts, torch.from_numpy(buf[rank * count:(rank + 1) * count].copy()), group=group)
-            for r in range(world):
-                buf[r * count:(r + 1) * count] = parts[r].numpy()
+        count = buf.size // world if op == _abi.XCHG_ALLGATHER else buf.size
+        dt = torch.from_numpy(buf[:0]).dtype
+        payload = torch.zeros(count + 1, dtype=dt)
+        try:
+            if local_error is not None:
+                raise local_error
+            src = buf[rank * count:(rank + 1) * count] if op == _abi.XCHG_ALLGATHER else buf
+            payload[:count] = torch.from_numpy(src.copy())
+        except Exception as e:  # noqa: BLE001 — still join the collective, flagged
+            payload.zero_()
+            payload[count] = 1
+            err = e
         else:
-            parts = [torch.empty(buf.size, dtype=torch.from_numpy(buf[:0]).dtype) for _ in range(world)]
-            dist.all_gather(parts, torch.from_numpy(buf.copy()), group=group)
-            acc = parts[0].numpy().copy()
+            err = None
+        parts = [torch.empty(count + 1, dtype=dt) for _ in range(world)]
+        dist.all_gather(parts, payload, group=group)
+        failed = [r for r in range(world) if float(parts[r][count]) != 0.0]
+        if failed:
+            raise RuntimeError(f"host exchange failed on rank(s) {failed}") from err
+        if op == _abi.XCHG_ALLGATHER:
+            for r in range(world):
+                buf[r * count:(r + 1) * count] = parts[r][:count].numpy()
+        else:
+            acc = parts[0][:count].numpy().copy()
             for r in range(1, world):
-                acc += parts[r].numpy()
+                acc += parts[r][:count].numpy()
             buf[:] = acc
 
     return fn
@@ -188,6 +206,9 @@ class CSVM:
 
     @staticmethod
     def _exchange_cb(exchange, world_size):
+        # exchange(buf, op) must be collective even when it fails: torch_exchange flags a local failure
+        # inside its collective so every rank raises (a custom exchange that raises before its collective
+        # leaves the peers waiting in theirs)
         def cb(ptr, count, real_bytes, op, user):
             try:
                 n = count * (world_size if op == _abi.XCHG_ALLGATHER else 1)

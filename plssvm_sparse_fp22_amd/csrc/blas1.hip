@@ -187,8 +187,9 @@ __device__ __forceinline__ void store_partials(T v1, T v2, T *red, T *__restrict
 // per-thread element order (and every sum) is unchanged.
 constexpr int CG_PRE = 2;
 
-// slabs != null: raw_i = sum_{k < P} slabs[k * m + i], summed as panel_reduce_kernel does (from 0, in
-// panel order: bitwise the reduced pass output)
+// slabs != null: raw_i = sum_{k < P} slabs[k * m + i], summed as panel_reduce_kernel does — from 0 in
+// panel order, and for P >= 16 (its split form) as four quarter sums of ceil(P / 4) panels combined
+// ((q0 + q1) + q2) + q3 — so Ad is bitwise the reduced pass output the other K·p calls see
 template <typename T>
 __global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__ raw, const T *__restrict__ slabs,
                                                          int64_t P, const T *__restrict__ q,
@@ -201,9 +202,20 @@ __global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__
     const int64_t i0 = (int64_t) blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t) gridDim.x * blockDim.x;
     auto load_raw = [&](int64_t i) {
         if (slabs == nullptr) return raw[i];
-        T rw = 0;
-        for (int64_t k = 0; k < P; ++k) rw += slabs[k * m + i];
-        return rw;
+        if (P < 16) {
+            T rw = 0;
+            for (int64_t k = 0; k < P; ++k) rw += slabs[k * m + i];
+            return rw;
+        }
+        const int64_t per = (P + 3) / 4;
+        T qs[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            T a = 0;
+            for (int64_t k = u * per; k < min(P, (u + 1) * per); ++k) a += slabs[k * m + i];
+            qs[u] = a;
+        }
+        return ((qs[0] + qs[1]) + qs[2]) + qs[3];
     };
     T rw[CG_PRE], qv[CG_PRE], dv[CG_PRE];
 #pragma unroll

@@ -261,6 +261,14 @@ int plssvm_mi_solve_cg(plssvm_mi_ctx *ctx, const void *b, const void *q, int64_t
     });
 }
 
+int plssvm_mi_set_progress(plssvm_mi_ctx *ctx, plssvm_mi_progress_fn fn, void *user) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    return ctx->call([&](auto &e) {
+        e.progress = fn;
+        e.progress_user = user;
+    });
+}
+
 int plssvm_mi_cg_begin(plssvm_mi_ctx *ctx, const void *b, const void *q, double eps, double *delta0_out) {
     if (!ctx || !b) return PLSSVM_MI_ERR_ARG;
     return ctx->call([&](auto &e) {

@@ -45,20 +45,27 @@ T host_kernel(int kernel, int degree, T gamma, T coef0, const T *a, const T *b, 
 
 }  // namespace
 
-// Balanced contiguous ranges of 8x8-tile super-blocks of the lower triangle (each holds 64 tiles,
-// diagonal ones 36, edge ones fewer): rank r gets the super-blocks whose cumulative tile count
-// crosses [r, r+1) * total / world. Host-only (plssvm_mi_partition exposes it for CPU tests).
+// The tile kernel's workgroup table: wg_off[k] = the first workgroup of super-block s0 + k (one
+// workgroup per real tile: 64 in a full super-block, 36 in a diagonal one, fewer in the ragged last
+// row), wg_off[nsuper] = the grid size. Workgroup ids are 32-bit: a share of more than 2^31 - 1 tiles
+// (m beyond ~8.4M rows on one rank) is rejected.
 void kp_tile_offsets(int64_t nb, int64_t s0, int64_t nsuper, std::vector<int32_t> &wg_off) {
     wg_off.assign((size_t) nsuper + 1, 0);
+    int64_t acc = 0;
     for (int64_t k = 0; k < nsuper; ++k) {
         int64_t SI, SJ;
         tri_tile(s0 + k, SI, SJ);
         const int64_t rows = std::min<int64_t>(KP_SUPER, nb - SI * KP_SUPER), cols = std::min<int64_t>(KP_SUPER, nb - SJ * KP_SUPER);
-        const int64_t tiles = SI == SJ ? rows * (rows + 1) / 2 : rows * cols;
-        wg_off[(size_t) k + 1] = (int32_t) (wg_off[(size_t) k] + tiles);
+        acc += SI == SJ ? rows * (rows + 1) / 2 : rows * cols;
+        if (acc > (int64_t) INT32_MAX)
+            throw mi_error(-5, "the dense pairwise share of this rank exceeds 2^31 tiles: use more GPUs");
+        wg_off[(size_t) k + 1] = (int32_t) acc;
     }
 }
 
+// Balanced contiguous ranges of 8x8-tile super-blocks of the lower triangle (each holds 64 tiles,
+// diagonal ones 36, edge ones fewer): rank r gets the super-blocks whose cumulative tile count
+// crosses [r, r+1) * total / world. Host-only (plssvm_mi_partition exposes it for CPU tests).
 void partition_superblocks(int64_t nb, int rank, int world, int64_t &s0, int64_t &s1, int64_t &s_total,
                            int64_t &tiles_total, int64_t &tiles_local) {
     const int64_t ns = ceil_div(nb, KP_SUPER);
@@ -195,6 +202,29 @@ void engine<T>::allgather_rows(T *buf) {
         MI_HIP_CHECK(hipMemcpyAsync(buf, xbuf.data(), sizeof(T) * (size_t) total, hipMemcpyHostToDevice, stream));
         MI_HIP_CHECK(hipStreamSynchronize(stream));
     }
+}
+
+// Small all-gather for setup decisions that every rank of a group must take identically (the sparse
+// algorithm, its fallbacks): each rank contributes K values and gets all world x K, rank-major, through
+// RCCL or the host exchange. The values pass through the real type T, so every rank compares the same
+// rounded numbers. No group (or a simulated rank): the local values.
+template <typename T>
+std::vector<double> engine<T>::group_gather(const std::vector<double> &v) {
+    const int64_t K = (int64_t) v.size();
+    if (!in_group() || K == 0) return v;
+    std::vector<T> h((size_t) (K * world), T(0));
+    for (int64_t k = 0; k < K; ++k) h[(size_t) (rank * K + k)] = (T) v[(size_t) k];
+    if (comm != nullptr) {
+        dev_buf<T> buf;
+        buf.alloc(K * world, stream);
+        MI_HIP_CHECK(hipMemcpyAsync(buf.get(), h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice, stream));
+        MI_NCCL_CHECK(ncclAllGather(buf.get() + rank * K, buf.get(), (size_t) K, nccl_type<T>(), comm, stream));
+        MI_HIP_CHECK(hipMemcpyAsync(h.data(), buf.get(), sizeof(T) * h.size(), hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+    } else if (xchg(h.data(), K, (int) sizeof(T), 1, xchg_user) != 0) {
+        throw mi_error(-3, "host exchange failed");
+    }
+    return std::vector<double>(h.begin(), h.end());
 }
 
 template <typename T>
@@ -509,6 +539,7 @@ void engine<T>::cg_step(int64_t nsteps, bool &converged, int64_t &iters) {
     cg_scalars<T> h{};
     MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));
     MI_HIP_CHECK(hipStreamSynchronize(stream));
+    polled = h;
     converged = h.converged != 0;
     iters = h.iters;
 }
@@ -540,11 +571,22 @@ void engine<T>::solve_cg(const T *b_host, const T *q_host, int64_t imax, T eps, 
     // batches of iterations between host polls (kernels after convergence exit at entry): 4, 8, 16,
     // then up to the first reset, then whole CG_RESET blocks (one captured graph each)
     int64_t batch = 4;
+    std::vector<double> seg;
     while (!conv && run < imax) {
         const int64_t ns = std::min<int64_t>(run < CG_RESET ? std::min<int64_t>(batch, CG_RESET - run) : CG_RESET,
                                              imax - run);
+        const int64_t first = it;
+        const auto t0 = std::chrono::steady_clock::now();
         cg_step(ns, conv, it);
         batch *= 2;
+        if (progress != nullptr && it > first) {
+            // the batch's residuals delta_first .. delta_it (the iterations' "Start Iteration" lines,
+            // OpenMP/csvm.cpp:115-117), the stop target and the batch's wall time
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            seg.resize((size_t) (it - first + 1));
+            MI_HIP_CHECK(hipMemcpy(seg.data(), trace.get() + first, sizeof(double) * seg.size(), hipMemcpyDeviceToHost));
+            progress(first, it - first, seg.data(), (double) polled.eps2delta0, ms, progress_user);
+        }
     }
     cg_result(x_out, trace_out, imax + 1, iters);
 }

@@ -71,6 +71,10 @@ struct engine : engine_base {
     bool cg_active = false;
     static constexpr int CG_RESET = 50;  // r = b - Q~x every 50th iteration (csvm.cpp:119-132)
     hipGraphExec_t cg_graph = nullptr;   // one captured block of CG_RESET iterations (graph_block)
+    cg_scalars<T> polled{};               // the CG scalars read by the last cg_step poll
+    // plssvm_mi_set_progress: called by solve_cg after each polled batch of iterations
+    void (*progress)(int64_t, int64_t, const double *, double, double, void *) = nullptr;
+    void *progress_user = nullptr;
 
     engine(int kernel_, int degree_, double gamma_, double coef0_, double cost_, int device_);
     ~engine() override;
@@ -145,6 +149,9 @@ struct engine : engine_base {
                  int zfmt, int64_t np, int64_t dz, T *out);
 
     void allreduce(T *buf, int64_t count);
+    // setup decisions of a real group: every rank's K values, rank-major (world == 1: the local ones)
+    std::vector<double> group_gather(const std::vector<double> &v);
+    bool in_group() const { return world > 1 && sim_world == 0 && (comm != nullptr || xchg != nullptr); }
     void allgather_rows(T *buf);
     int64_t device_bytes() const;
 };

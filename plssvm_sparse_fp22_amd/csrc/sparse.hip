@@ -733,7 +733,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         if (sparse_algo == 2 && !elig)
             throw mi_error(-5, "the kernel expansion cannot represent this kernel on this data (Taylor degree > 16 or "
                                "the factored rbf form out of range): use the Gram pattern");
-        const int64_t budget = sparse_mem_budget();
+        int64_t budget = sparse_mem_budget();
         const bool use_exp = elig && sparse_algo != 1;
         const bool unstored = sparse_algo == 3 || sparse_algo == 4;  // forced densified / on the fly
         if (!unstored) {
@@ -742,10 +742,39 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             csr.est_bytes = use_exp ? estimate_expansion_bytes(rowptr, col, colptr, crow, inc_total)
                                     : csr.pair_bound * (int64_t) (2 * (2 + sizeof(T))) + max_inc * 48;
         }
+        // A real group takes every choice below once, identically on all ranks (the paths run different
+        // collectives on different partitions): the largest estimate against the smallest budget, the
+        // slowest on-the-fly estimate, and a fallback only when the ranks agree a build failed.
+        // (eligibility, the forced options and t_dense depend only on data and parameters every rank holds)
+        if (in_group()) {
+            const auto g = group_gather({ (double) csr.est_bytes, (double) budget });
+            double est = 0.0, bud = 0.0;
+            for (int r = 0; r < world; ++r) {
+                est = std::max(est, g[(size_t) (2 * r)]);
+                bud = r == 0 ? g[1] : std::min(bud, g[(size_t) (2 * r + 1)]);
+            }
+            csr.est_bytes = (int64_t) est;
+            budget = (int64_t) bud;
+        }
+        // a failed step of the group: the same error on every rank (the worst code; ERR_OOM = fall back)
+        auto agree = [&](int code, const std::string &why) -> int {
+            if (!in_group()) return code;
+            const auto g = group_gather({ (double) code });
+            int worst = 0;
+            for (int r = 0; r < world; ++r) {
+                const int c = (int) g[(size_t) r];
+                if (c != 0 && (worst == 0 || worst == -4)) worst = c;
+            }
+            if (worst != 0 && worst != -4)
+                throw mi_error(worst, code != 0 ? why : std::string("sparse setup failed on another rank of the group"));
+            return worst;
+        };
         pt.mark("setup_csr: incidences + size estimate");
         const bool forced = sparse_algo == 1 || sparse_algo == 2;
         bool stored = false;
         if (!unstored && (forced || csr.est_bytes <= budget)) {
+            int fail = 0;
+            std::string why;
             try {
                 if (use_exp) {
                     // the two SELL passes of the kernel expansion (the factored linear path's plans, with K channels):
@@ -779,11 +808,22 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                 }
                 stored = true;
             } catch (const mi_error &e) {
-                if (e.code != -4 || forced) throw;
+                if (!in_group() && (e.code != -4 || forced)) throw;
+                fail = e.code;
+                why = e.what();
+            } catch (const std::bad_alloc &) {
+                if (!in_group() && forced) throw;
+                fail = -4;
+                why = "host allocation failed";
+            }
+            fail = agree(fail, why);
+            if (fail != 0 && forced) throw mi_error(fail, why.empty() ? "the forced sparse structure did not fit on another rank" : why);
+            if (fail != 0) {
                 MI_HIP_CHECK(hipStreamSynchronize(stream));
                 const int64_t keep = csr.est_bytes;  // the stored structure did not fit after all: drop it
                 release_sparse_structures();
                 csr.est_bytes = keep;
+                stored = false;
             }
         }
         if (!stored) {
@@ -796,24 +836,48 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                 const double dp = (double) round_up(std::max<int64_t>(d, 1), kp_dpad<T>());
                 const int eff_world = sim_world > 0 ? sim_world : world;
                 const double t_dense = (double) m * (double) m * dp / (double) eff_world / (0.85 * peak);
-                const double t_otf = otf_estimate_s(rowptr, col, colptr);
+                double t_otf = otf_estimate_s(rowptr, col, colptr);
+                if (in_group()) {  // the slowest rank's share decides
+                    const auto g = group_gather({ t_otf });
+                    t_otf = *std::max_element(g.begin(), g.end());
+                }
                 otf = t_otf < t_dense;
                 if (std::getenv("PLSSVM_MI_TIMING") != nullptr)
                     std::fprintf(stderr, "[plssvm_mi] unstored sparse K·p: on the fly ~%.3g s, densified ~%.3g s\n", t_otf,
                                  t_dense);
             }
             if (otf) {
+                int fail = 0;
+                std::string why;
                 try {
                     setup_otf(fact_ok ? 1 : 0);
                 } catch (const mi_error &e) {  // its tables did not fit either: the densified path decides
-                    if (e.code != -4 || sparse_algo == 4) throw;
+                    if (!in_group() && (e.code != -4 || sparse_algo == 4)) throw;
+                    fail = e.code;
+                    why = e.what();
+                }
+                fail = agree(fail, why);
+                if (fail != 0 && sparse_algo == 4) throw mi_error(fail, why.empty() ? "on-the-fly setup failed on another rank" : why);
+                if (fail != 0) {
                     MI_HIP_CHECK(hipStreamSynchronize(stream));
                     csr.seg.reset(), csr.ecb.reset(), csr.pne.reset(), csr.cjv.reset(), csr.otf_part.reset();
                     csr.otf_on = false;
                     otf = false;
                 }
             }
-            if (!otf) setup_sparse_dense();
+            if (!otf) {
+                int fail = 0;
+                std::string why;
+                try {
+                    setup_sparse_dense();
+                } catch (const mi_error &e) {
+                    if (!in_group()) throw;
+                    fail = e.code;
+                    why = e.what();
+                }
+                fail = agree(fail, why);
+                if (fail != 0) throw mi_error(fail, why.empty() ? "densified setup failed on another rank of the group" : why);
+            }
         }
     }
 }

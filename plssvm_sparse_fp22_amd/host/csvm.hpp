@@ -63,15 +63,30 @@ class csvm : public csvm_interface<T> {
         q.resize(this->num_data_points_ - 1);
         return q;
     }
+    // with print_info, the reference's per-iteration lines (OpenMP/csvm.cpp:115-117,161-166): the residual
+    // before each iteration and the stop target, streamed per polled batch of device iterations; the
+    // "Done in" time of an iteration is its batch's wall time / iterations (the device runs a batch
+    // without host round trips), truncated to ms like the reference's duration_cast
     std::vector<T> solver_CG(const std::vector<T> &b, std::size_t imax, T eps, const std::vector<T> &q) override {
         check(plssvm_mi_set_qa_cost(ctx_, (double) this->QA_cost_));  // learn() computed it on the host
         std::vector<T> x(std::max<std::size_t>(b.size(), 1));
         trace_.assign(imax + 1, 0.0);
         int64_t it = 0;
-        check(plssvm_mi_solve_cg(ctx_, b.data(), q.data(), (int64_t) imax, (double) eps, x.data(), trace_.data(), &it));
+        progress_state ps{ (int64_t) imax, 0.0, 0.0, 0 };
+        if (this->print_info_) check(plssvm_mi_set_progress(ctx_, &csvm::print_progress, &ps));
+        const int rc = plssvm_mi_solve_cg(ctx_, b.data(), q.data(), (int64_t) imax, (double) eps, x.data(), trace_.data(), &it);
+        if (this->print_info_) (void) plssvm_mi_set_progress(ctx_, nullptr, nullptr);
+        check(rc);
         iterations_ = it;
         trace_.resize((std::size_t) it + 1);
         x.resize(b.size());
+        if (this->print_info_) {
+            const int64_t shown = std::min<int64_t>(it, (int64_t) imax);  // min(run + 1, imax)
+            std::printf("Finished after %lld iterations with a residuum of %s (target: %s) and an average iteration time of %lldms.\n",
+                        (long long) shown, shortest((T) trace_.back()).c_str(), shortest((T) ps.target).c_str(),
+                        (long long) (shown > 0 ? ps.ms_total / (double) shown : 0.0));
+            std::fflush(stdout);
+        }
         return x;
     }
     // gpu_csvm::update_w (gpu_csvm.cpp:327-350): w_ = sum_i alpha_i x_i (linear model vector)
@@ -210,6 +225,24 @@ class csvm : public csvm_interface<T> {
     }
 
   private:
+    struct progress_state {
+        int64_t imax;
+        double target, ms_total;
+        int64_t printed;
+    };
+    static void print_progress(int64_t first, int64_t count, const double *deltas, double target, double batch_ms, void *user) {
+        auto &ps = *static_cast<progress_state *>(user);
+        ps.target = target;
+        const double per = batch_ms / (double) count;
+        for (int64_t k = 0; k < count; ++k) {
+            std::printf("Start Iteration %lld (max: %lld) with current residuum %s (target: %s). Done in %lldms.\n",
+                        (long long) (first + k + 1), (long long) ps.imax, shortest((T) deltas[k]).c_str(),
+                        shortest((T) target).c_str(), (long long) per);
+        }
+        ps.ms_total += (double) (long long) per * (double) count;
+        ps.printed += count;
+        std::fflush(stdout);
+    }
     void need_model() {
         if (this->alpha_ptr_ == nullptr) throw exception{ "No alphas provided for prediction!" };
         if (!on_device_) setup_data_on_device();

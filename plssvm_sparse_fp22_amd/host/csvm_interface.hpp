@@ -14,8 +14,10 @@
 // path, its parser densifies).
 #pragma once
 
+#include <chrono>
 #include <cmath>
 #include <cstddef>
+#include <cstdio>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -68,11 +70,16 @@ class csvm_interface {
             throw exception{ "Number of labels (" + std::to_string(value_ptr_->size()) +
                              ") must match the number of data points (" + std::to_string(num_data_points_) + ")!" };
         setup_data_on_device();
+        auto start = std::chrono::steady_clock::now();
         const std::vector<T> q = generate_q();
         std::vector<T> b(value_ptr_->begin(), value_ptr_->end() - 1);
         for (T &v : b) v -= value_ptr_->back();
         const std::vector<T> last = point(num_data_points_ - 1);
         QA_cost_ = kernel_function(last, last) + T(1) / cost_;
+        if (print_info_) {
+            std::printf("Setup for solving the optimization problem done in %lldms.\n", (long long) ms_since(start));
+            start = std::chrono::steady_clock::now();
+        }
         std::vector<T> alpha = solver_CG(b, imax, epsilon_, q);
         T s = 0, qa = 0;
         for (const T a : alpha) s += a;
@@ -81,9 +88,17 @@ class csvm_interface {
         alpha.push_back(-s);
         alpha_ptr_ = std::make_shared<const std::vector<T>>(std::move(alpha));
         w_.clear();
+        if (print_info_) {
+            std::printf("Solved minimization problem (r = b - Ax) using CG in %lldms.\n", (long long) ms_since(start));
+            std::fflush(stdout);
+        }
     }
 
   protected:
+    static long long ms_since(std::chrono::steady_clock::time_point t) {
+        return (long long) std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t).count();
+    }
+
     // ---- pure virtual, implemented by every backend (include/plssvm/csvm.hpp:188-214) ----
     virtual void setup_data_on_device() = 0;
     [[nodiscard]] virtual std::vector<real_type> generate_q() = 0;

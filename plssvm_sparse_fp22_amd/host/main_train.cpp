@@ -96,16 +96,10 @@ int train(const cli &c) {
     }
     const int device = c.opt.count("device") ? std::stoi(c.opt.at("device")) : 0;
     csvm<T> svm(params, device);
-    const auto t1 = std::chrono::steady_clock::now();
+    // learn() prints the reference's setup line, one line per CG iteration and the solve summary
+    // (csvm.cpp:226-266, OpenMP/csvm.cpp:115-117,161-166)
     if (c.opt.count("max_iter")) svm.learn((std::size_t) std::stoll(c.opt.at("max_iter")));
     else svm.learn();
-    const auto t2 = std::chrono::steady_clock::now();
-    if (params.print_info) {
-        std::printf("Solved minimization problem (r = b - Ax) using CG in %lldms (%lld iterations, residuum %s).\n",
-                    (long long) std::chrono::duration_cast<std::chrono::milliseconds>(t2 - t1).count(),
-                    (long long) svm.iterations(),
-                    csvm<T>::shortest((T) svm.residual_trace().back()).c_str());
-    }
     svm.write_model(params.model_filename);
     if (params.print_info) std::printf("Wrote model file ('%s').\n", params.model_filename.c_str());
     return EXIT_SUCCESS;

@@ -17,9 +17,16 @@ CASES = {
     "sparse_fp22_rbf": ("fp22", "rbf", "auto", np.float32, 10),
     "sparse_rbf_onthefly": ("csr", "rbf", "auto", np.float64, 40),
     "sparse_poly_onthefly": ("csr", "polynomial", "auto", np.float64, 40),
+    "sparse_rbf_budget_split": ("csr", "rbf", "auto", np.float64, 40),
 }
 # sparse poly / rbf K·p algorithm per case (default: auto)
 ALGO = {"sparse_rbf_onthefly": "onthefly", "sparse_poly_onthefly": "onthefly"}
+# per-rank device-memory budgets (PLSSVM_MI_MEM_BUDGET, bytes): the ranks' own estimates straddle the
+# budget — rank 0 would store the kernel expansion, rank 1 cannot — so only a group-wide decision keeps
+# both on one path
+BUDGET = {"sparse_rbf_budget_split": {1: "1"}}
+# cases whose K·p stores no pairs (on the fly / densified)
+UNSTORED = set(ALGO) | set(BUDGET)
 
 
 def case_data(name):

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from mr_cases import ALGO, make_case  # noqa: E402
+from mr_cases import ALGO, BUDGET, make_case  # noqa: E402
 
 
 def main():
@@ -29,6 +29,9 @@ def main():
 
     pm._abi.lib()
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    budget = BUDGET.get(case, {}).get(rank)
+    if budget is not None:
+        os.environ["PLSSVM_MI_MEM_BUDGET"] = budget
     prm, kp_mode, imax = make_case(case)
     svm = pm.CSVM(prm, device=0, rank=rank, world_size=world, kp_mode=kp_mode, exchange=pm.torch_exchange(dist),
                   sparse_algo=ALGO.get(case, "auto"))
@@ -44,7 +47,7 @@ def main():
     np.savez(os.path.join(out, f"rank{rank}.npz"), q=q, kp_minus=kp_minus, kp_plus=kp_plus, kpart=kpart,
              alpha=svm.alpha, bias=np.float64(svm.bias), trace=np.asarray(svm.trace), iters=svm.iters,
              QA=np.float64(svm.QA_cost), tiles_local=info["tiles_local"], tiles_total=info["tiles_total"],
-             pairs=info["pairs"], world=info["world_size"])
+             pairs=info["pairs"], world=info["world_size"], sparse_algo=info["sparse_algo"])
     svm.close()
     dist.barrier()
     dist.destroy_process_group()

@@ -76,6 +76,14 @@ def check(config, points=None, dtype=None, kernel=None, rows=256, seed=11, **csv
         cfg = cfg[:3] + (dtype,) + tuple(cfg[4:])
     kern, dt = cfg[0], cfg[3]
     prm, n, d, _, extra = bench.make_problem(cfg, points, None, 0)
+    if prm.val_fmt == pm._abi.VAL_FP22 and dt == np.float64:
+        # FP22 storage is a float-context format: an fp64 run takes the FP22-rounded values as doubles
+        from plssvm_sparse_fp22_amd import fp22
+
+        rowptr, col, words, _, _ = prm.csr
+        prm.csr = (rowptr, col, fp22.unpack(words, col.size).astype(np.float64), n, d)
+        prm.val_fmt = pm._abi.VAL_REAL
+        extra = dict(csr=prm.csr)
     m = n - 1
     rng = np.random.default_rng(seed)
     pv = rng.uniform(1.0, 2.0, m).astype(dt)

@@ -80,7 +80,14 @@ def test_learn_calls_the_backend_hooks_in_order(tmp_path):
                                                                                       "learn_call_order.cpp"),
                     "-o", str(exe)], check=True)
     r = subprocess.run([str(exe), fixture_path("5x4.libsvm")], capture_output=True, text=True)
-    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr
+    out = r.stdout.strip().splitlines()
+    assert r.returncode == 0 and out[-1] == "ok", r.stderr
+    # with print_info (the parameter default), learn() prints the reference's two timing lines per call
+    # (csvm.cpp:248-250, 263-265)
+    timing = [ln for ln in out[:-1]]
+    assert timing and all(re.fullmatch(r"(Setup for solving the optimization problem done in \d+ms\.|"
+                                       r"Solved minimization problem \(r = b - Ax\) using CG in \d+ms\.)", ln)
+                          for ln in timing), timing
 
 
 def test_shipped_adapter_derives_from_the_interface(tmp_path):

@@ -1,6 +1,7 @@
 """plssvm-train (C++ host executable over the C ABI): the reference's CLI smoke test
 (`plssvm-train --help`, tests/CMakeLists.txt:115-116) on CPU, and the golden 5x4 model on the GPU."""
 import os
+import re
 import subprocess
 
 import numpy as np
@@ -102,3 +103,63 @@ def test_train_binary_input_equals_libsvm(tmp_path):
     subprocess.run([EXE, "-q", "--sparse", fixture_path("5x4.libsvm"), str(m1)], check=True)
     subprocess.run([EXE, "-q", str(b), str(m2)], check=True)
     assert open(m1).read() == open(m2).read()
+
+
+TRACE_RE = re.compile(r"^Start Iteration (\d+) \(max: (\d+)\) with current residuum (\S+) \(target: (\S+)\)\. Done in (\d+)ms\.$",
+                      re.M)
+DONE_RE = re.compile(r"^Finished after (\d+) iterations with a residuum of (\S+) \(target: (\S+)\) and an average "
+                     r"iteration time of (\d+)ms\.$", re.M)
+
+
+def _write_libsvm(path, X, y):
+    with open(path, "w") as f:
+        for xi, yi in zip(X, y):
+            f.write(f"{int(yi)} " + " ".join(f"{k}:{v!r}" for k, v in enumerate(xi.tolist())) + "\n")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["5x4", "config1_500x4", "blobs_3000x256_rbf"])
+def test_train_prints_the_reference_residual_trace(tmp_path, case, oracle):
+    """plssvm-train without -q prints the reference solver_CG's lines (OpenMP/csvm.cpp:115-117,161-166):
+    'Start Iteration k (max: imax) with current residuum delta (target: eps^2 delta0).' per iteration and
+    the 'Finished after ...' summary. The printed residual curve equals the oracle's delta trace (fp64,
+    1e-6 per iteration), the iteration count and the stop target likewise. The RBF set (config 2's shape
+    at N = 3000) runs enough iterations to cross batched polls."""
+    from plssvm_sparse_fp22_amd import datagen, io
+
+    kernel = "linear"
+    if case == "5x4":
+        path = fixture_path("5x4.libsvm")
+        X, y = io.parse_libsvm(path)
+    else:
+        if case == "config1_500x4":
+            X, y = datagen.blobs(500, 4, seed=1)
+        else:
+            X, y = datagen.blobs(3000, 256, seed=2, cluster_std=4.0)
+            kernel = "rbf"
+        path = str(tmp_path / "train.libsvm")
+        _write_libsvm(path, X, y)
+        X2, y2 = io.parse_libsvm(path)
+        assert np.array_equal(X2, X) and np.array_equal(y2, y)
+    r = subprocess.run([EXE, "-t", "2" if kernel == "rbf" else "0", path, str(tmp_path / "m.model")],
+                       capture_output=True, text=True, check=True)
+    ref = oracle.learn(kernel, oracle.Data(np.ascontiguousarray(X)), y, eps=1e-3)
+    lines = TRACE_RE.findall(r.stdout)
+    assert len(lines) == ref["iters"] > 0, r.stdout[-3000:]
+    target = 1e-6 * ref["trace"][0]
+    for k, (it, imax, delta, tgt, _) in enumerate(lines):
+        assert int(it) == k + 1 and int(imax) == X.shape[1]
+        assert abs(float(delta) - ref["trace"][k]) <= 1e-6 * ref["trace"][k], (k, delta, ref["trace"][k])
+        assert abs(float(tgt) - target) <= 1e-6 * target
+    done = DONE_RE.findall(r.stdout)
+    assert len(done) == 1
+    assert int(done[0][0]) == ref["iters"]
+    assert abs(float(done[0][1]) - ref["trace"][-1]) <= 1e-6 * ref["trace"][-1]
+    assert "Setup for solving the optimization problem done in" in r.stdout
+    assert "Solved minimization problem (r = b - Ax) using CG in" in r.stdout
+
+
+def test_quiet_train_prints_nothing_on_cpu_error():
+    """-q gates every line (parameter_train.cpp:60,124): an error still goes to stderr only."""
+    r = subprocess.run([EXE, "-q", "/nonexistent.libsvm"], capture_output=True, text=True)
+    assert r.returncode != 0 and r.stdout == ""

@@ -176,3 +176,41 @@ def test_host_exchange_over_gloo(world):
     for r in range(world):
         assert result[r]["sum_ok"]
         np.testing.assert_array_equal(result[r]["gather"], np.repeat(np.arange(1, world + 1), 7).astype(np.float32))
+
+
+def _xchg_fail_worker(rank, world, port, result):
+    import torch.distributed as dist
+
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import plssvm_sparse_fp22_amd as pm
+    from plssvm_sparse_fp22_amd import _abi
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    fn = pm.torch_exchange(dist)
+    a = np.ones(64)
+    try:
+        # the last rank's local step fails before its collective; it must still join, and every rank raises
+        fn(a, _abi.XCHG_ALLREDUCE, local_error=ValueError("local failure") if rank == world - 1 else None)
+        result[rank] = "no error"
+    except RuntimeError as e:
+        result[rank] = str(e)
+    b = np.full(8, float(rank))  # the group is still usable afterwards
+    fn(b, _abi.XCHG_ALLREDUCE)
+    result[(rank, "after")] = float(b[0])
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_exchange_failure_reaches_every_rank(world):
+    """a rank whose exchange fails locally still takes part in the collective (status
+    element), so every rank raises — the library then returns PLSSVM_MI_ERR_RCCL on all of them — and
+    nobody hangs in the collective."""
+    import torch.multiprocessing as mp
+
+    manager = mp.Manager()
+    result = manager.dict()
+    mp.spawn(_xchg_fail_worker, args=(world, _free_port(), result), nprocs=world, join=True)
+    for r in range(world):
+        assert f"rank(s) [{world - 1}]" in result[r], result[r]
+        assert result[(r, "after")] == float(sum(range(world)))

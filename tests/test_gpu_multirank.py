@@ -23,7 +23,7 @@ import sys
 import numpy as np
 import pytest
 
-from mr_cases import ALGO, CASES, case_data
+from mr_cases import ALGO, BUDGET, CASES, UNSTORED, case_data
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -98,8 +98,14 @@ def test_world2_group_matches_oracle(oracle, case, tmp_path):
     if layout == "dense" and kp_mode != "factored":
         assert sum(int(r["tiles_local"]) for r in res) == int(res[0]["tiles_total"])
         assert all(int(r["tiles_local"]) > 0 for r in res)
-    if layout != "dense" and kernel != "linear" and case not in ALGO:  # stored pairs (the on-the-fly path stores none)
+    if layout != "dense" and kernel != "linear" and case not in UNSTORED:  # stored pairs (the on-the-fly path stores none)
         assert all(int(r["pairs"]) > 0 for r in res)
+    # one K·p algorithm for the whole group, also when the ranks' own estimates straddle the budget
+    assert len({int(r["sparse_algo"]) for r in res}) == 1, [int(r["sparse_algo"]) for r in res]
+    if case in BUDGET:
+        import plssvm_sparse_fp22_amd as pm
+
+        assert int(res[0]["sparse_algo"]) in (pm._abi.SPARSE_ONTHEFLY, pm._abi.SPARSE_DENSE)
     for rank, r in enumerate(res):
         assert int(r["world"]) == world
         np.testing.assert_allclose(r["q"], q_ref, rtol=ktol, atol=ktol * np.abs(q_ref).max())
