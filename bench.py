@@ -101,7 +101,7 @@ def collective_desc(world, sim, exchange):
 
 
 def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_seconds, kp_reps, sim=None,
-               kernel=None, dtype=None, points=0, features=0, data_cache=None):
+               kernel=None, dtype=None, points=0, features=0, data_cache=None, solve=False, solve_cap_s=20.0):
     """Measure one BASELINE configuration: setup, q, r0, `warmup` + `steps` CG iterations (timed with
     a barrier and stream synchronisation on both sides, max over ranks), the dominant kernel's
     average launch time (hipEvents on the engine stream), roofline, committed PMC traffic and the
@@ -144,6 +144,28 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
         elapsed = float(t.item())
     info = svm.info()
     ms_kp, ms_dom = svm.time_kp(kp_reps)
+    learn = None
+    if solve:
+        # time to solution (csvm.cpp:226-266 reports setup and CG separately): the reference's learn() —
+        # q, then CG from x0 = 1 at the default eps = 1e-3 with imax = num_features — on the resident data
+        t_q0 = time.perf_counter()
+        q = svm.generate_q()
+        t_q = time.perf_counter() - t_q0
+        # stepwise (the same device CG as solve_cg, 50-iteration graph blocks) so the bench stays bounded: a
+        # solve that has not converged after solve_cap_s is reported with the iterations it reached
+        t_cg0 = time.perf_counter()
+        delta0 = svm.cg_begin(b, q, eps=1e-3)
+        it, conv = 0, False
+        while not conv and it < d and time.perf_counter() - t_cg0 < solve_cap_s:
+            it, conv = svm.cg_step(min(50 - it % 50, d - it))
+        t_cg = time.perf_counter() - t_cg0
+        _, tr, _ = svm.cg_result(min(it + 1, 4096))
+        learn = {"eps": 1e-3, "imax": d, "setup_s": round(t_setup, 3), "q_s": round(t_q, 4), "cg_iters": it,
+                 "cg_s": round(t_cg, 4), "learn_s": round(t_setup + t_q + t_cg, 3), "converged": bool(conv),
+                 "final_rel_residual": float(tr[-1] / delta0) if len(tr) else None,
+                 "cap_s": solve_cap_s}
+        log(f"[rank {rank}] {name}: learn at eps 1e-3: setup {t_setup:.2f}s + q {t_q:.3f}s + CG {it} iterations "
+            f"{t_cg:.3f}s (converged: {conv})")
     svm.close()
     roof = roofline(cfg, info, n, d, share, ms_dom, extra)
     dts = "f64" if dt == np.float64 else "f32"
@@ -154,9 +176,11 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
         roof["traffic_frac"] = roof["traffic_GBps"] * 1e9 / PEAKS["hbm"]
     if roof["bound"] == "mfma":
         roof["mfma_util"], roof["mfma_util_source"] = pmc_mfma(tkey, n, d, world, kern, dts)
-    cpu = None
+    cpu = cpu_fact = None
     if want_cpu and rank == 0 and world == 1 and not sim:
         cpu = cpu_baseline(kern, dt, d, n - 1, cpu_seconds, extra)
+        if layout != "dense" and kern == "linear":
+            cpu_fact = cpu_baseline_factored(dt, extra, cpu_seconds * 0.5)
     rec = {
         "value": steps / elapsed, "unit": "CG iterations/s", "ms_per_step": elapsed / steps * 1e3, "steps": steps,
         "warmup": warmup, "dtype": dts,
@@ -165,6 +189,10 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
                    "parallelism": collective_desc(world, sim, args.host_exchange), "setup_s": round(t_setup, 3)},
         "roofline": roof, "cpu_baseline": cpu, "kp_ms": ms_kp,
     }
+    if cpu_fact is not None:
+        rec["cpu_baseline_factored"] = cpu_fact
+    if learn is not None:
+        rec["learn"] = learn
     if info["is_sparse"]:
         rec["config"]["nnz"] = info["nnz"]
     if sim:
@@ -194,6 +222,8 @@ def main():
                     help="one GPU computes rank R's share of a W-GPU job (no collective): measures one rank of a "
                          "multi-GPU configuration that does not fit one GPU (e.g. configs[4])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--solve", action="store_true",
+                    help="also time the whole learn() at eps = 1e-3 (setup, q, CG to convergence): 'learn' record")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -223,12 +253,13 @@ def main():
         pm.CSVM = _csvm
 
     cache = {}
-    rec = run_config(args.config, args, rank, world, dist, uid, args.steps, args.warmup, not args.no_cpu,
-                     args.cpu_seconds, args.kp_reps, sim=sim, kernel=args.kernel, dtype=args.dtype,
-                     points=args.points, features=args.features, data_cache=cache)
-    extra = None
     default_run = (args.config == "dense_rbf_100k" and not (args.kernel or args.dtype or args.points or
                                                             args.features or sim) and world == 1)
+    rec = run_config(args.config, args, rank, world, dist, uid, args.steps, args.warmup, not args.no_cpu,
+                     args.cpu_seconds, args.kp_reps, sim=sim, kernel=args.kernel, dtype=args.dtype,
+                     points=args.points, features=args.features, data_cache=cache,
+                     solve=(args.solve or default_run) and world == 1)
+    extra = None
     if default_run and not args.no_extra:
         # north_star's sparse target measured under the same clock: configs[2] with RBF (the >= 70 % HBM
         # row), configs[2] itself (sparse linear, same seeded matrix) and configs[4] (2M x 100k FP22 RBF,
@@ -236,7 +267,7 @@ def main():
         extra = {}
         for name, steps in (("csr_rbf_1m", 50), ("csr_linear_1m", 200), ("fp22_rbf_2m", 30)):
             extra[name] = run_config(name, args, rank, world, dist, uid, steps, 2, not args.no_cpu,
-                                     args.cpu_seconds * 0.6, args.kp_reps, data_cache=cache)
+                                     args.cpu_seconds * 0.6, args.kp_reps, data_cache=cache, solve=True)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -256,6 +287,9 @@ def main():
             "cpu_baseline": rec["cpu_baseline"],
             "kp_ms": rec["kp_ms"],
         }
+        for k in ("cpu_baseline_factored", "learn"):
+            if k in rec:
+                out[k] = rec[k]
         if extra:
             out["extra"] = extra
         print(json.dumps(out), flush=True)
@@ -385,10 +419,44 @@ def cpu_baseline(kernel, dtype, d, m, budget_s, extra):
         t = run(n_s)
     ms = n_s - 1
     t_full = t * (m * (m + 1)) / (ms * (ms + 1))  # the reference kernel visits every lower-triangle pair
+    if "X" in extra:
+        what = "the oracle (reference OpenMP kernel restated, -O3 -ffast-math)"
+    else:
+        # the reference itself densifies sparse input (parameter.cpp:66-87) and evaluates every pair over
+        # all d features; its 32-bit indices cannot address configs 3 / 5 at all. The oracle's
+        # CSR twin visits the same pairs but merges the two CSR rows per pair (O(nnz/row), not O(d))
+        what = ("the oracle's CSR twin of the reference OpenMP kernel (every lower-triangle pair, CSR rows merged per "
+                "pair instead of the reference's densified O(d) rows; -O3 -ffast-math)")
     return {"value": 1.0 / t_full, "unit": "CG iterations/s", "cores": threads, "kind": "port",
-            "sample": f"one K·p of the oracle (reference OpenMP kernel restated, -O3 -ffast-math) on the first "
-                      f"{n_s} of {n_all} points ({t:.2f}s), scaled by the lower-triangle pair count to N={n_all}",
+            "sample": f"one K·p of {what} on the first {n_s} of {n_all} points ({t:.2f}s), scaled by the "
+                      f"lower-triangle pair count to N={n_all}",
             "pair_per_s": ms * (ms + 1) / 2 / t}
+
+
+def cpu_baseline_factored(dtype, extra, budget_s):
+    """The O(nnz) factored CPU K·p of sparse linear data at full size: w = X_m^T p,
+    then X_m w + the rank-1 terms, OpenMP on all host threads (oracle/oracle_tmpl.h orc_kp_csr_factored)."""
+    from oracle import pyoracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    rowptr, col, val, n, d = extra["csr"]
+    data = pyoracle.Data(rowptr=rowptr, col=col, val=val, n=n, d=d, dtype=dtype)
+    m = n - 1
+    q = np.ones(m, dtype=dtype)
+    pvec = np.ones(m, dtype=dtype)
+    ret = np.zeros(m, dtype=dtype)
+    pyoracle.kp_csr_factored(data, q, dtype(1.0), 1.0, 1.0, pvec, ret, nthreads=threads)  # warm-up (page-in)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        pyoracle.kp_csr_factored(data, q, dtype(1.0), 1.0, 1.0, pvec, ret, nthreads=threads)
+        reps += 1
+        t = time.perf_counter() - t0
+        if t >= budget_s or reps >= 200:
+            break
+    return {"value": reps / t, "unit": "CG iterations/s (K·p only)", "cores": threads, "kind": "port",
+            "sample": f"{reps} full-size K·p of the O(nnz) factored form X_m(X_m^T p) + rank-1 terms on the CSR data "
+                      f"({t:.2f}s, OpenMP, -O3 -ffast-math): the honest CPU cost of the sparse linear product, "
+                      f"which the reference (densifying, pairwise) does not implement"}
 
 
 if __name__ == "__main__":

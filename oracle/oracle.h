@@ -43,6 +43,9 @@ extern "C" {
     void orc_kp_csr_##SUF(int kernel, int degree, REAL gamma, REAL coef0, const int64_t *rowptr,                \
                           const int32_t *col, const REAL *val, int64_t n, int64_t d, const REAL *q,             \
                           REAL QA_cost, REAL cost_inv, REAL add, const REAL *p, REAL *ret, int nthreads);       \
+    void orc_kp_csr_factored_##SUF(const int64_t *rowptr, const int32_t *col, const REAL *val, int64_t n, int64_t d, \
+                                   const REAL *q, REAL QA_cost, REAL cost_inv, REAL add, const REAL *p, REAL *ret, \
+                                   int nthreads);                                                               \
     int64_t orc_cg_##SUF(int kernel, int degree, REAL gamma, REAL coef0, const REAL *X, const int64_t *rowptr,  \
                          const int32_t *col, int64_t n, int64_t d, const REAL *b, int64_t imax, REAL eps,       \
                          const REAL *q, REAL QA_cost, REAL cost_inv, REAL *x_out, double *delta_trace,          \

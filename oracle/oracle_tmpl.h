@@ -172,6 +172,48 @@ void FN(orc_kp_csr)(int kernel, int degree, REAL gamma, REAL coef0, const int64_
     FN(orc_kp_view)(&v, n - 1, q, QA_cost, cost_inv, add, p, ret, nthreads);
 }
 
+/* CPU baseline only ("cpu_ref CSR K·p at full size, O(nnz) factored form"):
+ * the linear K·p in the factored form SURVEY §8(d) verified against the reference kernel (8.7e-16),
+ *   ret += add * ( X_m (X_m^T p) + (QA_cost - q_i) sum(p) - q^T p + p_i / C ),
+ * on CSR rows 0..m-1, OpenMP: w = X_m^T p with per-thread column accumulators reduced in thread order,
+ * then one row-parallel pass. Not a restatement of a reference function (the reference has no sparse
+ * path); it is the honest O(nnz) CPU cost of the same product, timed beside the GPU. */
+void FN(orc_kp_csr_factored)(const int64_t *rowptr, const int32_t *col, const REAL *val, int64_t n, int64_t d,
+                             const REAL *q, REAL QA_cost, REAL cost_inv, REAL add, const REAL *p, REAL *ret,
+                             int nthreads) {
+    const int64_t m = n - 1;
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+    REAL *wt = (REAL *) calloc((size_t) nthreads * (size_t) d, sizeof(REAL));
+    REAL *w = (REAL *) calloc((size_t) d, sizeof(REAL));
+    REAL sp = 0, sqp = 0;
+#pragma omp parallel num_threads(nthreads)
+    {
+        REAL *mine = wt + (size_t) omp_get_thread_num() * (size_t) d;
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < m; ++i)
+            for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) mine[col[k]] += val[k] * p[i];
+#pragma omp for schedule(static)
+        for (int64_t f = 0; f < d; ++f) {
+            REAL a = 0;
+            for (int t = 0; t < nthreads; ++t) a += wt[(size_t) t * (size_t) d + f];
+            w[f] = a;
+        }
+#pragma omp for reduction(+ : sp, sqp) schedule(static)
+        for (int64_t i = 0; i < m; ++i) {
+            sp += p[i];
+            sqp += q[i] * p[i];
+        }
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < m; ++i) {
+            REAL raw = 0;
+            for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) raw += val[k] * w[col[k]];
+            ret[i] += add * (raw + (QA_cost - q[i]) * sp - sqp + cost_inv * p[i]);
+        }
+    }
+    free(wt);
+    free(w);
+}
+
 /* openmp::csvm::solver_CG (src/plssvm/backends/OpenMP/csvm.cpp:82-170), the normative CG:
  * x0 = 1; r = b - Q~x; delta = r.r; loop run < imax: Ad = Q~d; a = delta/(d.Ad); x += a*d;
  * r = (run % 50 == 49) ? b - Q~x : r - a*Ad; stop if delta <= eps^2 delta0; d = beta*d + r.

@@ -53,6 +53,8 @@ def _declare(L):
         f.argtypes = [_INT, _INT, R, R, _P, _P, _P, _I64, _I64, _P]
         f = getattr(L, f"orc_kp_csr_{suf}")
         f.argtypes = [_INT, _INT, R, R, _P, _P, _P, _I64, _I64, _P, R, R, R, _P, _P, _INT]
+        f = getattr(L, f"orc_kp_csr_factored_{suf}")
+        f.argtypes = [_P, _P, _P, _I64, _I64, _P, R, R, R, _P, _P, _INT]
         f = getattr(L, f"orc_cg_{suf}")
         f.argtypes = [_INT, _INT, R, R, _P, _P, _P, _I64, _I64, _P, _I64, R, _P, R, R, _P, _P, _INT]
         f.restype = _I64
@@ -134,6 +136,19 @@ def kp(kernel, data: Data, q, QA_cost, cost, add, p, ret=None, degree=3, gamma=1
     else:
         getattr(lib(fast), f"orc_kp_{s}")(KERNELS[kernel], degree, gamma, coef0, _ptr(data.X), data.n, data.d,
                                            _ptr(q), QA_cost, cost_inv, add, _ptr(p), _ptr(ret), nthreads)
+    return ret
+
+
+def kp_csr_factored(data: Data, q, QA_cost, cost, add, p, ret=None, nthreads=0, fast=True):
+    """CPU baseline only: the linear K·p of CSR data in the O(nnz) factored form."""
+    assert data.csr
+    dt = data.dtype
+    q = np.ascontiguousarray(q, dtype=dt)
+    p = np.ascontiguousarray(p, dtype=dt)
+    ret = np.zeros(data.n - 1, dtype=dt) if ret is None else ret
+    getattr(lib(fast), f"orc_kp_csr_factored_{_suf(dt)}")(_ptr(data.rowptr), _ptr(data.col), _ptr(data.X), data.n,
+                                                          data.d, _ptr(q), QA_cost, dt.type(1) / dt.type(cost), add,
+                                                          _ptr(p), _ptr(ret), nthreads)
     return ret
 
 

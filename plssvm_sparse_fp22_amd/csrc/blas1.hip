@@ -52,16 +52,23 @@ __global__ __launch_bounds__(256) void dot2_kernel(const T *__restrict__ a, cons
     }
 }
 
+// G > 1: a sharded group's gathered partials, G sets of 2 x RED_BLOCKS (rank-major); every thread adds its
+// partials' G values in rank order (the same order, hence the same bits, on every rank)
 template <typename T>
-__global__ __launch_bounds__(256) void dot_final_kernel(const T *__restrict__ partials, cg_scalars<T> *sc, int op,
-                                                        int64_t run, double *trace, int64_t trace_cap,
+__global__ __launch_bounds__(256) void dot_final_kernel(const T *__restrict__ partials, int G, cg_scalars<T> *sc,
+                                                        int op, int64_t run, double *trace, int64_t trace_cap,
                                                         T *plain_out) {
     if (op != FIN_PLAIN && sc->converged) return;
     __shared__ T red[8];
     T s1 = 0, s2 = 0;
     for (int i = threadIdx.x; i < RED_BLOCKS; i += blockDim.x) {
-        s1 += partials[i];
-        s2 += partials[RED_BLOCKS + i];
+        T a = partials[i], b = partials[RED_BLOCKS + i];
+        for (int g = 1; g < G; ++g) {
+            a += partials[g * 2 * RED_BLOCKS + i];
+            b += partials[g * 2 * RED_BLOCKS + RED_BLOCKS + i];
+        }
+        s1 += a;
+        s2 += b;
     }
     const T r1 = block_sum(s1, red);
     __syncthreads();
@@ -159,13 +166,19 @@ __device__ __forceinline__ T block_sum_all(T v, T *red, T *bc) {
     return out;
 }
 
-// the RED_BLOCKS partial pairs of a dot2_kernel-shaped producer, summed as dot_final_kernel does
+// the RED_BLOCKS partial pairs of a dot2_kernel-shaped producer (G gathered sets of a sharded group),
+// summed as dot_final_kernel does
 template <typename T>
-__device__ __forceinline__ void partials_total(const T *__restrict__ partials, T *red, T *bc, T &r1, T &r2) {
+__device__ __forceinline__ void partials_total(const T *__restrict__ partials, int G, T *red, T *bc, T &r1, T &r2) {
     T s1 = 0, s2 = 0;
     for (int i = threadIdx.x; i < RED_BLOCKS; i += blockDim.x) {
-        s1 += partials[i];
-        s2 += partials[RED_BLOCKS + i];
+        T a = partials[i], b = partials[RED_BLOCKS + i];
+        for (int g = 1; g < G; ++g) {
+            a += partials[g * 2 * RED_BLOCKS + i];
+            b += partials[g * 2 * RED_BLOCKS + RED_BLOCKS + i];
+        }
+        s1 += a;
+        s2 += b;
     }
     r1 = block_sum_all(s1, red, bc);
     r2 = block_sum_all(s2, red, bc);
@@ -192,8 +205,8 @@ constexpr int CG_PRE = 2;
 // ((q0 + q1) + q2) + q3 — so Ad is bitwise the reduced pass output the other K·p calls see
 template <typename T>
 __global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__ raw, const T *__restrict__ slabs,
-                                                         int64_t P, const T *__restrict__ q,
-                                                         const T *__restrict__ d, const T *__restrict__ psum,
+                                                         int64_t P, int64_t sstride, const T *__restrict__ q,
+                                                         const T *__restrict__ d, const T *__restrict__ psum, int G,
                                                          T QA_cost, T cost_inv, int raw_only, int64_t m,
                                                          T *__restrict__ Ad, T *__restrict__ pdad,
                                                          cg_scalars<T> *sc) {
@@ -204,7 +217,7 @@ __global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__
         if (slabs == nullptr) return raw[i];
         if (P < 16) {
             T rw = 0;
-            for (int64_t k = 0; k < P; ++k) rw += slabs[k * m + i];
+            for (int64_t k = 0; k < P; ++k) rw += slabs[k * sstride + i];
             return rw;
         }
         const int64_t per = (P + 3) / 4;
@@ -212,7 +225,7 @@ __global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             T a = 0;
-            for (int64_t k = u * per; k < min(P, (u + 1) * per); ++k) a += slabs[k * m + i];
+            for (int64_t k = u * per; k < min(P, (u + 1) * per); ++k) a += slabs[k * sstride + i];
             qs[u] = a;
         }
         return ((qs[0] + qs[1]) + qs[2]) + qs[3];
@@ -224,7 +237,7 @@ __global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__
         if (i < m) rw[e] = load_raw(i), qv[e] = q[i], dv[e] = d[i];
     }
     T sp, sqp;
-    partials_total(psum, red, bc, sp, sqp);
+    partials_total(psum, G, red, bc, sp, sqp);
     if (blockIdx.x == 0 && threadIdx.x == 0) sc->sp = sp, sc->sqp = sqp;
     T s1 = 0;
     auto one = [&](int64_t i, T r_, T q_, T d_) {
@@ -249,8 +262,8 @@ __global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__
 template <typename T>
 __global__ __launch_bounds__(CG_NT) void cg_upd_rr_kernel(T *__restrict__ x, T *__restrict__ r, const T *__restrict__ d,
                                                         const T *__restrict__ Ad, const T *__restrict__ b, int reset,
-                                                        const T *__restrict__ pdad, int64_t m, T *__restrict__ prr,
-                                                        cg_scalars<T> *sc) {
+                                                        const T *__restrict__ pdad, int G, int64_t m,
+                                                        T *__restrict__ prr, cg_scalars<T> *sc) {
     if (sc->converged) return;
     __shared__ T red[CG_NT / 64], bc[1];
     const int64_t i0 = (int64_t) blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t) gridDim.x * blockDim.x;
@@ -261,7 +274,7 @@ __global__ __launch_bounds__(CG_NT) void cg_upd_rr_kernel(T *__restrict__ x, T *
         if (i < m) xv[e] = x[i], dv[e] = d[i], av[e] = reset ? b[i] : Ad[i], rv[e] = reset ? T(0) : r[i];
     }
     T dAd, unused;
-    partials_total(pdad, red, bc, dAd, unused);
+    partials_total(pdad, G, red, bc, dAd, unused);
     const T delta = sc->delta;
     const T alpha = delta / dAd;
     if (blockIdx.x == 0 && threadIdx.x == 0) sc->dAd = dAd, sc->alpha = alpha, sc->delta_prev = delta;
@@ -289,8 +302,8 @@ __global__ __launch_bounds__(CG_NT) void cg_upd_rr_kernel(T *__restrict__ x, T *
 
 template <typename T>
 __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, const T *__restrict__ r,
-                                                          const T *__restrict__ q, const T *__restrict__ prr, int init,
-                                                          double *trace, int64_t trace_cap, int64_t m,
+                                                          const T *__restrict__ q, const T *__restrict__ prr, int G,
+                                                          int init, double *trace, int64_t trace_cap, int64_t m,
                                                           T *__restrict__ psum, cg_scalars<T> *sc) {
     if (sc->converged) return;
     __shared__ T red[CG_NT / 64], bc[1];
@@ -304,7 +317,7 @@ __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, c
     T beta = 0;
     if (!init) {
         T rr, unused;
-        partials_total(prr, red, bc, rr, unused);
+        partials_total(prr, G, red, bc, rr, unused);
         const bool conv = rr <= sc->eps2delta0;
         beta = rr / sc->delta_prev;
         if (blockIdx.x == 0 && threadIdx.x == 0) {  // FIN_DELTA of dot_final_kernel
@@ -343,24 +356,26 @@ __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, c
 }  // namespace
 
 template <typename T>
-void launch_cg_fin_dad(const T *raw, const T *slabs, int64_t P, const T *q, const T *d, const T *psum, T QA_cost,
-                       T cost_inv, int raw_only, int64_t m, T *Ad, T *pdad, cg_scalars<T> *sc, hipStream_t s) {
-    hipLaunchKernelGGL(cg_fin_dad_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, raw, slabs, P, q, d, psum, QA_cost,
-                       cost_inv, raw_only, m, Ad, pdad, sc);
+void launch_cg_fin_dad(const T *raw, const T *slabs, int64_t P, int64_t sstride, const T *q, const T *d, const T *psum,
+                       int G, T QA_cost, T cost_inv, int raw_only, int64_t m, T *Ad, T *pdad, cg_scalars<T> *sc,
+                       hipStream_t s) {
+    hipLaunchKernelGGL(cg_fin_dad_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, raw, slabs, P, sstride, q, d, psum, G,
+                       QA_cost, cost_inv, raw_only, m, Ad, pdad, sc);
     MI_LAUNCH_CHECK();
 }
 
 template <typename T>
-void launch_cg_upd_rr(T *x, T *r, const T *d, const T *Ad, const T *b, int reset, const T *pdad, int64_t m, T *prr,
-                      cg_scalars<T> *sc, hipStream_t s) {
-    hipLaunchKernelGGL(cg_upd_rr_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, x, r, d, Ad, b, reset, pdad, m, prr, sc);
+void launch_cg_upd_rr(T *x, T *r, const T *d, const T *Ad, const T *b, int reset, const T *pdad, int G, int64_t m,
+                      T *prr, cg_scalars<T> *sc, hipStream_t s) {
+    hipLaunchKernelGGL(cg_upd_rr_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, x, r, d, Ad, b, reset, pdad, G, m, prr,
+                       sc);
     MI_LAUNCH_CHECK();
 }
 
 template <typename T>
-void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int init, double *trace,
+void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int G, int init, double *trace,
                         int64_t trace_cap, int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s) {
-    hipLaunchKernelGGL(cg_dir_sums_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, d, r, q, prr, init, trace,
+    hipLaunchKernelGGL(cg_dir_sums_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, d, r, q, prr, G, init, trace,
                        trace_cap, m, psum, sc);
     MI_LAUNCH_CHECK();
 }
@@ -374,8 +389,8 @@ void launch_dot2(const T *a, const T *b, const T *c, const T *e, int64_t n, T *p
 
 template <typename T>
 void launch_dot_final(const T *partials, cg_scalars<T> *sc, int op, int64_t run, double *trace, int64_t trace_cap,
-                      T *plain_out, hipStream_t s) {
-    hipLaunchKernelGGL(dot_final_kernel<T>, dim3(1), dim3(256), 0, s, partials, sc, op, run, trace, trace_cap,
+                      T *plain_out, hipStream_t s, int G) {
+    hipLaunchKernelGGL(dot_final_kernel<T>, dim3(1), dim3(256), 0, s, partials, G, sc, op, run, trace, trace_cap,
                        plain_out);
     MI_LAUNCH_CHECK();
 }
@@ -414,17 +429,17 @@ void launch_cg_direction(T *d, const T *r, int64_t m, const cg_scalars<T> *sc, h
     template void launch_dot2<T>(const T *, const T *, const T *, const T *, int64_t, T *, const cg_scalars<T> *, \
                                  hipStream_t);                                                                    \
     template void launch_dot_final<T>(const T *, cg_scalars<T> *, int, int64_t, double *, int64_t, T *,           \
-                                      hipStream_t);                                                               \
+                                      hipStream_t, int);                                                          \
     template void launch_cg_init<T>(const T *, int64_t, T *, T *, hipStream_t);                                   \
     template void launch_copy<T>(const T *, int64_t, T *, const cg_scalars<T> *, hipStream_t);                    \
     template void launch_cg_update<T>(T *, T *, const T *, const T *, const T *, int, int64_t,                    \
                                       const cg_scalars<T> *, hipStream_t);                                        \
     template void launch_cg_direction<T>(T *, const T *, int64_t, const cg_scalars<T> *, hipStream_t);             \
-    template void launch_cg_fin_dad<T>(const T *, const T *, int64_t, const T *, const T *, const T *, T, T, int,  \
-                                       int64_t, T *, T *, cg_scalars<T> *, hipStream_t);                                               \
-    template void launch_cg_upd_rr<T>(T *, T *, const T *, const T *, const T *, int, const T *, int64_t, T *,      \
+    template void launch_cg_fin_dad<T>(const T *, const T *, int64_t, int64_t, const T *, const T *, const T *,    \
+                                       int, T, T, int, int64_t, T *, T *, cg_scalars<T> *, hipStream_t);           \
+    template void launch_cg_upd_rr<T>(T *, T *, const T *, const T *, const T *, int, const T *, int, int64_t, T *, \
                                       cg_scalars<T> *, hipStream_t);                                                \
-    template void launch_cg_dir_sums<T>(T *, const T *, const T *, const T *, int, double *, int64_t, int64_t,      \
+    template void launch_cg_dir_sums<T>(T *, const T *, const T *, const T *, int, int, double *, int64_t, int64_t, \
                                         T *, cg_scalars<T> *, hipStream_t);
 INST(float)
 INST(double)

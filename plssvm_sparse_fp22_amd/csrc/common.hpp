@@ -3,8 +3,12 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
+#include <exception>
+#include <thread>
+#include <vector>
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
@@ -43,6 +47,42 @@ struct phase_timer {
         t = now;
     }
 };
+
+// host worker threads for setup-time loops: OMP_NUM_THREADS when set (the GPU box sets it to its CPU
+// share), else the hardware threads, at most 64
+inline int host_threads() {
+    static const int n = [] {
+        int v = 0;
+        if (const char *e = std::getenv("OMP_NUM_THREADS")) v = std::atoi(e);
+        if (v <= 0) v = (int) std::thread::hardware_concurrency();
+        return v < 1 ? 1 : (v > 64 ? 64 : v);
+    }();
+    return n;
+}
+
+// f(t, begin, end) on host_threads() threads over contiguous parts of [0, n) (part t = [t n / T, (t+1) n / T)),
+// joined before returning; the first exception is rethrown
+template <typename F>
+void host_parallel(int64_t n, F f, int nthreads = 0) {
+    const int T = (int) std::max<int64_t>(1, std::min<int64_t>(nthreads > 0 ? nthreads : host_threads(), std::max<int64_t>(n, 1)));
+    if (T == 1) {
+        f(0, (int64_t) 0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err((size_t) T);
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            try {
+                f(t, n * t / T, n * (t + 1) / T);
+            } catch (...) {
+                err[(size_t) t] = std::current_exception();
+            }
+        });
+    for (auto &x : th) x.join();
+    for (auto &e : err)
+        if (e) std::rethrow_exception(e);
+}
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }

@@ -189,6 +189,41 @@ void engine<T>::allreduce(T *buf, int64_t count) {
     }
 }
 
+// sharded CG: the 2 x RED_BLOCKS partials of every rank (rank-major, into slot `slot` of cgp_g); the
+// consumers sum them in rank order. Unsharded or a single rank: the local partials.
+template <typename T>
+const T *engine<T>::gather_partials(T *local, int slot) {
+    if (G <= 1) return local;
+    const int64_t K = 2 * RED_BLOCKS;
+    T *out = cgp_g.get() + (int64_t) slot * G * K;
+    if (comm != nullptr) {
+        MI_NCCL_CHECK(ncclAllGather(local, out, (size_t) K, nccl_type<T>(), comm, stream));
+    } else {
+        xpart.resize((size_t) (G * K));
+        MI_HIP_CHECK(hipMemcpyAsync(xpart.data() + rank * K, local, sizeof(T) * (size_t) K, hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        if (xchg(xpart.data(), K, (int) sizeof(T), 1, xchg_user) != 0) throw mi_error(-3, "host exchange failed");
+        MI_HIP_CHECK(hipMemcpyAsync(out, xpart.data(), sizeof(T) * xpart.size(), hipMemcpyHostToDevice, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+    return out;
+}
+
+template <typename T>
+void engine<T>::gather_input(const T *p) {
+    if (shard && in_group()) allgather_rows(const_cast<T *>(p));
+}
+
+template <typename T>
+void engine<T>::reduce_scatter_rows(T *buf) {
+    if (comm != nullptr) {
+        MI_NCCL_CHECK(ncclReduceScatter(buf, buf + (int64_t) rank * chunk, (size_t) chunk, nccl_type<T>(), ncclSum, comm,
+                                        stream));
+    } else if (xchg != nullptr) {
+        allreduce(buf, chunk * world);  // the host transport sums everything; the own rows are used
+    }
+}
+
 template <typename T>
 void engine<T>::allgather_rows(T *buf) {
     if (comm != nullptr) {
@@ -268,12 +303,22 @@ void engine<T>::finish_setup() {
     r0 = std::min<int64_t>(m, eff_rank * chunk);
     r1 = std::min<int64_t>(m, r0 + chunk);
     const int64_t vec_len = std::max<int64_t>(n_pad, chunk * eff_world);
+    {
+        const char *se = std::getenv("PLSSVM_MI_SHARD");
+        const int opt = se != nullptr ? std::atoi(se) : -1;
+        shard = (in_group() && (opt == 1 || (opt < 0 && sparse))) || (sim_world > 0 && opt == 1);
+        v0 = shard ? r0 : 0;
+        vn = shard ? r1 - r0 : m;
+        G = (shard && in_group()) ? world : 1;
+        if (G > 1) cgp_g.alloc(4 * (int64_t) G * 2 * RED_BLOCKS, stream);
+    }
+    tiles_upload();
     if (!sparse && !factored()) {
-        partial.alloc(std::max<int64_t>(nb, 1) * n_pad, stream, false);
+        // the rank's tile slab: one record of row and column sums per own tile (scales with 1 / world)
+        partial.alloc(std::max<int64_t>(kp_wgs, 1) * KP_REC, stream, false);
     } else {
         partial.reset();
     }
-    tiles_upload();
     q.alloc(vec_len, stream);
     pv.alloc(vec_len, stream);
     ret.alloc(vec_len, stream);
@@ -338,12 +383,14 @@ template <typename T>
 void engine<T>::kp_device(const T *p, T *out, T add, bool overwrite, const cg_scalars<T> *status) {
     if (m <= 0) return;
     cg_scalars<T> *scp = sc.get();
-    // sum(p) and sum(q p): the rank-1 parts of Q~ (QA_cost - q_i - q_j) never enter the tiles
-    launch_dot2<T>(p, nullptr, q.get(), p, m, red.get(), status, stream);
-    launch_dot_final<T>(red.get(), scp, FIN_SP_SQP, 0, nullptr, 0, nullptr, stream);
+    // sum(p) and sum(q p): the rank-1 parts of Q~ (QA_cost - q_i - q_j) never enter the tiles (sharded: this
+    // rank's rows, then the gathered partials of all ranks)
+    launch_dot2<T>(p + v0, nullptr, q.get() + v0, p + v0, vn, red.get(), status, stream);
+    launch_dot_final<T>(gather_partials(red.get(), 3), scp, FIN_SP_SQP, 0, nullptr, 0, nullptr, stream, G);
     kp_raw(p, status);
-    const int flags = (overwrite ? 1 : 0) | ((sim_world > 0 && sim_rank != 0) ? 2 : 0);
-    launch_kp_finalize<T>(raw.get(), q.get(), p, scp, QA_cost, cost_inv(), add, flags, m, out, status, stream);
+    const int flags = (overwrite ? 1 : 0) | ((sim_world > 0 && sim_rank != 0 && !shard) ? 2 : 0);
+    launch_kp_finalize<T>(raw.get() + v0, q.get() + v0, p + v0, scp, QA_cost, cost_inv(), add, flags, vn, out + v0,
+                          status, stream);
 }
 
 template <typename T>
@@ -352,15 +399,18 @@ void engine<T>::kp_raw(const T *p, const cg_scalars<T> *status) {
     if (sparse_stored()) {
         sparse_kp_raw(p, status);
     } else if (factored()) {
-        launch_gemv_t<T>(XT.get(), n_pad, d, sim_world > 0 ? 0 : r0, sim_world > 0 ? m : r1, p, w.get(), status, stream);
+        const bool all_rows = sim_world > 0 && !shard;
+        launch_gemv_t<T>(XT.get(), n_pad, d, all_rows ? 0 : r0, all_rows ? m : r1, p, w.get(), status, stream);
         allreduce(w.get(), d);
         launch_gemv_n<T>(XT.get(), n_pad, d, r0, r1, w.get(), raw.get(), status, stream);
-        allgather_rows(raw.get());
+        if (!shard) allgather_rows(raw.get());
     } else {
+        gather_input(p);
         launch_kp_tiles<T>(kf(), XT.get(), norms.get(), p, partial.get(), n_pad, d_pad, nb, t0, t1 - t0, kp_wgoff.get(), kp_wgs, status,
                            stream);
-        launch_kp_reduce<T>(partial.get(), nb, n_pad, m, t0, t1, raw.get(), status, stream);
-        allreduce(raw.get(), m);
+        launch_kp_reduce<T>(partial.get(), nb, m, t0, t1, kp_wgoff.get(), raw.get(), status, stream);
+        if (shard) reduce_scatter_rows(raw.get());
+        else allreduce(raw.get(), m);
     }
 }
 
@@ -375,6 +425,7 @@ void engine<T>::kp_host(const T *q_host, const T *p, T *ret_host, T add) {
         MI_HIP_CHECK(hipMemcpyAsync(pv.get(), p, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
         MI_HIP_CHECK(hipMemcpyAsync(ret.get(), ret_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
         kp_device(pv.get(), ret.get(), add, false, nullptr);
+        if (shard && in_group()) allgather_rows(ret.get());  // device_reduction's result on every rank
         MI_HIP_CHECK(hipMemcpyAsync(ret_host, ret.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
@@ -395,6 +446,7 @@ void engine<T>::kp_part(const T *p_host, T *out_host, int part) {
         MI_HIP_CHECK(hipMemcpyAsync(pv.get(), p_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
         if (part == 1) sparse_kp_raw(pv.get(), nullptr, false);
         else kp_raw(pv.get(), nullptr);
+        if (shard && in_group()) allgather_rows(raw.get());
         MI_HIP_CHECK(hipMemcpyAsync(out_host, raw.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
@@ -417,11 +469,13 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
     // x = 1; r = b; r -= Q~x   (csvm.cpp:85-90)
     launch_cg_init<T>(b.get(), m, x.get(), r.get(), stream);
     kp_device(x.get(), r.get(), T(-1), false, nullptr);
-    // delta = r.r ; delta0 ; d = r   (:92-97)
-    launch_dot2<T>(r.get(), r.get(), nullptr, nullptr, m, red.get(), nullptr, stream);
-    launch_dot_final<T>(red.get(), sc.get(), FIN_DELTA0, 0, trace.get(), trace_cap, nullptr, stream);
+    // delta = r.r ; delta0 ; d = r   (:92-97)   (sharded: this rank's rows, the ranks' partials gathered)
+    launch_dot2<T>(r.get() + v0, r.get() + v0, nullptr, nullptr, vn, red.get(), nullptr, stream);
+    launch_dot_final<T>(gather_partials(red.get(), 3), sc.get(), FIN_DELTA0, 0, trace.get(), trace_cap, nullptr, stream, G);
     // d = r, with sum d / sum q d for the first Q~d
-    launch_cg_dir_sums<T>(dv.get(), r.get(), q.get(), nullptr, 1, nullptr, 0, m, cgp.get(), sc.get(), stream);
+    launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, q.get() + v0, nullptr, 1, 1, nullptr, 0, vn, cgp.get(), sc.get(),
+                          stream);
+    gather_partials(cgp.get(), 0);
     run = 0;
     cg_active = true;
     // a solve that can reach a whole block captures it now (capture launches nothing; the
@@ -440,7 +494,9 @@ template <typename T>
 void engine<T>::cg_iter(int reset) {
     const cg_scalars<T> *st = sc.get();
     T *psum = cgp.get(), *pdad = psum + 2 * RED_BLOCKS, *prr = psum + 4 * RED_BLOCKS;
-    const int raw_only = (sim_world > 0 && sim_rank != 0) ? 1 : 0;
+    // sharded: the partials the previous step gathered (slot 0: sum d / sum q d)
+    const T *psum_in = G > 1 ? cgp_g.get() : psum;
+    const int raw_only = (sim_world > 0 && sim_rank != 0 && !shard) ? 1 : 0;
     // Ad = Q~ d (:111-113); alpha = delta / (d . Ad) (:116) in the next kernel
     const T *slabs = nullptr;
     int64_t P = 0;
@@ -460,16 +516,19 @@ void engine<T>::cg_iter(int reset) {
         kp_raw(dv.get(), st);
     }
     if (!(sparse_stored() && factored() && world == 1 && sim_world == 0 && csr.rb_csr.nblk > 0))
-        launch_cg_fin_dad<T>(raw.get(), slabs, P, q.get(), dv.get(), psum, QA_cost, cost_inv(), raw_only, m, Ad.get(),
-                             pdad, sc.get(), stream);
+        launch_cg_fin_dad<T>(raw.get() + v0, slabs, P, m, q.get() + v0, dv.get() + v0, psum_in, G, QA_cost, cost_inv(),
+                             raw_only, vn, Ad.get() + v0, pdad, sc.get(), stream);
     // x += alpha d; r = b - Q~x every 50th iteration, else r -= alpha Ad   (:119-132)
-    launch_cg_upd_rr<T>(x.get(), r.get(), dv.get(), Ad.get(), b.get(), reset, pdad, m, prr, sc.get(), stream);
+    launch_cg_upd_rr<T>(x.get() + v0, r.get() + v0, dv.get() + v0, Ad.get() + v0, b.get() + v0, reset,
+                        gather_partials(pdad, 1), G, vn, prr, sc.get(), stream);
     if (reset) {
         kp_device(x.get(), r.get(), T(-1), false, st);
-        launch_dot2<T>(r.get(), r.get(), nullptr, nullptr, m, prr, st, stream);
+        launch_dot2<T>(r.get() + v0, r.get() + v0, nullptr, nullptr, vn, prr, st, stream);
     }
     // delta = r.r ; stop test ; beta (:135-146); d = beta d + r (:149-151), with sum d / sum q d
-    launch_cg_dir_sums<T>(dv.get(), r.get(), q.get(), prr, 0, trace.get(), trace_cap, m, psum, sc.get(), stream);
+    launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, q.get() + v0, gather_partials(prr, 2), G, 0, trace.get(), trace_cap,
+                          vn, psum, sc.get(), stream);
+    gather_partials(psum, 0);
 }
 
 // Iteration blocks of CG_RESET (the reset period) starting at a multiple of it are replayed from one
@@ -550,8 +609,10 @@ void engine<T>::cg_result(T *x_out, double *trace_out, int64_t trace_len, int64_
     MI_HIP_CHECK(hipSetDevice(device));
     cg_scalars<T> h{};
     MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));
-    if (x_out && m > 0)
+    if (x_out && m > 0) {
+        if (shard && in_group()) allgather_rows(x.get());  // every rank's rows of the solution
         MI_HIP_CHECK(hipMemcpyAsync(x_out, x.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
+    }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
     const int64_t it = h.iters;
     if (iters) *iters = it;

@@ -59,6 +59,19 @@ struct engine : engine_base {
     void tiles_upload();
     int64_t r0 = 0, r1 = 0, chunk = 0;    // rows owned by this rank (factored / sparse row paths)
 
+    // sharded CG (a real group on sparse data by default; PLSSVM_MI_SHARD = 0 / 1 overrides, 1 also for dense
+    // data and simulated ranks): each rank updates only its rows [v0, v0 + vn) of x, r, d, Ad; every dot is
+    // summed from the G ranks' gathered partials in rank order (the same bits everywhere); a K·p input the
+    // path needs whole is gathered first, a path's full-length partial result reduce-scattered
+    bool shard = false;
+    int64_t v0 = 0, vn = 0;
+    int G = 1;
+    dev_buf<T> cgp_g;      // gathered partials, slots [4][G][2 RED_BLOCKS]: sum d / sum q d, d.Ad, r.r, kp sums
+    std::vector<T> xpart;  // host staging of the host exchange's partial gathers
+    const T *gather_partials(T *local, int slot);
+    void gather_input(const T *p);   // sharded group: p's rows of every rank, in place
+    void reduce_scatter_rows(T *buf);  // sharded group: own rows of the sum over ranks
+
     // ---- vectors (n_pad, zero padded) ----
     dev_buf<T> partial, q, pv, ret, x, r, dv, Ad, b, raw, w, red;
     dev_buf<T> cgp;  // fused CG partials: [0, 2R) sum d / sum q d, [2R, 4R) d.Ad, [4R, 6R) r.r

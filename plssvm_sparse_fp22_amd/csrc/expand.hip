@@ -226,6 +226,218 @@ __global__ __launch_bounds__(256) void exp_iota_kernel(uint32_t *__restrict__ v,
     if (t < n) v[t] = (uint32_t) t;
 }
 
+// ---- row join: the remainder's symmetric rows built per row (default; PLSSVM_MI_EXP_JOIN=sort keeps the
+// column-join sort below) ------------------------------------------------------------------------------
+constexpr int RJ_NT = 1024;
+constexpr int RJ_BMW = 32768;  // bitmap words: 1 048 576 partner rows per pass (128 KiB of LDS)
+constexpr int RJ_LCAP = 2048;  // repeat sightings held per pass (more: the pass range is halved)
+constexpr int RJ_ECAP = 256;   // entries of row i held in LDS (longer rows: the sort join)
+constexpr int RJ_WPT = RJ_BMW / RJ_NT;
+
+// Rows [r0, r0 + gridDim.x) of the rank, one workgroup per row i: its partners j != i sharing two or more
+// features, ascending, in both triangles. Per pass over a range of partner rows, the column entries of
+// row i's features (the incidences, read coalesced from the CSC) mark an LDS bitmap; a second sighting of
+// a row appends it to a list, the list becomes a set in the bitmap and is enumerated in ascending order
+// (a block scan of per-thread popcounts). Count mode (sj == nullptr): cnt[r] = #partners. Write mode:
+// partner k of row r at sj[off8[r] + k], pads up to off8[r + 1] marked -1 (exp_rowjoin_h_kernel then
+// forms H). Both modes take the same passes (the halving decisions depend on the data only): deterministic.
+__global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__restrict__ rowptr,
+                                                            const int32_t *__restrict__ col,
+                                                            const int64_t *__restrict__ colptr,
+                                                            const int32_t *__restrict__ crow, int64_t m, int64_t r0,
+                                                            int64_t *__restrict__ cnt, const int64_t *__restrict__ off8,
+                                                            int32_t *__restrict__ sj) {
+    __shared__ uint32_t bm[RJ_BMW];
+    __shared__ int32_t rep[RJ_LCAP];
+    __shared__ int32_t zcol[RJ_ECAP];
+    __shared__ int32_t zoff[RJ_ECAP + 1];
+    __shared__ int64_t cst[RJ_ECAP];
+    __shared__ int32_t wtot[RJ_NT / 64];
+    __shared__ int nrep_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t r = blockIdx.x, i = r0 + r;
+    const int64_t e0 = rowptr[i];
+    const int ne = (int) (rowptr[i + 1] - e0);  // <= RJ_ECAP (host-checked)
+    for (int e = tid; e < ne; e += RJ_NT) {
+        const int32_t f = col[e0 + e];
+        zcol[e] = f;
+        cst[e] = colptr[f];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int32_t a = 0;
+        for (int e = 0; e < ne; ++e) {
+            zoff[e] = a;
+            a += (int32_t) (colptr[zcol[e] + 1] - cst[e]);
+        }
+        zoff[ne] = a;
+    }
+    __syncthreads();
+    const int32_t inc = zoff[ne];
+    const bool wr = sj != nullptr;
+    int64_t written = 0;
+    int64_t span = (int64_t) RJ_BMW * 32;
+    for (int64_t R0 = 0; R0 < m;) {
+        const int64_t R1 = min(m, R0 + span);
+        for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
+        if (tid == 0) nrep_s = 0;
+        __syncthreads();
+        int e = 0;
+        for (int32_t t = tid; t < inc; t += RJ_NT) {
+            while (zoff[e + 1] <= t) ++e;
+            const int64_t j = crow[cst[e] + (t - zoff[e])];
+            if (j == i || j < R0 || j >= R1) continue;
+            const uint32_t bit = 1u << ((j - R0) & 31);
+            const uint32_t old = atomicOr(&bm[(j - R0) >> 5], bit);
+            if (old & bit) {
+                const int q = atomicAdd(&nrep_s, 1);
+                if (q < RJ_LCAP) rep[q] = (int32_t) j;
+            }
+        }
+        __syncthreads();
+        const int nr = nrep_s;
+        if (nr > RJ_LCAP) {  // uniform: this range again in halves
+            span = (span + 1) / 2;
+            __syncthreads();
+            continue;
+        }
+        for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
+        __syncthreads();
+        for (int q = tid; q < nr; q += RJ_NT) {
+            const int64_t j = rep[q] - R0;
+            atomicOr(&bm[j >> 5], 1u << (j & 31));
+        }
+        __syncthreads();
+        int c = 0;
+#pragma unroll 8
+        for (int w = 0; w < RJ_WPT; ++w) c += __popc(bm[tid * RJ_WPT + w]);
+        // exclusive block scan of c (wave scans + wave totals)
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wtot[wave] = incl;
+        __syncthreads();
+        int before = 0, U = 0;
+        for (int w = 0; w < RJ_NT / 64; ++w) {
+            const int v = wtot[w];
+            if (w < wave) before += v;
+            U += v;
+        }
+        if (wr) {
+            int pos = before + incl - c;
+            for (int w = 0; w < RJ_WPT; ++w) {
+                uint32_t word = bm[tid * RJ_WPT + w];
+                while (word) {
+                    const int b = __ffs(word) - 1;
+                    word &= word - 1;
+                    rep[pos++] = (int32_t) (R0 + (int64_t) (tid * RJ_WPT + w) * 32 + b);
+                }
+            }
+            __syncthreads();
+            const int64_t base = off8[r] + written;
+            for (int q = tid; q < U; q += RJ_NT) sj[base + q] = rep[q];
+        }
+        written += U;
+        __syncthreads();  // bm / rep are reused by the next pass
+        R0 = R1;
+    }
+    if (!wr) {
+        if (tid == 0) cnt[r] = written;
+        return;
+    }
+    const int64_t b0 = off8[r], b1 = off8[r + 1];
+    for (int64_t k = b0 + written + tid; k < b1; k += RJ_NT) sj[k] = -1;  // pads (exp_rowjoin_h_kernel)
+}
+
+// H of the row join's partners (sj from exp_rowjoin_kernel's write pass): one 256-thread workgroup per row
+// i (row i in LDS), one partner per wave at a time: the lanes take row j's entries (coalesced, 64 per step),
+// look each up in row i (binary search), and the matches — ascending features — are summed in that order
+// from a ballot: H_ij = phi(s_ij) - sum_f phi(x_if x_jf) in fp64, rounded to T (the sequential sum of the
+// sort join). The next partner's row bounds are loaded one step ahead. Pads (sj < 0): j = i, H = 0.
+// lower_nz += #(j < i, H != 0 in T).
+constexpr int RJH_NT = 256;
+template <typename T>
+__global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__restrict__ rowptr,
+                                                               const int32_t *__restrict__ col,
+                                                               const T *__restrict__ val, int64_t r0, phi_fn phi,
+                                                               const int64_t *__restrict__ off8, int32_t *__restrict__ sj,
+                                                               T *__restrict__ sv,
+                                                               unsigned long long *__restrict__ lower_nz) {
+    __shared__ int32_t zcol[RJ_ECAP];
+    __shared__ T zval[RJ_ECAP];
+    __shared__ unsigned long long lnz_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t r = blockIdx.x, i = r0 + r;
+    const int64_t e0 = rowptr[i];
+    const int ne = (int) (rowptr[i + 1] - e0);
+    for (int e = tid; e < ne; e += RJH_NT) zcol[e] = col[e0 + e], zval[e] = val[e0 + e];
+    if (tid == 0) lnz_s = 0ull;
+    __syncthreads();
+    unsigned long long lnz = 0ull;
+    const int64_t q0 = off8[r], q1 = off8[r + 1];
+    constexpr int NW = RJH_NT / 64;
+    int64_t q = q0 + wave;
+    int64_t jn = q < q1 ? sj[q] : -1, kbn = 0, ken = 0;
+    if (jn >= 0) kbn = rowptr[jn], ken = rowptr[jn + 1];
+    for (; q < q1; q += NW) {
+        const int64_t j = jn, kb = kbn, ke = ken;
+        const int64_t qn = q + NW;  // the next partner of this wave, one step ahead
+        jn = qn < q1 ? sj[qn] : -1;
+        if (jn >= 0) kbn = rowptr[jn], ken = rowptr[jn + 1];
+        if (j < 0) {  // pad
+            if (lane == 0) {
+                sj[q] = (int32_t) i;
+                sv[q] = T(0);
+            }
+            continue;
+        }
+        double sd = 0.0, sphi = 0.0;
+        for (int64_t k0 = kb; k0 < ke; k0 += 64) {
+            const int64_t k = k0 + lane;
+            double a = 0.0, pa = 0.0;
+            bool hit = false;
+            if (k < ke && ne > 0) {
+                const int32_t f = col[k];
+                int lo = 0, hi = ne - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (zcol[mid] < f) lo = mid + 1;
+                    else hi = mid;
+                }
+                if (zcol[lo] == f) {
+                    a = (double) zval[lo] * (double) val[k];
+                    pa = phi(a);
+                    hit = true;
+                }
+            }
+            uint64_t mask = __ballot(hit);
+            while (mask) {  // wave-uniform: the shared features in ascending order
+                const int b = __ffsll((long long) mask) - 1;
+                mask &= mask - 1;
+                sd += __shfl(a, b);
+                sphi += __shfl(pa, b);
+            }
+        }
+        const T h = (T) (phi(sd) - sphi);
+        if (lane == 0) {
+            sv[q] = h;
+            if (j < i && h != T(0)) ++lnz;
+        }
+    }
+    if (lane == 0 && lnz) atomicAdd(&lnz_s, lnz);
+    __syncthreads();
+    if (tid == 0 && lnz_s) atomicAdd(lower_nz, lnz_s);
+}
+
+__global__ __launch_bounds__(256) void exp_pad8_cnt_kernel(const int64_t *__restrict__ cnt, int64_t R,
+                                                           int64_t *__restrict__ cnt8) {
+    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < R) cnt8[r] = (cnt[r] + 7) & ~int64_t(7);
+}
+
 // ---- per K·p ------------------------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void exp_w_kernel(const T *__restrict__ e, const T *__restrict__ p, int64_t m,
@@ -724,11 +936,11 @@ template <typename T>
 __global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ e, const T *__restrict__ w,
                                                           const T *__restrict__ hdiag, const T *__restrict__ phin,
                                                           const T *__restrict__ hs, const T *__restrict__ ssc, T kappa,
-                                                          int64_t m, int64_t r0, int64_t r1, int overlap_only,
+                                                          int64_t ib, int64_t ie, int64_t r0, int64_t r1, int overlap_only,
                                                           T *__restrict__ raw, const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
-    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
+    const int64_t i = ib + (int64_t) blockIdx.x * blockDim.x + threadIdx.x;  // rows [ib, ie)
+    if (i >= ie) return;
     if (i < r0 || i >= r1) {
         raw[i] = T(0);
         return;
@@ -801,8 +1013,10 @@ bool engine<T>::expansion_eligible() {
     return true;
 }
 
-// Setup: the remainder H of the pairs sharing >= 2 features, from the column join (sort +
-// reduce-by-key of (a, phi(a)) per pair), as symmetric rows [r0, r1); H_ii; the moment buffers.
+// Setup: the remainder H of the pairs sharing >= 2 features as symmetric rows [r0, r1) — by the row join
+// (exp_rowjoin_kernel: per row, an LDS bitmap of the rows met in its features' columns; count pass, scan,
+// write pass with H from a merge of the two rows), or by the column-join sort (every incidence (i, j < i,
+// a, phi(a)) generated, radix-sorted and reduced by key; PLSSVM_MI_EXP_JOIN=sort); H_ii; the moment buffers.
 template <typename T>
 void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
     auto &ex = csr.ex;
@@ -820,254 +1034,314 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
                            csr.val.get(), m, phi, ex.hdiag.get(), ex.phin.get());
     MI_LAUNCH_CHECK();
 
-    // ---- incidences per row (host) -> row sub-blocks of at most CAP incidences ----
-    std::vector<int64_t> inc(std::max<int64_t>(m, 1), 0);
-    {
-        dev_buf<int64_t> cnt;
-        cnt.alloc(std::max<int64_t>(m, 1), stream);
-        if (m > 0)
-            hipLaunchKernelGGL(exp_count_kernel, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream,
-                               csr.rowptr.get(), csr.col.get(), cpos, csr.colptr.get(), (int64_t) 0, m, cnt.get());
-        MI_LAUNCH_CHECK();
-        if (m > 0)
-            MI_HIP_CHECK(hipMemcpyAsync(inc.data(), cnt.get(), sizeof(int64_t) * (size_t) m, hipMemcpyDeviceToHost,
-                                        stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-    }
-    // incidences per sub-block (≈ 80 B each in flight); PLSSVM_MI_EXP_CAPLOG = log2 (measurements)
-    const int64_t CAP = int64_t(1) << [] {
-        const char *e = std::getenv("PLSSVM_MI_EXP_CAPLOG");
-        const int v = e ? std::atoi(e) : 0;
-        return v >= 20 && v <= 31 ? v : 27;
-    }();
-    constexpr int64_t ROWS_MAX = 65536;            // rows per sub-block (one workgroup per row)
-    std::vector<std::pair<int64_t, int64_t>> blocks;
-    {
-        int64_t a = r0, acc = 0;  // pairs (i, j < i) touch rows [r0, r1) only if i >= r0
-        for (int64_t i = r0; i < m; ++i) {
-            if (inc[i] > CAP) throw mi_error(-4, "a data point shares features with more than 2^27 others (dense row)");
-            if (i > a && (acc + inc[i] > CAP || i - a >= ROWS_MAX)) {
-                blocks.emplace_back(a, i);
-                a = i;
-                acc = 0;
-            }
-            acc += inc[i];
-        }
-        if (a < m) blocks.emplace_back(a, m);
-    }
-    int64_t max_blk = 1;
-    for (auto &b : blocks) {
-        int64_t s = 0;
-        for (int64_t i = b.first; i < b.second; ++i) s += inc[i];
-        max_blk = std::max(max_blk, s);
-    }
-
-    // ---- temporaries ----
-    dev_buf<uint64_t> keys, keys_s;
-    dev_buf<double2> vals, vals_s;
-    dev_buf<hpair> hp, hsel;
-    dev_buf<int64_t> cntb, off, nruns, nsel;
-    keys.alloc(max_blk, stream, false);
-    keys_s.alloc(max_blk, stream, false);
-    vals.alloc(max_blk, stream, false);
-    vals_s.alloc(max_blk, stream, false);
-    cntb.alloc(ROWS_MAX + 1, stream);
-    off.alloc(ROWS_MAX + 1, stream);
-    nruns.alloc(1, stream);
-    nsel.alloc(1, stream);
-    size_t tmp_sort = 0, tmp_scan = 0, tmp_red = 0, tmp_sel = 0;
-    const int nmax = (int) max_blk;
-    MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, keys.get(), keys_s.get(), vals.get(),
-                                                    vals_s.get(), nmax, 0, 64, stream));
-    MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_scan, cntb.get(), off.get(), (int) (ROWS_MAX + 1), stream));
-    MI_HIP_CHECK(hipcub::DeviceReduce::ReduceByKey(nullptr, tmp_red, keys_s.get(), keys.get(), vals_s.get(), vals.get(),
-                                                   nruns.get(), d2sum(), nmax, stream));
-    hp.alloc(max_blk, stream, false);
-    hsel.alloc(max_blk, stream, false);
-    MI_HIP_CHECK(hipcub::DeviceSelect::If(nullptr, tmp_sel, hp.get(), hsel.get(), nsel.get(), nmax,
-                                          h_keep{ 0, r0, r1, sizeof(T) == 4 }, stream));
-    dev_buf<unsigned char> tmp;
-    tmp.alloc((int64_t) std::max({ tmp_sort, tmp_scan, tmp_red, tmp_sel, (size_t) 16 }), stream, false);
-
-    // growable list of kept lower pairs (li > lj), in (li, lj) order
-    dev_buf<int32_t> Li, Lj;
-    dev_buf<T> Lh;
-    int64_t P = 0, cap = 0;
-    auto grow = [&](int64_t need) {
-        if (need <= cap) return;
-        const int64_t nc = std::max<int64_t>(need, cap + cap / 2 + 1024);
-        dev_buf<int32_t> ni, nj;
-        dev_buf<T> nh;
-        ni.alloc(nc, stream, false);
-        nj.alloc(nc, stream, false);
-        nh.alloc(nc, stream, false);
-        if (P > 0) {
-            MI_HIP_CHECK(hipMemcpyAsync(ni.get(), Li.get(), sizeof(int32_t) * (size_t) P, hipMemcpyDeviceToDevice, stream));
-            MI_HIP_CHECK(hipMemcpyAsync(nj.get(), Lj.get(), sizeof(int32_t) * (size_t) P, hipMemcpyDeviceToDevice, stream));
-            MI_HIP_CHECK(hipMemcpyAsync(nh.get(), Lh.get(), sizeof(T) * (size_t) P, hipMemcpyDeviceToDevice, stream));
-        }
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-        Li = std::move(ni);
-        Lj = std::move(nj);
-        Lh = std::move(nh);
-        cap = nc;
-    };
-    double st_gen = 0, st_sort = 0, st_red = 0, st_sel = 0;  // PLSSVM_MI_TIMING: stage seconds
-    auto stage = [&](double &acc) {
-        if (!pt.on) return;
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-        const auto now = std::chrono::steady_clock::now();
-        acc += std::chrono::duration<double>(now - pt.t).count();
-        pt.t = now;
-    };
-    for (auto &b : blocks) {
-        const int64_t i0 = b.first, rows = b.second - b.first;
-        int64_t total = 0;
-        for (int64_t i = b.first; i < b.second; ++i) total += inc[i];
-        if (total == 0) continue;
-        hipLaunchKernelGGL(exp_count_kernel, dim3((unsigned) ceil_div(rows, 256)), dim3(256), 0, stream,
-                           csr.rowptr.get(), csr.col.get(), cpos, csr.colptr.get(), i0, b.second, cntb.get());
-        MI_LAUNCH_CHECK();
-        size_t ts = tmp_scan;
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.get(), ts, cntb.get(), off.get(), (int) (rows + 1), stream));
-        hipLaunchKernelGGL(exp_gen_kernel<T>, dim3((unsigned) rows), dim3(256), 0, stream, csr.rowptr.get(), csr.col.get(),
-                           csr.val.get(), cpos, csr.colptr.get(), csr.crow.get(), csr.cval.get(), i0, off.get(),
-                           keys.get(), vals.get(), phi);
-        MI_LAUNCH_CHECK();
-        stage(st_gen);
-        const int end_bit = 32 + std::max(1, (int) std::ceil(std::log2((double) rows + 1.0)));
-        size_t t1s = tmp_sort;
-        MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp.get(), t1s, keys.get(), keys_s.get(), vals.get(),
-                                                        vals_s.get(), (int) total, 0, end_bit, stream));
-        stage(st_sort);
-        size_t t2s = tmp_red;
-        MI_HIP_CHECK(hipcub::DeviceReduce::ReduceByKey(tmp.get(), t2s, keys_s.get(), keys.get(), vals_s.get(),
-                                                       vals.get(), nruns.get(), d2sum(), (int) total, stream));
-        hipLaunchKernelGGL(exp_h_kernel, dim3((unsigned) ceil_div(total, 256)), dim3(256), 0, stream, keys.get(),
-                           vals.get(), nruns.get(), phi, hp.get());
-        MI_LAUNCH_CHECK();
-        stage(st_red);
-        int64_t nu = 0;
-        MI_HIP_CHECK(hipMemcpyAsync(&nu, nruns.get(), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-        size_t t3s = tmp_sel;
-        MI_HIP_CHECK(hipcub::DeviceSelect::If(tmp.get(), t3s, hp.get(), hsel.get(), nsel.get(), (int) nu,
-                                              h_keep{ i0, r0, r1, sizeof(T) == 4 }, stream));
-        int64_t ns = 0;
-        MI_HIP_CHECK(hipMemcpyAsync(&ns, nsel.get(), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-        if (ns == 0) continue;
-        grow(P + ns);
-        hipLaunchKernelGGL(exp_append_kernel<T>, dim3((unsigned) ceil_div(ns, 256)), dim3(256), 0, stream, hsel.get(),
-                           nsel.get(), i0, Li.get() + P, Lj.get() + P, Lh.get() + P);
-        MI_LAUNCH_CHECK();
-        P += ns;
-        stage(st_sel);
-    }
-    if (pt.on)
-        std::fprintf(stderr, "[plssvm_mi] column join: %zu blocks, gen %.3f sort %.3f reduce %.3f select+append %.3f\n",
-                     blocks.size(), st_gen, st_sort, st_red, st_sel);
-    keys.reset(), keys_s.reset(), vals.reset(), vals_s.reset(), hp.reset(), hsel.reset(), tmp.reset();
-    pt.mark("expansion: column join (blocks)");
-    if (P > INT32_MAX) throw mi_error(-5, "more than 2^31 multi-feature pairs on one rank: use more GPUs");
-
-    // ---- symmetric rows [r0, r1), padded to 8 slots ----
+    // ---- the remainder's symmetric rows [r0, r1), padded to 8 slots: off8[R + 1], (sj, sv)[nslot8] ----
     const int64_t R = r1 - r0;
-    dev_buf<unsigned long long> clo, cup;
-    dev_buf<int64_t> cnt8, off8, lo_start, up_start;
-    dev_buf<uint32_t> ukey, ukey_s, uidx, uidx_s;
-    clo.alloc(std::max<int64_t>(R, 1), stream);
-    cup.alloc(std::max<int64_t>(R, 1), stream);
-    cnt8.alloc(R + 1, stream);
-    off8.alloc(R + 1, stream);
-    lo_start.alloc(R + 1, stream);
-    up_start.alloc(R + 1, stream);
-    ukey.alloc(std::max<int64_t>(P, 1), stream, false);
-    if (P > 0) {
-        hipLaunchKernelGGL(exp_hist_kernel, dim3((unsigned) ceil_div(P, 256)), dim3(256), 0, stream, Li.get(), Lj.get(), P,
-                           r0, r1, clo.get(), cup.get(), ukey.get());
-        MI_LAUNCH_CHECK();
-    }
-    if (R > 0) {
-        hipLaunchKernelGGL(exp_pad8_kernel, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream, clo.get(), cup.get(),
-                           R, cnt8.get());
-        MI_LAUNCH_CHECK();
-    }
-    {
-        size_t ta = 0, tb = 0, tc = 0;  // each scan queries its own temporary size (types differ)
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ta, cnt8.get(), off8.get(), (int) (R + 1), stream));
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, clo.get(), lo_start.get(), (int) R, stream));
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tc, cup.get(), up_start.get(), (int) R, stream));
-        dev_buf<unsigned char> t;
-        t.alloc((int64_t) std::max({ ta, tb, tc, (size_t) 16 }), stream, false);
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), ta, cnt8.get(), off8.get(), (int) (R + 1), stream));
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, clo.get(), lo_start.get(), (int) R, stream));
-        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tc, cup.get(), up_start.get(), (int) R, stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-    }
-    ex.pairs = 0;
-    {
-        // rows' lower pairs are the list's prefix (sorted by li); count them
-        std::vector<unsigned long long> hlo(std::max<int64_t>(R, 1), 0);
-        if (R > 0)
-            MI_HIP_CHECK(hipMemcpyAsync(hlo.data(), clo.get(), sizeof(unsigned long long) * (size_t) R,
-                                        hipMemcpyDeviceToHost, stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-        for (int64_t r = 0; r < R; ++r) ex.pairs += (int64_t) hlo[r];
-    }
-    // padded symmetric rows (temporary): row r's entries in [off8[r], off8[r + 1]), sorted by j
-    int64_t nslot8 = 0;
-    MI_HIP_CHECK(hipMemcpyAsync(&nslot8, off8.get() + R, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
-    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    dev_buf<int64_t> off8;
     dev_buf<int32_t> sj;
     dev_buf<T> sv;
-    dev_buf<int32_t> scrow;
-    sj.alloc(std::max<int64_t>(nslot8, 8), stream, false);
-    sv.alloc(std::max<int64_t>(nslot8, 8), stream);
-    scrow.alloc(std::max<int64_t>(nslot8 / 8, 1), stream, false);
-    if (R > 0) {
-        hipLaunchKernelGGL(exp_init_rows_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream, off8.get(), R,
-                           r0, sj.get(), sv.get(), scrow.get());
-        MI_LAUNCH_CHECK();
-    }
-    scrow.reset();
-    if (P > 0) {
-        hipLaunchKernelGGL(exp_place_lower_kernel<T>, dim3((unsigned) ceil_div(P, 256)), dim3(256), 0, stream, Li.get(),
-                           Lj.get(), Lh.get(), P, r0, r1, lo_start.get(), off8.get(), sj.get(), sv.get());
-        MI_LAUNCH_CHECK();
-        // upper part: entries with j in [r0, r1), stably sorted by j (their li order is kept)
-        uidx.alloc(P, stream, false);
-        ukey_s.alloc(P, stream, false);
-        uidx_s.alloc(P, stream, false);
+    int64_t nslot8 = 0;
+    // the column-join sort (PLSSVM_MI_EXP_JOIN=sort, and rows longer than the row join's LDS copy)
+    auto sort_join = [&]() {
+        // ---- incidences per row (host) -> row sub-blocks of at most CAP incidences ----
+        std::vector<int64_t> inc(std::max<int64_t>(m, 1), 0);
         {
-            hipLaunchKernelGGL(exp_iota_kernel, dim3((unsigned) ceil_div(P, 256)), dim3(256), 0, stream, uidx.get(), P);
+            dev_buf<int64_t> cnt;
+            cnt.alloc(std::max<int64_t>(m, 1), stream);
+            if (m > 0)
+                hipLaunchKernelGGL(exp_count_kernel, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream,
+                                   csr.rowptr.get(), csr.col.get(), cpos, csr.colptr.get(), (int64_t) 0, m, cnt.get());
             MI_LAUNCH_CHECK();
-            size_t tb = 0;
-            MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ukey.get(), ukey_s.get(), uidx.get(),
-                                                            uidx_s.get(), (int) P, 0, 32, stream));
-            dev_buf<unsigned char> t;
-            t.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
-            MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(t.get(), tb, ukey.get(), ukey_s.get(), uidx.get(),
-                                                            uidx_s.get(), (int) P, 0, 32, stream));
+            if (m > 0)
+                MI_HIP_CHECK(hipMemcpyAsync(inc.data(), cnt.get(), sizeof(int64_t) * (size_t) m, hipMemcpyDeviceToHost,
+                                            stream));
             MI_HIP_CHECK(hipStreamSynchronize(stream));
         }
-        int64_t nup = 0;
+        // incidences per sub-block (≈ 80 B each in flight); PLSSVM_MI_EXP_CAPLOG = log2 (measurements)
+        const int64_t CAP = int64_t(1) << [] {
+            const char *e = std::getenv("PLSSVM_MI_EXP_CAPLOG");
+            const int v = e ? std::atoi(e) : 0;
+            return v >= 20 && v <= 31 ? v : 27;
+        }();
+        constexpr int64_t ROWS_MAX = 65536;            // rows per sub-block (one workgroup per row)
+        std::vector<std::pair<int64_t, int64_t>> blocks;
         {
-            std::vector<unsigned long long> hup(std::max<int64_t>(R, 1), 0);
+            int64_t a = r0, acc = 0;  // pairs (i, j < i) touch rows [r0, r1) only if i >= r0
+            for (int64_t i = r0; i < m; ++i) {
+                if (inc[i] > CAP) throw mi_error(-4, "a data point shares features with more than 2^27 others (dense row)");
+                if (i > a && (acc + inc[i] > CAP || i - a >= ROWS_MAX)) {
+                    blocks.emplace_back(a, i);
+                    a = i;
+                    acc = 0;
+                }
+                acc += inc[i];
+            }
+            if (a < m) blocks.emplace_back(a, m);
+        }
+        int64_t max_blk = 1;
+        for (auto &b : blocks) {
+            int64_t s = 0;
+            for (int64_t i = b.first; i < b.second; ++i) s += inc[i];
+            max_blk = std::max(max_blk, s);
+        }
+
+        // ---- temporaries ----
+        dev_buf<uint64_t> keys, keys_s;
+        dev_buf<double2> vals, vals_s;
+        dev_buf<hpair> hp, hsel;
+        dev_buf<int64_t> cntb, off, nruns, nsel;
+        keys.alloc(max_blk, stream, false);
+        keys_s.alloc(max_blk, stream, false);
+        vals.alloc(max_blk, stream, false);
+        vals_s.alloc(max_blk, stream, false);
+        cntb.alloc(ROWS_MAX + 1, stream);
+        off.alloc(ROWS_MAX + 1, stream);
+        nruns.alloc(1, stream);
+        nsel.alloc(1, stream);
+        size_t tmp_sort = 0, tmp_scan = 0, tmp_red = 0, tmp_sel = 0;
+        const int nmax = (int) max_blk;
+        MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_sort, keys.get(), keys_s.get(), vals.get(),
+                                                        vals_s.get(), nmax, 0, 64, stream));
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_scan, cntb.get(), off.get(), (int) (ROWS_MAX + 1), stream));
+        MI_HIP_CHECK(hipcub::DeviceReduce::ReduceByKey(nullptr, tmp_red, keys_s.get(), keys.get(), vals_s.get(), vals.get(),
+                                                       nruns.get(), d2sum(), nmax, stream));
+        hp.alloc(max_blk, stream, false);
+        hsel.alloc(max_blk, stream, false);
+        MI_HIP_CHECK(hipcub::DeviceSelect::If(nullptr, tmp_sel, hp.get(), hsel.get(), nsel.get(), nmax,
+                                              h_keep{ 0, r0, r1, sizeof(T) == 4 }, stream));
+        dev_buf<unsigned char> tmp;
+        tmp.alloc((int64_t) std::max({ tmp_sort, tmp_scan, tmp_red, tmp_sel, (size_t) 16 }), stream, false);
+
+        // growable list of kept lower pairs (li > lj), in (li, lj) order
+        dev_buf<int32_t> Li, Lj;
+        dev_buf<T> Lh;
+        int64_t P = 0, cap = 0;
+        auto grow = [&](int64_t need) {
+            if (need <= cap) return;
+            const int64_t nc = std::max<int64_t>(need, cap + cap / 2 + 1024);
+            dev_buf<int32_t> ni, nj;
+            dev_buf<T> nh;
+            ni.alloc(nc, stream, false);
+            nj.alloc(nc, stream, false);
+            nh.alloc(nc, stream, false);
+            if (P > 0) {
+                MI_HIP_CHECK(hipMemcpyAsync(ni.get(), Li.get(), sizeof(int32_t) * (size_t) P, hipMemcpyDeviceToDevice, stream));
+                MI_HIP_CHECK(hipMemcpyAsync(nj.get(), Lj.get(), sizeof(int32_t) * (size_t) P, hipMemcpyDeviceToDevice, stream));
+                MI_HIP_CHECK(hipMemcpyAsync(nh.get(), Lh.get(), sizeof(T) * (size_t) P, hipMemcpyDeviceToDevice, stream));
+            }
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            Li = std::move(ni);
+            Lj = std::move(nj);
+            Lh = std::move(nh);
+            cap = nc;
+        };
+        double st_gen = 0, st_sort = 0, st_red = 0, st_sel = 0;  // PLSSVM_MI_TIMING: stage seconds
+        auto stage = [&](double &acc) {
+            if (!pt.on) return;
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            const auto now = std::chrono::steady_clock::now();
+            acc += std::chrono::duration<double>(now - pt.t).count();
+            pt.t = now;
+        };
+        for (auto &b : blocks) {
+            const int64_t i0 = b.first, rows = b.second - b.first;
+            int64_t total = 0;
+            for (int64_t i = b.first; i < b.second; ++i) total += inc[i];
+            if (total == 0) continue;
+            hipLaunchKernelGGL(exp_count_kernel, dim3((unsigned) ceil_div(rows, 256)), dim3(256), 0, stream,
+                               csr.rowptr.get(), csr.col.get(), cpos, csr.colptr.get(), i0, b.second, cntb.get());
+            MI_LAUNCH_CHECK();
+            size_t ts = tmp_scan;
+            MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.get(), ts, cntb.get(), off.get(), (int) (rows + 1), stream));
+            hipLaunchKernelGGL(exp_gen_kernel<T>, dim3((unsigned) rows), dim3(256), 0, stream, csr.rowptr.get(), csr.col.get(),
+                               csr.val.get(), cpos, csr.colptr.get(), csr.crow.get(), csr.cval.get(), i0, off.get(),
+                               keys.get(), vals.get(), phi);
+            MI_LAUNCH_CHECK();
+            stage(st_gen);
+            const int end_bit = 32 + std::max(1, (int) std::ceil(std::log2((double) rows + 1.0)));
+            size_t t1s = tmp_sort;
+            MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp.get(), t1s, keys.get(), keys_s.get(), vals.get(),
+                                                            vals_s.get(), (int) total, 0, end_bit, stream));
+            stage(st_sort);
+            size_t t2s = tmp_red;
+            MI_HIP_CHECK(hipcub::DeviceReduce::ReduceByKey(tmp.get(), t2s, keys_s.get(), keys.get(), vals_s.get(),
+                                                           vals.get(), nruns.get(), d2sum(), (int) total, stream));
+            hipLaunchKernelGGL(exp_h_kernel, dim3((unsigned) ceil_div(total, 256)), dim3(256), 0, stream, keys.get(),
+                               vals.get(), nruns.get(), phi, hp.get());
+            MI_LAUNCH_CHECK();
+            stage(st_red);
+            int64_t nu = 0;
+            MI_HIP_CHECK(hipMemcpyAsync(&nu, nruns.get(), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            size_t t3s = tmp_sel;
+            MI_HIP_CHECK(hipcub::DeviceSelect::If(tmp.get(), t3s, hp.get(), hsel.get(), nsel.get(), (int) nu,
+                                                  h_keep{ i0, r0, r1, sizeof(T) == 4 }, stream));
+            int64_t ns = 0;
+            MI_HIP_CHECK(hipMemcpyAsync(&ns, nsel.get(), sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            if (ns == 0) continue;
+            grow(P + ns);
+            hipLaunchKernelGGL(exp_append_kernel<T>, dim3((unsigned) ceil_div(ns, 256)), dim3(256), 0, stream, hsel.get(),
+                               nsel.get(), i0, Li.get() + P, Lj.get() + P, Lh.get() + P);
+            MI_LAUNCH_CHECK();
+            P += ns;
+            stage(st_sel);
+        }
+        if (pt.on)
+            std::fprintf(stderr, "[plssvm_mi] column join: %zu blocks, gen %.3f sort %.3f reduce %.3f select+append %.3f\n",
+                         blocks.size(), st_gen, st_sort, st_red, st_sel);
+        keys.reset(), keys_s.reset(), vals.reset(), vals_s.reset(), hp.reset(), hsel.reset(), tmp.reset();
+        pt.mark("expansion: column join (blocks)");
+        if (P > INT32_MAX) throw mi_error(-5, "more than 2^31 multi-feature pairs on one rank: use more GPUs");
+
+        // ---- symmetric rows [r0, r1), padded to 8 slots ----
+        dev_buf<unsigned long long> clo, cup;
+        dev_buf<int64_t> cnt8, lo_start, up_start;
+        dev_buf<uint32_t> ukey, ukey_s, uidx, uidx_s;
+        clo.alloc(std::max<int64_t>(R, 1), stream);
+        cup.alloc(std::max<int64_t>(R, 1), stream);
+        cnt8.alloc(R + 1, stream);
+        off8.alloc(R + 1, stream);
+        lo_start.alloc(R + 1, stream);
+        up_start.alloc(R + 1, stream);
+        ukey.alloc(std::max<int64_t>(P, 1), stream, false);
+        if (P > 0) {
+            hipLaunchKernelGGL(exp_hist_kernel, dim3((unsigned) ceil_div(P, 256)), dim3(256), 0, stream, Li.get(), Lj.get(), P,
+                               r0, r1, clo.get(), cup.get(), ukey.get());
+            MI_LAUNCH_CHECK();
+        }
+        if (R > 0) {
+            hipLaunchKernelGGL(exp_pad8_kernel, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream, clo.get(), cup.get(),
+                               R, cnt8.get());
+            MI_LAUNCH_CHECK();
+        }
+        {
+            size_t ta = 0, tb = 0, tc = 0;  // each scan queries its own temporary size (types differ)
+            MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, ta, cnt8.get(), off8.get(), (int) (R + 1), stream));
+            MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, clo.get(), lo_start.get(), (int) R, stream));
+            MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tc, cup.get(), up_start.get(), (int) R, stream));
+            dev_buf<unsigned char> t;
+            t.alloc((int64_t) std::max({ ta, tb, tc, (size_t) 16 }), stream, false);
+            MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), ta, cnt8.get(), off8.get(), (int) (R + 1), stream));
+            MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, clo.get(), lo_start.get(), (int) R, stream));
+            MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tc, cup.get(), up_start.get(), (int) R, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+        }
+        ex.pairs = 0;
+        {
+            // rows' lower pairs are the list's prefix (sorted by li); count them
+            std::vector<unsigned long long> hlo(std::max<int64_t>(R, 1), 0);
             if (R > 0)
-                MI_HIP_CHECK(hipMemcpyAsync(hup.data(), cup.get(), sizeof(unsigned long long) * (size_t) R,
+                MI_HIP_CHECK(hipMemcpyAsync(hlo.data(), clo.get(), sizeof(unsigned long long) * (size_t) R,
                                             hipMemcpyDeviceToHost, stream));
             MI_HIP_CHECK(hipStreamSynchronize(stream));
-            for (int64_t r = 0; r < R; ++r) nup += (int64_t) hup[r];
+            for (int64_t r = 0; r < R; ++r) ex.pairs += (int64_t) hlo[r];
         }
-        if (nup > 0) {
-            hipLaunchKernelGGL(exp_place_upper_kernel<T>, dim3((unsigned) ceil_div(nup, 256)), dim3(256), 0, stream,
-                               ukey_s.get(), uidx_s.get(), nup, Li.get(), Lh.get(), clo.get(), up_start.get(), off8.get(),
-                               sj.get(), sv.get());
+        // padded symmetric rows (temporary): row r's entries in [off8[r], off8[r + 1]), sorted by j
+        MI_HIP_CHECK(hipMemcpyAsync(&nslot8, off8.get() + R, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        dev_buf<int32_t> scrow;
+        sj.alloc(std::max<int64_t>(nslot8, 8), stream, false);
+        sv.alloc(std::max<int64_t>(nslot8, 8), stream);
+        scrow.alloc(std::max<int64_t>(nslot8 / 8, 1), stream, false);
+        if (R > 0) {
+            hipLaunchKernelGGL(exp_init_rows_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream, off8.get(), R,
+                               r0, sj.get(), sv.get(), scrow.get());
             MI_LAUNCH_CHECK();
         }
+        scrow.reset();
+        if (P > 0) {
+            hipLaunchKernelGGL(exp_place_lower_kernel<T>, dim3((unsigned) ceil_div(P, 256)), dim3(256), 0, stream, Li.get(),
+                               Lj.get(), Lh.get(), P, r0, r1, lo_start.get(), off8.get(), sj.get(), sv.get());
+            MI_LAUNCH_CHECK();
+            // upper part: entries with j in [r0, r1), stably sorted by j (their li order is kept)
+            uidx.alloc(P, stream, false);
+            ukey_s.alloc(P, stream, false);
+            uidx_s.alloc(P, stream, false);
+            {
+                hipLaunchKernelGGL(exp_iota_kernel, dim3((unsigned) ceil_div(P, 256)), dim3(256), 0, stream, uidx.get(), P);
+                MI_LAUNCH_CHECK();
+                size_t tb = 0;
+                MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ukey.get(), ukey_s.get(), uidx.get(),
+                                                                uidx_s.get(), (int) P, 0, 32, stream));
+                dev_buf<unsigned char> t;
+                t.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
+                MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(t.get(), tb, ukey.get(), ukey_s.get(), uidx.get(),
+                                                                uidx_s.get(), (int) P, 0, 32, stream));
+                MI_HIP_CHECK(hipStreamSynchronize(stream));
+            }
+            int64_t nup = 0;
+            {
+                std::vector<unsigned long long> hup(std::max<int64_t>(R, 1), 0);
+                if (R > 0)
+                    MI_HIP_CHECK(hipMemcpyAsync(hup.data(), cup.get(), sizeof(unsigned long long) * (size_t) R,
+                                                hipMemcpyDeviceToHost, stream));
+                MI_HIP_CHECK(hipStreamSynchronize(stream));
+                for (int64_t r = 0; r < R; ++r) nup += (int64_t) hup[r];
+            }
+            if (nup > 0) {
+                hipLaunchKernelGGL(exp_place_upper_kernel<T>, dim3((unsigned) ceil_div(nup, 256)), dim3(256), 0, stream,
+                                   ukey_s.get(), uidx_s.get(), nup, Li.get(), Lh.get(), clo.get(), up_start.get(), off8.get(),
+                                   sj.get(), sv.get());
+                MI_LAUNCH_CHECK();
+            }
+        }
+        Li.reset(), Lj.reset(), Lh.reset(), uidx.reset(), ukey.reset(), ukey_s.reset(), uidx_s.reset();
+    };
+    const char *je = std::getenv("PLSSVM_MI_EXP_JOIN");
+    bool row_join = !(je != nullptr && std::strcmp(je, "sort") == 0);
+    if (row_join && R > 0) {
+        // host checks: every row of the rank within the row join's LDS copy, incidences within int32
+        std::vector<int64_t> rp((size_t) (R + 1));
+        MI_HIP_CHECK(hipMemcpyAsync(rp.data(), csr.rowptr.get() + r0, sizeof(int64_t) * (size_t) (R + 1),
+                                    hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        for (int64_t r = 0; r < R && row_join; ++r) row_join = rp[(size_t) r + 1] - rp[(size_t) r] <= RJ_ECAP;
+        if (row_join && csr.nnz >= (int64_t) INT32_MAX) row_join = false;  // a row's incidences <= nnz
     }
-    Li.reset(), Lj.reset(), Lh.reset(), uidx.reset(), ukey.reset(), ukey_s.reset(), uidx_s.reset();
+    if (row_join) {
+        off8.alloc(R + 1, stream);
+        dev_buf<int64_t> cnt, cnt8;
+        dev_buf<unsigned long long> lnz;
+        cnt.alloc(std::max<int64_t>(R, 1), stream);
+        cnt8.alloc(R + 1, stream);
+        lnz.alloc(1, stream);
+        if (R > 0) {
+            hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
+                               csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(),
+                               (const int64_t *) nullptr, (int32_t *) nullptr);
+            MI_LAUNCH_CHECK();
+            hipLaunchKernelGGL(exp_pad8_cnt_kernel, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream, cnt.get(),
+                               R, cnt8.get());
+            MI_LAUNCH_CHECK();
+        }
+        size_t tb = 0;
+        MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt8.get(), off8.get(), (int) (R + 1), stream));
+        {
+            dev_buf<unsigned char> t;
+            t.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
+            MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, cnt8.get(), off8.get(), (int) (R + 1), stream));
+            MI_HIP_CHECK(hipMemcpyAsync(&nslot8, off8.get() + R, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+        }
+        pt.mark("expansion: row join (count)");
+        sj.alloc(std::max<int64_t>(nslot8, 8), stream, false);
+        sv.alloc(std::max<int64_t>(nslot8, 8), stream, false);
+        if (R > 0) {
+            hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
+                               csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(), off8.get(), sj.get());
+            MI_LAUNCH_CHECK();
+            hipLaunchKernelGGL(exp_rowjoin_h_kernel<T>, dim3((unsigned) R), dim3(RJH_NT), 0, stream, csr.rowptr.get(),
+                               csr.col.get(), csr.val.get(), r0, phi, off8.get(), sj.get(), sv.get(), lnz.get());
+            MI_LAUNCH_CHECK();
+        }
+        unsigned long long np = 0;
+        MI_HIP_CHECK(hipMemcpyAsync(&np, lnz.get(), sizeof(np), hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        ex.pairs = (int64_t) np;
+        pt.mark("expansion: row join (rows)");
+    } else {
+        sort_join();
+    }
     pt.mark("expansion: symmetric rows");
 
     // ---- cells: blocks of RB rows x windows of CW partners, rows padded to 4 slots per cell ----
@@ -1273,13 +1547,18 @@ void engine<T>::expansion_moments(const T *w, const cg_scalars<T> *status) {
 template <typename T>
 void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base) {
     auto &ex = csr.ex;
+    // sharded: w of this rank's rows, then gathered from every rank (the remainder stream reads partners of
+    // all rows); the raw of this rank's rows stays local (no row gather)
+    const int64_t ib = shard ? r0 : 0, ie = shard ? r1 : m;
     const T *w = p;
     if (kernel == 2) {
-        hipLaunchKernelGGL(exp_w_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream, csr.e.get(), p, m,
-                           ex.wv.get(), status);
+        if (ie > ib)
+            hipLaunchKernelGGL(exp_w_kernel<T>, dim3((unsigned) ceil_div(ie - ib, 256)), dim3(256), 0, stream,
+                               csr.e.get() + ib, p + ib, ie - ib, ex.wv.get() + ib, status);
         MI_LAUNCH_CHECK();
         w = ex.wv.get();
     }
+    gather_input(w);
     launch_dot2<T>(w, nullptr, nullptr, nullptr, m, red.get(), status, stream);  // S = sum_j w_j
     launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
     expansion_moments(w, status);
@@ -1291,11 +1570,12 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     }
     // J_i = sum_{f in x_i} sum_k x_if^(k+1) M[f][k]: one SELL pass over this rank's CSR rows (mode 2)
     if (r1 > r0) launch_panel_spmv<T>(csr.spmv_csr, ex.M.get(), d, raw.get() + r0, status, stream, ex.KM, 2);
-    hipLaunchKernelGGL(exp_combine_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream,
-                       kernel == 2 ? csr.e.get() : nullptr, w, ex.hdiag.get(), ex.phin.get(), ex.hs.get(), csr.ssc.get(),
-                       kappa, m, r0, r1, with_base ? 0 : 1, raw.get(), status);
+    if (ie > ib)
+        hipLaunchKernelGGL(exp_combine_kernel<T>, dim3((unsigned) ceil_div(ie - ib, 256)), dim3(256), 0, stream,
+                           kernel == 2 ? csr.e.get() : nullptr, w, ex.hdiag.get(), ex.phin.get(), ex.hs.get(),
+                           csr.ssc.get(), kappa, ib, ie, r0, r1, with_base ? 0 : 1, raw.get(), status);
     MI_LAUNCH_CHECK();
-    allgather_rows(raw.get());
+    if (!shard) allgather_rows(raw.get());
 }
 
 // ---- predict through the expansion (csvm::predict on sparse poly / rbf models) -----------------------

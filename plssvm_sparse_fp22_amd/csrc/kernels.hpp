@@ -54,7 +54,10 @@ void launch_q_dense(kfun<T> kf, const T *XT, int64_t n_pad, int64_t d, int64_t m
 // (SI, SJ), SI >= SJ, linear index tri_index(SI, SJ)); a rank owns a contiguous super-block range.
 constexpr int KP_SUPER = 8;
 
-// partial[c][i]: sum_{j in col-block c} k(x_i,x_j) p_j for the tiles of super-blocks [s0, s0+nsuper)
+// slab record of one tile: its 128 row sums, then its 128 column sums (the rank's slab: wgs records)
+constexpr int KP_REC = 2 * KP_TILE;
+// partial[wg][KP_REC]: per tile wg of super-blocks [s0, s0+nsuper), sum_{j in J} k(x_i,x_j) p_j for i in I
+// and sum_{i in I} k(x_i,x_j) p_i for j in J
 // wg_off[k] (k = 0..nsuper): first workgroup of super-block s0 + k (one workgroup per real tile: 64 for a
 // full super-block, 36 for a diagonal one, fewer in the ragged last row); wgs = wg_off[nsuper]
 void kp_tile_offsets(int64_t nb, int64_t s0, int64_t nsuper, std::vector<int32_t> &wg_off);
@@ -63,9 +66,10 @@ void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *par
                      int64_t nb, int64_t s0, int64_t nsuper, const int32_t *wg_off, int64_t wgs,
                      const cg_scalars<T> *status, hipStream_t s);
 
-// raw[i] = sum_c partial[c][i] over the tiles whose super-block lies in [s0, s1); i < m
+// raw[i] = sum over the column blocks c in order of row i's slab values of the tiles whose super-block lies
+// in [s0, s1) (tile (Ib, c) row sums for c <= Ib, tile (c, Ib) column sums for c > Ib); i < m
 template <typename T>
-void launch_kp_reduce(const T *partial, int64_t nb, int64_t n_pad, int64_t m, int64_t s0, int64_t s1, T *raw,
+void launch_kp_reduce(const T *partial, int64_t nb, int64_t m, int64_t s0, int64_t s1, const int32_t *wg_off, T *raw,
                       const cg_scalars<T> *status, hipStream_t s);
 
 // ret[i] = (overwrite ? 0 : ret[i]) + add * (raw[i] + (QA - q_i) * sum(p) - sum(q p) + p_i / C)
@@ -90,9 +94,10 @@ void launch_dot2(const T *a, const T *b, const T *c, const T *e, int64_t n, T *p
                  hipStream_t s);
 // final reductions with CG scalar updates; `what` selects the update (see blas1.hip)
 enum final_op { FIN_SP_SQP = 0, FIN_DELTA0 = 1, FIN_ALPHA = 2, FIN_DELTA = 3, FIN_PLAIN = 4 };
+// G > 1: G gathered partial sets of a sharded group (rank-major, summed in rank order per partial)
 template <typename T>
 void launch_dot_final(const T *partials, cg_scalars<T> *sc, int op, int64_t run, double *trace, int64_t trace_cap,
-                      T *plain_out, hipStream_t s);
+                      T *plain_out, hipStream_t s, int G = 1);
 template <typename T>
 void launch_cg_init(const T *b, int64_t m, T *x, T *r, hipStream_t s);
 template <typename T>
@@ -108,19 +113,22 @@ void launch_cg_direction(T *d, const T *r, int64_t m, const cg_scalars<T> *sc, h
 // dot_final_kernel's order: every block gets the same value), so no final-reduction launch sits
 // between them; dots keep dot2_kernel's grid and order, so the results are bitwise those of the
 // unfused sequence.
+// The input partials (psum, pdad, prr) are G gathered sets in a sharded group (G = 1 otherwise); the
+// vectors are the caller's element range (pointers offset to it, m = its length).
 // Ad = Q~ d from raw (kp_finalize arithmetic, add = 1, overwrite), sum d / sum q d from psum;
-// d.Ad partials -> pdad. slabs != null: raw = the P panel slabs [P][m] of an unreduced SpMV pass.
+// d.Ad partials -> pdad. slabs != null: raw = the P panel slabs [P][sstride] of an unreduced SpMV pass.
 template <typename T>
-void launch_cg_fin_dad(const T *raw, const T *slabs, int64_t P, const T *q, const T *d, const T *psum, T QA_cost,
-                       T cost_inv, int raw_only, int64_t m, T *Ad, T *pdad, cg_scalars<T> *sc, hipStream_t s);
+void launch_cg_fin_dad(const T *raw, const T *slabs, int64_t P, int64_t sstride, const T *q, const T *d, const T *psum,
+                       int G, T QA_cost, T cost_inv, int raw_only, int64_t m, T *Ad, T *pdad, cg_scalars<T> *sc,
+                       hipStream_t s);
 // alpha = delta / d.Ad (pdad); x += alpha d; r -= alpha Ad and r.r partials -> prr (reset: r = b)
 template <typename T>
-void launch_cg_upd_rr(T *x, T *r, const T *d, const T *Ad, const T *b, int reset, const T *pdad, int64_t m, T *prr,
-                      cg_scalars<T> *sc, hipStream_t s);
+void launch_cg_upd_rr(T *x, T *r, const T *d, const T *Ad, const T *b, int reset, const T *pdad, int G, int64_t m,
+                      T *prr, cg_scalars<T> *sc, hipStream_t s);
 // delta = r.r (prr), stop test, beta; d = beta d + r (init: d = r, scalars untouched);
 // sum d / sum q d partials -> psum. The iteration index is sc->iters (trace[iters + 1] = delta, iters += 1).
 template <typename T>
-void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int init, double *trace, int64_t trace_cap,
+void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int G, int init, double *trace, int64_t trace_cap,
                         int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s);
 
 // ---- sparse (CSR / FP22) ------------------------------------------------------------------------

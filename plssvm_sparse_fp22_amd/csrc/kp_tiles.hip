@@ -12,8 +12,9 @@
 //     v_mfma_f32_16x16x4_f32 (exact fma chains in k order);
 //   * epilogue in registers: kernel function (RBF via ||a||^2 + ||b||^2 - 2 a.b, clamped at 0),
 //     times p_j -> row sums (16-lane shuffles) and times p_i -> mirrored column sums (cross-half
-//     shuffles); results go to partial[J][i in I] and partial[I][j in J] — no atomics, so a
-//     fixed-order second pass makes K·p bitwise reproducible;
+//     shuffles); results go to the tile's own 256-value record of the rank's slab (row sums, then
+//     column sums: the slab holds only this rank's tiles, so it shrinks with the group) — no atomics,
+//     so a fixed-order second pass makes K·p bitwise reproducible;
 //   * tiles are visited in 8x8 super-blocks (16 panels = 4 MiB in fp64: one XCD's L2) and the
 //     workgroup ids are remapped so each XCD walks a contiguous range of super-blocks.
 #include "kernels.hpp"
@@ -367,62 +368,66 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
         const T *cp = smem + OFF_PAN + 2 * RHALF + (h * KP_TILE + q) * CSTR;
         T c = (cp[0] + cp[1]) + (cp[2] + cp[3]);
         c += __shfl_xor(c, 1);
-        if (h == 1) partial[I * n_pad + J0 + q] = c;
+        if (h == 1) partial[wg * KP_REC + KP_TILE + q] = c;  // column sums of the J rows
     }
-    if (h == 0) partial[J * n_pad + I0 + q] = a;
+    if (h == 0) partial[wg * KP_REC + q] = a;  // row sums of the I rows
 }
 
+// The slab record of tile (I, J), I >= J, of the rank's super-blocks [s0, s1): its workgroup index
+// (kp_tile_offsets' table + the tile's place in its super-block), or -1 when another rank owns it.
+__device__ __forceinline__ int64_t kp_tile_record(int64_t I, int64_t J, int64_t nb, int64_t s0, int64_t s1,
+                                                  const int32_t *__restrict__ wg_off) {
+    const int64_t SI = I / KP_SUPER, SJ = J / KP_SUPER, sb = tri_index(SI, SJ);
+    if (sb < s0 || sb >= s1) return -1;
+    const int64_t ta = I - SI * KP_SUPER, tb = J - SJ * KP_SUPER;
+    const int64_t local = SI == SJ ? ta * (ta + 1) / 2 + tb : ta * min<int64_t>(KP_SUPER, nb - SJ * KP_SUPER) + tb;
+    return (int64_t) wg_off[sb - s0] + local;
+}
+
+// value of column block c for row i (block Ib): tile (Ib, c)'s row sums when c <= Ib, tile (c, Ib)'s column
+// sums when c > Ib; 0 for a tile of another rank
 template <typename T>
-__global__ __launch_bounds__(256) void kp_reduce_kernel(const T *__restrict__ partial, int64_t nb, int64_t n_pad,
-                                                        int64_t m, int64_t s0, int64_t s1, int64_t s_total,
-                                                        T *__restrict__ raw,
+__device__ __forceinline__ T kp_slab_value(const T *__restrict__ partial, int64_t Ib, int64_t q, int64_t c, int64_t nb,
+                                           int64_t s0, int64_t s1, const int32_t *__restrict__ wg_off) {
+    const int64_t rec = c <= Ib ? kp_tile_record(Ib, c, nb, s0, s1, wg_off) : kp_tile_record(c, Ib, nb, s0, s1, wg_off);
+    return rec < 0 ? T(0) : partial[rec * KP_REC + (c <= Ib ? 0 : KP_TILE) + q];
+}
+
+// raw[i] = sum over the column blocks c = 0 .. nb-1 of the slab values of row i (kp_slab_value), in c order:
+// the whole triangle on one rank. 8 records in flight per step (one thread per i: memory parallelism sets the
+// speed); a row's 64-lane group reads 64 consecutive values of each record
+template <typename T>
+__global__ __launch_bounds__(256) void kp_reduce_kernel(const T *__restrict__ partial, int64_t nb, int64_t m,
+                                                        const int32_t *__restrict__ wg_off, T *__restrict__ raw,
                                                         const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
+    const int64_t Ib = i / KP_TILE, q = i % KP_TILE, s_all = INT64_MAX;
     T s = 0;
-    if (s0 == 0 && s1 == s_total) {
-        // 8 slab rows in flight per step (one thread per i: memory parallelism sets the speed)
-        int64_t c = 0;
-        for (; c + 8 <= nb; c += 8) {
-            T v[8];
+    int64_t c = 0;
+    for (; c + 8 <= nb; c += 8) {
+        T v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = partial[(c + u) * n_pad + i];
+        for (int u = 0; u < 8; ++u) v[u] = kp_slab_value(partial, Ib, q, c + u, nb, 0, s_all, wg_off);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s += v[u];
-        }
-        for (; c < nb; ++c) s += partial[c * n_pad + i];
-    } else {  // one rank's share: only the slab rows of its super-blocks (same c order as above)
-        const int64_t RS = (i / KP_TILE) / KP_SUPER;
-        const int64_t ns = (nb + KP_SUPER - 1) / KP_SUPER;
-        for (int64_t CS = 0; CS < ns; ++CS) {
-            const int64_t sb = (RS >= CS) ? tri_index(RS, CS) : tri_index(CS, RS);
-            if (sb < s0 || sb >= s1) continue;
-            const int64_t c0 = CS * KP_SUPER, c1 = min(nb, c0 + KP_SUPER);
-            if (c1 - c0 == KP_SUPER) {
-                T v[KP_SUPER];
-#pragma unroll
-                for (int u = 0; u < KP_SUPER; ++u) v[u] = partial[(c0 + u) * n_pad + i];
-#pragma unroll
-                for (int u = 0; u < KP_SUPER; ++u) s += v[u];
-            } else {
-                for (int64_t c = c0; c < c1; ++c) s += partial[c * n_pad + i];
-            }
-        }
+        for (int u = 0; u < 8; ++u) s += v[u];
     }
+    for (; c < nb; ++c) s += kp_slab_value(partial, Ib, q, c, nb, 0, s_all, wg_off);
     raw[i] = s;
 }
 
-// one rank's share (s0, s1 not the whole triangle): raw[i] = sum of the slab rows of the rank's own
-// super-blocks. A rank owning the bottom rows of the triangle sees up to nb slab rows per row i, so the
+// one rank's share (s0, s1 not the whole triangle): raw[i] = sum of the slab values of the rank's own
+// super-blocks. A rank owning the bottom rows of the triangle sees up to nb records per row i, so the
 // column super-blocks are split over the 16 waves of a block (64 rows per block, lanes = rows: coalesced)
 // and the 16 partial sums are added in wave order: a fixed order, deterministic; the critical path per
 // thread is 1/16 of the row (one thread per row made the last rank of 8 4 % slower than the others)
 constexpr int KP_RED_G = 16;
 template <typename T>
 __global__ __launch_bounds__(64 * KP_RED_G) void kp_reduce_share_kernel(const T *__restrict__ partial, int64_t nb,
-                                                                        int64_t n_pad, int64_t m, int64_t s0,
-                                                                        int64_t s1, T *__restrict__ raw,
+                                                                        int64_t m, int64_t s0, int64_t s1,
+                                                                        const int32_t *__restrict__ wg_off,
+                                                                        T *__restrict__ raw,
                                                                         const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
     __shared__ T red[KP_RED_G][64];
@@ -431,7 +436,7 @@ __global__ __launch_bounds__(64 * KP_RED_G) void kp_reduce_share_kernel(const T 
     const int64_t ns = (nb + KP_SUPER - 1) / KP_SUPER;
     T s = 0;
     if (i < m) {
-        const int64_t RS = (i / KP_TILE) / KP_SUPER;
+        const int64_t Ib = i / KP_TILE, q = i % KP_TILE, RS = Ib / KP_SUPER;
         const int64_t cs0 = g * ns / KP_RED_G, cs1 = (g + 1) * ns / KP_RED_G;
         for (int64_t CS = cs0; CS < cs1; ++CS) {
             const int64_t sb = (RS >= CS) ? tri_index(RS, CS) : tri_index(CS, RS);
@@ -440,11 +445,11 @@ __global__ __launch_bounds__(64 * KP_RED_G) void kp_reduce_share_kernel(const T 
             if (c1 - c0 == KP_SUPER) {
                 T v[KP_SUPER];
 #pragma unroll
-                for (int u = 0; u < KP_SUPER; ++u) v[u] = partial[(c0 + u) * n_pad + i];
+                for (int u = 0; u < KP_SUPER; ++u) v[u] = kp_slab_value(partial, Ib, q, c0 + u, nb, s0, s1, wg_off);
 #pragma unroll
                 for (int u = 0; u < KP_SUPER; ++u) s += v[u];
             } else {
-                for (int64_t c = c0; c < c1; ++c) s += partial[c * n_pad + i];
+                for (int64_t c = c0; c < c1; ++c) s += kp_slab_value(partial, Ib, q, c, nb, s0, s1, wg_off);
             }
         }
     }
@@ -487,16 +492,16 @@ void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *par
 }
 
 template <typename T>
-void launch_kp_reduce(const T *partial, int64_t nb, int64_t n_pad, int64_t m, int64_t s0, int64_t s1, T *raw,
+void launch_kp_reduce(const T *partial, int64_t nb, int64_t m, int64_t s0, int64_t s1, const int32_t *wg_off, T *raw,
                       const cg_scalars<T> *status, hipStream_t s) {
     if (m <= 0) return;
     const int64_t ns = ceil_div(nb, KP_SUPER);
     if (s0 == 0 && s1 == ns * (ns + 1) / 2) {
-        hipLaunchKernelGGL(kp_reduce_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, partial, nb, n_pad,
-                           m, s0, s1, ns * (ns + 1) / 2, raw, status);
+        hipLaunchKernelGGL(kp_reduce_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, partial, nb, m,
+                           wg_off, raw, status);
     } else {
         hipLaunchKernelGGL(kp_reduce_share_kernel<T>, dim3((unsigned) ceil_div(m, 64)), dim3(64 * KP_RED_G), 0, s,
-                           partial, nb, n_pad, m, s0, s1, raw, status);
+                           partial, nb, m, s0, s1, wg_off, raw, status);
     }
     MI_LAUNCH_CHECK();
 }
@@ -505,7 +510,7 @@ void launch_kp_reduce(const T *partial, int64_t nb, int64_t n_pad, int64_t m, in
     template void launch_kp_tiles<T>(kfun<T>, const T *, const T *, const T *, T *, int64_t, int64_t, int64_t, \
                                      int64_t, int64_t, const int32_t *, int64_t, const cg_scalars<T> *,        \
                                      hipStream_t);                                                              \
-    template void launch_kp_reduce<T>(const T *, int64_t, int64_t, int64_t, int64_t, int64_t, T *,             \
+    template void launch_kp_reduce<T>(const T *, int64_t, int64_t, int64_t, int64_t, const int32_t *, T *,     \
                                       const cg_scalars<T> *, hipStream_t);
 INST(float)
 INST(double)

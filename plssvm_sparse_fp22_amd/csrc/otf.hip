@@ -384,8 +384,9 @@ void engine<T>::otf_dominant(const T *p, const cg_scalars<T> *status) {
 template <typename T>
 void engine<T>::otf_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base) {
     MI_HIP_CHECK(hipMemsetAsync(raw.get(), 0, sizeof(T) * (size_t) m, stream));
+    gather_input(p);  // sharded group: the partners' p from every rank
     otf_dominant(p, status);
-    allgather_rows(raw.get());
+    if (!shard) allgather_rows(raw.get());
     if (with_base && !(sim_world > 0 && sim_rank != 0)) {
         launch_dot2<T>(p, kernel == 2 ? csr.e.get() : nullptr, nullptr, nullptr, m, red.get(), status, stream);
         launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);

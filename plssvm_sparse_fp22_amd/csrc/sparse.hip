@@ -609,7 +609,9 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     csr.val.alloc(std::max<int64_t>(nnz, 1), stream);
     if (nnz && val_fmt == PLSSVM_MI_VAL_FP22) {
         std::vector<T> dec((size_t) nnz);
-        for (int64_t k = 0; k < nnz; ++k) dec[(size_t) k] = hval(k);
+        host_parallel(nnz, [&](int, int64_t k0, int64_t k1) {
+            for (int64_t k = k0; k < k1; ++k) dec[(size_t) k] = hval(k);
+        });
         MI_HIP_CHECK(hipMemcpyAsync(csr.val.get(), dec.data(), sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice, stream));
         MI_HIP_CHECK(hipStreamSynchronize(stream));
     } else if (nnz) {
@@ -624,66 +626,101 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     finish_setup();  // row split r0, r1
     pt.mark("setup_csr: check + upload + norms");
 
-    if (factored()) {
-        // factored linear (DESIGN.md §3.3): w = X_rows^T p over rows [csc_r0, csc_r1) — all rows for
-        // a single or simulated rank, this rank's rows in a real group (w is then all-reduced) — and
-        // raw[r0, r1) = X w, both as panelled SELL-64 SpMVs (spmv.hpp)
-        const bool local = world > 1 && sim_world == 0;
-        csr.csc_r0 = local ? r0 : 0;
-        csr.csc_r1 = local ? r1 : m;
-        const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
-        const int64_t blocks = sell_target_blocks();
-        build_spmv_plan<T>(
-            csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22,
-            [&](auto emit) {
-                for (int64_t i = csr.csc_r0; i < csr.csc_r1; ++i)
-                    for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit((int64_t) col[k], i - csr.csc_r0, (double) hval(k));
-            },
-            blocks, stream);
-        build_spmv_plan<T>(
-            csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22,
-            [&](auto emit) {
-                for (int64_t i = r0; i < r1; ++i)
-                    for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit(i - r0, (int64_t) col[k], (double) hval(k));
-            },
-            blocks, stream);
-        if (world == 1 && sim_world == 0 && rowblock_fused_enabled())  // CG iterations: CSR pass + finalize in one launch
-            build_rowblock_plan<T>(
-                csr.rb_csr, m, d, f22,
-                [&](auto emit) {
-                    for (int64_t i = 0; i < m; ++i)
-                        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit(i, (int64_t) col[k], (double) hval(k));
-                },
-                blocks, stream);
-        return;
-    }
-
     // CSC of rows 0..m-1 for the Gram pattern (counting sort: rows ascending inside each column) and,
     // per CSR entry, its CSC position (the column join needs "rows < i in this column" = cpos - colptr)
-    csr.csc_r0 = 0;
-    csr.csc_r1 = m;
+    // (a counting sort on the host threads: thread t owns a contiguous row range, so its entries of a column
+    // follow thread t - 1's — the same CSC as the sequential sort)
     std::vector<int64_t> colptr(d + 1, 0), cpos(std::max<int64_t>(nnz, 1));
-    for (int64_t k = 0; k < nnz; ++k) ++colptr[col[k] + 1];
-    for (int64_t f = 0; f < d; ++f) colptr[f + 1] += colptr[f];
-    std::vector<int64_t> fill(colptr.begin(), colptr.end() - 1);
     std::vector<int32_t> crow(std::max<int64_t>(nnz, 1));
     // values in CSC order, decoded (FP22 input included: the Gram build multiplies them once at setup,
     // the K·p stream holds the products s_ij, so FP22 changes only the input format)
     std::vector<T> cval_real(std::max<int64_t>(nnz, 1));
     double amax = 0.0, nmax = 0.0;  // max x^2 and max |x_i|^2 (kernel expansion eligibility)
-    for (int64_t i = 0; i < m; ++i) {
-        double nrm = 0.0;
-        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-            const int64_t t = fill[col[k]]++;
-            crow[t] = (int32_t) i;
-            cpos[k] = t;
-            cval_real[t] = hval(k);
-            const double x = (double) cval_real[t];
-            amax = std::max(amax, x * x);
-            nrm += x * x;
+    {
+        const int NT = (int) std::max<int64_t>(1, std::min<int64_t>(host_threads(), nnz / 65536 + 1));
+        std::vector<int64_t> rb(NT + 1, 0);  // row ranges balanced by entries
+        for (int t = 1; t < NT; ++t)
+            rb[t] = std::upper_bound(rowptr, rowptr + m + 1, (nnz * t) / NT) - rowptr - 1;
+        rb[NT] = m;
+        for (int t = 1; t <= NT; ++t) rb[t] = std::max(rb[t], rb[t - 1]);
+        std::vector<std::vector<int64_t>> cnt((size_t) NT);
+        std::vector<double> amax_t(NT, 0.0), nmax_t(NT, 0.0);
+        host_parallel(NT, [&](int, int64_t t0, int64_t t1) {
+            for (int64_t t = t0; t < t1; ++t) {
+                auto &c = cnt[(size_t) t];
+                c.assign((size_t) d, 0);
+                for (int64_t k = rowptr[rb[t]]; k < rowptr[rb[t + 1]]; ++k) ++c[(size_t) col[k]];
+            }
+        }, NT);
+        for (int64_t f = 0; f < d; ++f) {  // colptr and each thread's first slot per column
+            int64_t a = colptr[f];
+            for (int t = 0; t < NT; ++t) {
+                const int64_t v = cnt[(size_t) t][(size_t) f];
+                cnt[(size_t) t][(size_t) f] = a;
+                a += v;
+            }
+            colptr[f + 1] = a;
         }
-        nmax = std::max(nmax, nrm);
+        host_parallel(NT, [&](int, int64_t t0, int64_t t1) {
+            for (int64_t t = t0; t < t1; ++t) {
+                auto &fill = cnt[(size_t) t];
+                double am = 0.0, nm = 0.0;
+                for (int64_t i = rb[t]; i < rb[t + 1]; ++i) {
+                    double nrm = 0.0;
+                    for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+                        const int64_t q = fill[(size_t) col[k]]++;
+                        crow[q] = (int32_t) i;
+                        cpos[k] = q;
+                        cval_real[q] = hval(k);
+                        const double x = (double) cval_real[q];
+                        am = std::max(am, x * x);
+                        nrm += x * x;
+                    }
+                    nm = std::max(nm, nrm);
+                }
+                amax_t[(size_t) t] = am;
+                nmax_t[(size_t) t] = nm;
+            }
+        }, NT);
+        for (int t = 0; t < NT; ++t) amax = std::max(amax, amax_t[(size_t) t]), nmax = std::max(nmax, nmax_t[(size_t) t]);
     }
+    // CSC segments of rows [c0, c1) (rows ascending in each column: a contiguous part of the column)
+    auto csc_gen = [&](int64_t c0, int64_t c1) {
+        return [&, c0, c1](auto emit, int64_t f0, int64_t f1) {
+            for (int64_t f = f0; f < f1; ++f) {
+                const int32_t *b0 = crow.data() + colptr[f], *b1 = crow.data() + colptr[f + 1];
+                const int32_t *lo = c0 > 0 ? std::lower_bound(b0, b1, (int32_t) c0) : b0;
+                const int32_t *hi = c1 < m ? std::lower_bound(lo, b1, (int32_t) c1) : b1;
+                for (const int32_t *t = lo; t < hi; ++t) emit(f, (int64_t) *t - c0, (double) cval_real[(size_t) (t - crow.data())]);
+            }
+        };
+    };
+    // CSR segments = rows [base + s0, base + s1)
+    auto csr_gen = [&](int64_t base) {
+        return [&, base](auto emit, int64_t s0, int64_t s1) {
+            for (int64_t s = s0; s < s1; ++s)
+                for (int64_t k = rowptr[base + s]; k < rowptr[base + s + 1]; ++k) emit(s, (int64_t) col[k], (double) hval(k));
+        };
+    };
+    if (factored()) {
+        // factored linear (DESIGN.md §3.3): w = X_rows^T p over rows [csc_r0, csc_r1) — all rows for
+        // a single or simulated rank, this rank's rows in a real group (w is then all-reduced) — and
+        // raw[r0, r1) = X w, both as panelled SELL-64 SpMVs (spmv.hpp)
+        const bool local = (world > 1 && sim_world == 0) || (sim_world > 0 && shard);
+        csr.csc_r0 = local ? r0 : 0;
+        csr.csc_r1 = local ? r1 : m;
+        const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
+        const int64_t blocks = sell_target_blocks();
+        build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22,
+                           csc_gen(csr.csc_r0, csr.csc_r1), blocks, stream);
+        build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks, stream);
+        if (world == 1 && sim_world == 0 && rowblock_fused_enabled())  // CG iterations: CSR pass + finalize in one launch
+            build_rowblock_plan<T>(csr.rb_csr, m, d, f22, csr_gen(0), blocks, stream);
+        pt.mark("setup_csr: SELL plans");
+        return;
+    }
+    csr.csc_r0 = 0;
+    csr.csc_r1 = m;
     csr.colptr.alloc(d + 1, stream);
     MI_HIP_CHECK(hipMemcpyAsync(csr.colptr.get(), colptr.data(), sizeof(int64_t) * (size_t) (d + 1),
                                 hipMemcpyHostToDevice, stream));
@@ -702,8 +739,14 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         // Gram pattern: row blocks owned by this rank, balanced by column-join incidences
         const int64_t nRB = ceil_div(std::max<int64_t>(m, 1), GRAM_RB);
         std::vector<int64_t> inc_rb(nRB, 0);
-        for (int64_t i = 0; i < m; ++i)
-            for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) inc_rb[i / GRAM_RB] += cpos[k] - colptr[col[k]];
+        host_parallel(nRB, [&](int, int64_t I0, int64_t I1) {
+            for (int64_t I = I0; I < I1; ++I) {
+                int64_t a = 0;
+                for (int64_t k = rowptr[I * GRAM_RB]; k < rowptr[std::min<int64_t>(m, (I + 1) * GRAM_RB)]; ++k)
+                    a += cpos[k] - colptr[col[k]];
+                inc_rb[(size_t) I] = a;
+            }
+        });
         const int eff_world = sim_world > 0 ? sim_world : world, eff_rank = sim_world > 0 ? sim_rank : rank;
         std::vector<int64_t> cum(nRB + 1, 0);
         for (int64_t I = 0; I < nRB; ++I) cum[I + 1] = cum[I] + inc_rb[I];
@@ -782,24 +825,13 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                     // or of all rows, the Horner pass over this rank's CSR rows
                     const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
                     const int64_t blocks = sell_target_blocks();
-                    const bool local = world > 1 && sim_world == 0;
+                    const bool local = (world > 1 && sim_world == 0) || (sim_world > 0 && shard);
                     csr.csc_r0 = local ? r0 : 0;
                     csr.csc_r1 = local ? r1 : m;
-                    build_spmv_plan<T>(
-                        csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22,
-                        [&](auto emit) {
-                            for (int64_t i = csr.csc_r0; i < csr.csc_r1; ++i)
-                                for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k)
-                                    emit((int64_t) col[k], i - csr.csc_r0, (double) hval(k));
-                        },
-                        blocks, stream, 0, 1, csr.ex.KM);
-                    build_spmv_plan<T>(
-                        csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22,
-                        [&](auto emit) {
-                            for (int64_t i = r0; i < r1; ++i)
-                                for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) emit(i - r0, (int64_t) col[k], (double) hval(k));
-                        },
-                        blocks, stream, 0, csr.ex.KM, 1);
+                    build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0],
+                                       f22, csc_gen(csr.csc_r0, csr.csc_r1), blocks, stream, 0, 1, csr.ex.KM);
+                    build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks, stream,
+                                       0, csr.ex.KM, 1);
                     pt.mark("setup_csr: SELL plans");
                     build_expansion(cpos_d.get(), max_inc);
                     pt.mark("setup_csr: expansion");
@@ -959,7 +991,7 @@ __global__ __launch_bounds__(256) void csr_densify_kernel(const int64_t *__restr
 template <typename T>
 void engine<T>::setup_sparse_dense() {
     const int64_t dp = round_up(std::max<int64_t>(d, 1), kp_dpad<T>());
-    const int64_t need = (dp * n_pad + std::max<int64_t>(nb, 1) * n_pad) * (int64_t) sizeof(T);
+    const int64_t need = (dp * n_pad + std::max<int64_t>(kp_wgs, 1) * KP_REC) * (int64_t) sizeof(T);
     size_t free_b = 0, total_b = 0;
     MI_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     if ((double) need > 0.95 * (double) free_b)
@@ -969,7 +1001,7 @@ void engine<T>::setup_sparse_dense() {
                                " MiB free: use more GPUs or a smaller data set");
     d_pad = dp;
     XT.alloc(d_pad * n_pad, stream);
-    partial.alloc(std::max<int64_t>(nb, 1) * n_pad, stream, false);
+    partial.alloc(std::max<int64_t>(kp_wgs, 1) * KP_REC, stream, false);
     if (m > 0)
         hipLaunchKernelGGL(csr_densify_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream,
                            csr.rowptr.get(), csr.col.get(), csr.val.get(), m, n_pad, XT.get());
@@ -1166,7 +1198,7 @@ void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status, bool with
         spmv_pass_csc(p, status);
         allreduce(w.get(), d);
         spmv_pass_csr(status);
-        allgather_rows(raw.get());
+        if (!shard) allgather_rows(raw.get());
         return;
     }
     if (csr.otf_on) {
@@ -1178,13 +1210,15 @@ void engine<T>::sparse_kp_raw(const T *p, const cg_scalars<T> *status, bool with
         return;
     }
     // separable sum: sum(e p) (rbf) or sum(p) (poly)
+    gather_input(p);
     launch_dot2<T>(p, kernel == 2 ? csr.e.get() : nullptr, nullptr, nullptr, m, red.get(), status, stream);
     launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
     sparse_dominant(p, status);
     hipLaunchKernelGGL(gram_reduce_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream,
                        csr.slab_row.get(), csr.slab_col.get(), m, csr.m_pad, csr.rb0, csr.rb1, raw.get(), status);
     MI_LAUNCH_CHECK();
-    allreduce(raw.get(), m);
+    if (shard) reduce_scatter_rows(raw.get());
+    else allreduce(raw.get(), m);
     if (with_base && !(sim_world > 0 && sim_rank != 0)) {
         T kappa = 0;
         if (kernel == 1) {

@@ -359,8 +359,27 @@ inline void launch_panel_spmv(const spmv_plan<T> &pl, const T *x, int64_t xn, T 
     }
 }
 
-// Host construction. gen(emit) must call emit(s, global_index, value) for every entry, the entries
-// of one segment in their summation order (for each panel). xn = length of the gathered vector.
+// packed FP22 words of v (16 values per 11 words, fp22_words(n) + 1 words), groups on the host threads
+inline std::vector<uint32_t> fp22_pack_host(const std::vector<float> &v) {
+    const int64_t n = (int64_t) v.size(), groups = (n + 15) / 16;
+    std::vector<uint32_t> words((size_t) (fp22_words(n) + 1), 0u);
+    host_parallel(groups, [&](int, int64_t g0, int64_t g1) {
+        for (int64_t g = g0; g < g1; ++g)
+            for (int k = 0; k < 16 && g * 16 + k < n; ++k) {
+                const uint64_t code = fp22_encode_host(v[(size_t) (g * 16 + k)]);
+                const int bit = 22 * k;
+                const int64_t wi = g * 11 + (bit >> 5);
+                const int sh = bit & 31;
+                words[(size_t) wi] |= (uint32_t) (code << sh);
+                if (sh > 10) words[(size_t) wi + 1] |= (uint32_t) (code >> (32 - sh));
+            }
+    });
+    return words;
+}
+
+// Host construction. gen(emit, s0, s1) must call emit(s, global_index, value) for every entry of the
+// segments s in [s0, s1), the entries of one segment in their summation order (for each panel); it is
+// called from several host threads on disjoint segment ranges. xn = length of the gathered vector.
 // target_blocks: workgroups per pass (each loads its panel of x once). force_mode: 0 auto,
 // 1 LDS panels, 2 one panel gathered from global memory.
 // xch: channels of the gathered vector (mode 2 passes: the LDS panel holds sell_width / xch indices);
@@ -381,27 +400,34 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
     pl.P = ldsx ? P_lds : 1;
     pl.W = ldsx ? Wmax : std::max<int64_t>(xn, 1);
     const int64_t P = pl.P, W = pl.W;
-    // segment lengths per panel
+    // segment lengths per panel (segment ranges on the host threads: each length has one writer)
     std::vector<int32_t> len((size_t) (P * nseg), 0);
-    gen([&](int64_t s, int64_t g, double) { ++len[(size_t) ((g / W) * nseg + s)]; });
+    host_parallel(nseg, [&](int, int64_t s0, int64_t s1) {
+        gen([&](int64_t s, int64_t g, double) { ++len[(size_t) ((g / W) * nseg + s)]; }, s0, s1);
+    });
     // per panel: sort windows by length (descending, stable), deal 64 slots per chunk
     const int64_t slots_per_panel = round_up(nseg, 64);
     const int64_t nch_per_panel = slots_per_panel / 64;
     std::vector<sell_chunk> chunks((size_t) (P * nch_per_panel));
     std::vector<int32_t> perm((size_t) (P * slots_per_panel), -1);
     std::vector<int64_t> pos((size_t) (P * nseg));  // next storage position of segment (q, s)
-    std::vector<int32_t> order;
-    int64_t off = 0;
-    for (int64_t q = 0; q < P; ++q) {
-        const int32_t *lq = len.data() + q * nseg;
-        for (int64_t w0 = 0; w0 < nseg; w0 += SELL_SIGMA) {
+    const int64_t nwin = ceil_div(nseg, (int64_t) SELL_SIGMA);
+    host_parallel(P * nwin, [&](int, int64_t a, int64_t b) {
+        std::vector<int32_t> order;
+        for (int64_t task = a; task < b; ++task) {
+            const int64_t q = task / nwin, w0 = (task % nwin) * SELL_SIGMA;
+            const int32_t *lq = len.data() + q * nseg;
             const int64_t w1 = std::min(nseg, w0 + (int64_t) SELL_SIGMA);
             order.resize((size_t) (w1 - w0));
             std::iota(order.begin(), order.end(), (int32_t) w0);
-            std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return lq[a] > lq[b]; });
+            std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return lq[x] > lq[y]; });
             // the slots of this window are [w0, w1) (SELL_SIGMA is a multiple of 64)
             for (int64_t k = 0; k < (int64_t) order.size(); ++k) perm[(size_t) (q * slots_per_panel + w0 + k)] = order[k];
         }
+    });
+    int64_t off = 0;
+    for (int64_t q = 0; q < P; ++q) {
+        const int32_t *lq = len.data() + q * nseg;
         for (int64_t c = 0; c < nch_per_panel; ++c) {
             int32_t width = 0;
             for (int l = 0; l < 64; ++l) {
@@ -421,37 +447,33 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
     pl.nchunks = (int64_t) chunks.size();
     pl.nchp = nch_per_panel;
     pl.slots_total = P * slots_per_panel;
-    // fill (zero padding: index 0, value 0 contributes exactly 0) plus a 64-entry zero tail
+    // fill (zero padding: index 0, value 0 contributes exactly 0) plus a 64-entry zero tail; segment ranges
+    // on the host threads (disjoint slots; FP22 words hold several segments' values, so they are packed
+    // afterwards from a float copy, 16-value groups per thread)
     const int64_t cap = off + 64;
     std::vector<uint16_t> i16(ldsx ? cap : 0, 0);
     std::vector<int32_t> i32(ldsx ? 0 : cap, 0);
     std::vector<T> vr(fp22 ? 0 : cap, T(0));
-    std::vector<uint32_t> v22(fp22 ? fp22_words(cap) + 1 : 0, 0u);
-    gen([&](int64_t s, int64_t g, double v) {
-        const int64_t q = g / W;
-        int64_t &p = pos[(size_t) (q * nseg + s)];
-        const int64_t t = p;
-        p += 64;
-        if (ldsx) {
-            // IDX2: entry j of slot l (value position t = off + 64 j + l) keeps its index at
-            // off + 128 (j >> 1) + 2 l + (j & 1)
-            const int64_t ti = SELL_IDX2 ? sell_pair_pos(t) : t;
-            i16[ti] = (uint16_t) (g - q * W);
-        }
-        else i32[t] = (int32_t) g;
-        const int64_t tv = (SELL_VAL2 && ldsx) ? sell_pair_pos(t) : t;  // value position
-        if (fp22) {
-            const uint64_t code = fp22_encode_host((float) v);
-            const int64_t gg = tv >> 4;
-            const int bit = 22 * (int) (tv & 15);
-            const int64_t wi = gg * 11 + (bit >> 5);
-            const int sh = bit & 31;
-            v22[wi] |= (uint32_t) (code << sh);
-            if (sh > 10) v22[wi + 1] |= (uint32_t) (code >> (32 - sh));
-        } else {
-            vr[tv] = (T) v;
-        }
+    std::vector<float> vf(fp22 ? cap : 0, 0.0f);
+    host_parallel(nseg, [&](int, int64_t s0, int64_t s1) {
+        gen([&](int64_t s, int64_t g, double v) {
+            const int64_t q = g / W;
+            int64_t &p = pos[(size_t) (q * nseg + s)];
+            const int64_t t = p;
+            p += 64;
+            if (ldsx) {
+                // IDX2: entry j of slot l (value position t = off + 64 j + l) keeps its index at
+                // off + 128 (j >> 1) + 2 l + (j & 1)
+                const int64_t ti = SELL_IDX2 ? sell_pair_pos(t) : t;
+                i16[ti] = (uint16_t) (g - q * W);
+            }
+            else i32[t] = (int32_t) g;
+            const int64_t tv = (SELL_VAL2 && ldsx) ? sell_pair_pos(t) : t;  // value position
+            if (fp22) vf[tv] = (float) v;
+            else vr[tv] = (T) v;
+        }, s0, s1);
     });
+    const std::vector<uint32_t> v22 = fp22 ? fp22_pack_host(vf) : std::vector<uint32_t>{};
     // blocks: target_blocks contiguous chunk ranges of equal cost (entries + a per-chunk charge for its
     // descriptor, slot map and output) over the panel-major chunk sequence; a range may cross panels
     constexpr int64_t CHUNK_COST = 8 * 64;
@@ -675,21 +697,33 @@ bool build_rowblock_plan(rb_plan<T> &pl, int64_t nrows, int64_t xn, bool fp22, G
     if (nblk > RED_BLOCKS) return false;
     pl.P = P, pl.W = W, pl.RBK = RBK, pl.nblk = nblk, pl.nrows = nrows;
     std::vector<int32_t> len((size_t) (P * nrows), 0);
-    gen([&](int64_t s, int64_t g, double) { ++len[(size_t) ((g / W) * nrows + s)]; });
+    host_parallel(nrows, [&](int, int64_t s0, int64_t s1) {
+        gen([&](int64_t s, int64_t g, double) { ++len[(size_t) ((g / W) * nrows + s)]; }, s0, s1);
+    });
     const int64_t cpb = RBK / 64;  // chunks per (block, panel)
     std::vector<sell_chunk> chunks((size_t) (nblk * P * cpb));
     std::vector<int32_t> perm(chunks.size() * 64, -1);
     std::vector<int64_t> pos((size_t) (P * nrows));
     std::vector<int32_t> bpc{ 0 };
-    std::vector<int32_t> order;
-    int64_t off = 0, c = 0;
-    for (int64_t b = 0; b < nblk; ++b) {
-        const int64_t r0 = b * RBK, r1 = std::min(nrows, r0 + RBK);
-        for (int64_t qq = 0; qq < P; ++qq) {
+    // each (block, panel)'s rows sorted by their panel length (descending, stable), on the host threads
+    std::vector<std::vector<int32_t>> orders((size_t) (nblk * P));
+    host_parallel(nblk * P, [&](int, int64_t a, int64_t b) {
+        for (int64_t task = a; task < b; ++task) {
+            const int64_t blk = task / P, qq = task % P;
+            const int64_t r0 = blk * RBK, r1 = std::min(nrows, r0 + RBK);
             const int32_t *lq = len.data() + qq * nrows;
+            auto &order = orders[(size_t) task];
             order.resize((size_t) (r1 - r0));
             std::iota(order.begin(), order.end(), (int32_t) r0);
-            std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b2) { return lq[a] > lq[b2]; });
+            std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return lq[x] > lq[y]; });
+        }
+    });
+    int64_t off = 0, c = 0;
+    for (int64_t b = 0; b < nblk; ++b) {
+        const int64_t r0 = b * RBK;
+        for (int64_t qq = 0; qq < P; ++qq) {
+            const int32_t *lq = len.data() + qq * nrows;
+            const auto &order = orders[(size_t) (b * P + qq)];
             for (int64_t k = 0; k < cpb; ++k, ++c) {
                 int32_t width = 0;
                 for (int l = 0; l < 64; ++l) {
@@ -715,25 +749,19 @@ bool build_rowblock_plan(rb_plan<T> &pl, int64_t nrows, int64_t xn, bool fp22, G
     const int64_t cap = off + 128;
     std::vector<uint16_t> i16((size_t) cap, 0);
     std::vector<T> vr(fp22 ? 0 : (size_t) cap, T(0));
-    std::vector<uint32_t> v22(fp22 ? fp22_words(cap) + 1 : 0, 0u);
-    gen([&](int64_t s, int64_t g, double v) {
-        const int64_t qq = g / W;
-        int64_t &p = pos[(size_t) (qq * nrows + s)];
-        const int64_t t = p;
-        p += 64;
-        i16[(size_t) sell_pair_pos(t)] = (uint16_t) (g - qq * W);
-        if (fp22) {
-            const uint64_t code = fp22_encode_host((float) v);
-            const int64_t gg = t >> 4;
-            const int bit = 22 * (int) (t & 15);
-            const int64_t wi = gg * 11 + (bit >> 5);
-            const int sh = bit & 31;
-            v22[(size_t) wi] |= (uint32_t) (code << sh);
-            if (sh > 10) v22[(size_t) wi + 1] |= (uint32_t) (code >> (32 - sh));
-        } else {
-            vr[(size_t) t] = (T) v;
-        }
+    std::vector<float> vf(fp22 ? (size_t) cap : 0, 0.0f);
+    host_parallel(nrows, [&](int, int64_t s0, int64_t s1) {
+        gen([&](int64_t s, int64_t g, double v) {
+            const int64_t qq = g / W;
+            int64_t &p = pos[(size_t) (qq * nrows + s)];
+            const int64_t t = p;
+            p += 64;
+            i16[(size_t) sell_pair_pos(t)] = (uint16_t) (g - qq * W);
+            if (fp22) vf[(size_t) t] = (float) v;
+            else vr[(size_t) t] = (T) v;
+        }, s0, s1);
     });
+    const std::vector<uint32_t> v22 = fp22 ? fp22_pack_host(vf) : std::vector<uint32_t>{};
     auto up = [&](auto &buf, const auto &vec) {
         using E = typename std::decay_t<decltype(vec)>::value_type;
         if (vec.empty()) return;

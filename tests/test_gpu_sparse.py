@@ -438,3 +438,34 @@ def test_coo_rejects_duplicates_and_bad_indices():
     p.coo = (np.array([0, 5], np.int64), np.array([1, 1], np.int32), np.ones(2), 3, 4)
     with pm.CSVM(p) as svm, pytest.raises(pm.BackendError, match="row index out of range"):
         svm.setup_data_on_device()
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("kernel,shape,sim", [("rbf", (20000, 3000, 20), None), ("polynomial", (6000, 800, 30), None),
+                                              ("rbf", (20000, 3000, 20), (1, 3)), ("rbf", (3000, 50, 20), None)])
+def test_expansion_row_join_equals_sort_join(kernel, shape, sim, dtype, monkeypatch):
+    """The remainder's symmetric rows built per row (the default row join: LDS bitmap of the rows met in
+    the row's feature columns, H from a merge of the two rows) against the column-join sort
+    (PLSSVM_MI_EXP_JOIN=sort: every incidence generated, radix-sorted, reduced by key): the same pairs
+    (info.pairs) and the same K·p overlap sums — both sum a pair's per-feature products in ascending
+    feature order in fp64, so H agrees to the last bit of fp64 before the rounding to the real type.
+    (3000 x 50 @ 40 %: dense-ish rows whose repeats overflow a pass, so passes are split.)"""
+    n, d, k = shape
+    csr, _ = datagen.sparse_csr(n, d, k, seed=17, dtype=np.float64)
+    m = n - 1
+    x = np.random.default_rng(3).uniform(1, 2, m).astype(dtype)
+    out = {}
+    for join in ("row", "sort"):
+        if join == "sort":
+            monkeypatch.setenv("PLSSVM_MI_EXP_JOIN", "sort")
+        else:
+            monkeypatch.delenv("PLSSVM_MI_EXP_JOIN", raising=False)
+        with sparse_svm(csr, kernel, dtype, sim=sim, algo="expansion") as svm:
+            svm.setup_data_on_device()
+            info = svm.info()
+            assert info["sparse_algo"] == pm._abi.SPARSE_EXPANSION
+            out[join] = (svm.kp_part(x, "overlap"), info["pairs"], info["pair_slots"])
+    assert out["row"][1] == out["sort"][1] and out["row"][2] == out["sort"][2]
+    a, b = out["row"][0].astype(np.float64), out["sort"][0].astype(np.float64)
+    tol = 1e-14 if dtype == np.float64 else 1e-6
+    assert np.abs(a - b).max() <= tol * max(np.abs(b).max(), 1e-300), np.abs(a - b).max()

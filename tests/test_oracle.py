@@ -177,3 +177,18 @@ def test_product_fp22_codec_matches_oracle(oracle):
     assert np.array_equal(fp22.pack(v), oracle.fp22_pack(v))
     assert np.array_equal(fp22.unpack(fp22.pack(v), v.size), oracle.fp22_unpack(oracle.fp22_pack(v), v.size))
     assert np.isnan(fp22.unpack(fp22.pack(np.float32([np.nan])), 1)[0])
+
+
+def test_factored_csr_baseline_equals_the_pairwise_oracle(oracle):
+    """The CPU baseline's O(nnz) factored linear K·p (bench.py cpu_baseline_factored) is the same product as
+    the oracle's pairwise restatement of the reference kernel (exact up to rounding)."""
+    from plssvm_sparse_fp22_amd import datagen
+
+    for dt, tol in ((np.float64, 1e-13), (np.float32, 1e-5)):
+        (rowptr, col, val, n, d), _ = datagen.sparse_csr(3000, 400, 20, seed=4, dtype=dt)
+        data = oracle.Data(rowptr=rowptr, col=col, val=val, n=n, d=d, dtype=dt)
+        q = oracle.generate_q("linear", data)
+        p = np.random.default_rng(1).uniform(1, 2, n - 1).astype(dt)
+        want = oracle.kp("linear", data, q, dt(2.5), 1.0, -1.0, p)
+        got = oracle.kp_csr_factored(data, q, dt(2.5), 1.0, -1.0, p, fast=False)
+        assert np.abs(got - want).max() <= tol * np.abs(want).max()

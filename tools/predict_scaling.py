@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Predicted strong scaling of a W-GPU job from its measured rank shares (tools/sim_shares.sh).
+
+Every rank's share of one CG iteration is measured on one MI355X (bench.py --sim-rank r/W: exactly that
+rank's kernels, no collective); the job's iteration = the slowest share + the iteration's collectives,
+which one GPU cannot measure. They are modelled per collective as  t = alpha + bytes / beta  (ring
+algorithms over xGMI; bytes = what one GPU sends: all-gather (G-1)/G x total, all-reduce 2 (G-1)/G x
+total) for a range of RCCL latencies alpha and bus bandwidths beta — an assumption, stated as such.
+
+Collectives per CG iteration (engine.hip / sparse.hip / expand.hip):
+  dense pairwise (replicated CG):   all-reduce of raw (m reals)
+  sparse expansion (sharded CG):    all-gather of w (m reals), all-reduce of the column moments
+                                    (d x KM reals), 3 all-gathers of 2 x 512 dot partials per rank
+  sparse factored linear (sharded): all-reduce of w (d reals), 3 partial all-gathers
+
+usage: tools/predict_scaling.py <shares.jsonl> <one-GPU ms per iteration> [KM]
+"""
+import json
+import sys
+
+MODELS = [("fast", 8e-6, 200e9), ("mid", 12e-6, 150e9), ("slow", 20e-6, 100e9)]
+
+
+def collectives(rec, G, km):
+    cfg = rec["config"]
+    m, d = cfg["N"] - 1, cfg["d"]
+    s = 8 if rec["dtype"] == "f64" else 4
+    tiny = 2 * 512 * s * G  # gathered partials (bytes of the gathered buffer)
+    if cfg["layout"] == "dense" and cfg["kp_mode"] == "pairwise":
+        return [("allreduce", m * s)]
+    if cfg["kp_mode"] == "factored":
+        return [("allreduce", d * s)] + [("allgather", tiny)] * 3
+    return [("allgather", m * s), ("allreduce", d * km * s)] + [("allgather", tiny)] * 3
+
+
+def t_coll(kind, total, G, alpha, beta):
+    f = (G - 1) / G * (2 if kind == "allreduce" else 1)
+    return alpha + f * total / beta
+
+
+def main():
+    rows = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")]
+    one = float(sys.argv[2])
+    km = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    G = len(rows)
+    ms = [r["ms_per_step"] for r in rows]
+    out = {"config": rows[0]["config"]["workload"], "W": G, "ms_per_step_by_rank": ms, "max_share_ms": max(ms),
+           "one_gpu_ms": one, "predictions": {}}
+    for name, alpha, beta in MODELS:
+        c = sum(t_coll(k, b, G, alpha, beta) for k, b in collectives(rows[0], G, km)) * 1e3
+        t = max(ms) + c
+        out["predictions"][name] = {"alpha_us": alpha * 1e6, "beta_GBps": beta / 1e9, "collectives_ms": round(c, 4),
+                                    "iteration_ms": round(t, 4), "speedup": round(one / t, 2)}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
