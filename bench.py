@@ -115,7 +115,8 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
     p, n, d, y, extra = make_problem(cfg, points, features, rank, data_cache)
     ndev = pm.device_count()
     device = int(os.environ.get("LOCAL_RANK", str(rank))) % ndev if ndev > 0 else 0
-    svm = pm.CSVM(p, device=device, rank=rank, world_size=world, uid=uid, sim_rank=sim)
+    svm = pm.CSVM(p, device=device, rank=rank, world_size=world, uid=uid, sim_rank=sim,
+                  sparse_algo=getattr(args, "sparse_algo", "auto") if layout != "dense" else "auto")
     share = sim[1] if sim else world  # the work split divides the implicit matrix by this
     t0 = time.time()
     svm.setup_data_on_device()
@@ -155,9 +156,12 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
         # solve that has not converged after solve_cap_s is reported with the iterations it reached
         t_cg0 = time.perf_counter()
         delta0 = svm.cg_begin(b, q, eps=1e-3)
-        it, conv = 0, False
+        it, conv, batch = 0, False, 4
         while not conv and it < d and time.perf_counter() - t_cg0 < solve_cap_s:
-            it, conv = svm.cg_step(min(50 - it % 50, d - it))
+            # solve_cg's polling: batches of 4, 8, 16, ... up to the first reset, then 50-iteration blocks
+            n = min(batch, 50 - it % 50, d - it) if it < 50 else min(50 - it % 50, d - it)
+            it, conv = svm.cg_step(n)
+            batch *= 2
         t_cg = time.perf_counter() - t_cg0
         _, tr, _ = svm.cg_result(min(it + 1, 4096))
         learn = {"eps": 1e-3, "imax": d, "setup_s": round(t_setup, 3), "q_s": round(t_q, 4), "cg_iters": it,
@@ -222,6 +226,8 @@ def main():
                     help="one GPU computes rank R's share of a W-GPU job (no collective): measures one rank of a "
                          "multi-GPU configuration that does not fit one GPU (e.g. configs[4])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--sparse-algo", default="auto", choices=["auto", "pattern", "expansion", "dense", "onthefly"],
+                    help="sparse poly/rbf K·p algorithm (PLSSVM_MI_OPT_SPARSE_ALGO; ablations / time-to-solution studies)")
     ap.add_argument("--solve", action="store_true",
                     help="also time the whole learn() at eps = 1e-3 (setup, q, CG to convergence): 'learn' record")
     args = ap.parse_args()

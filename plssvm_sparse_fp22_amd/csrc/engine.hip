@@ -14,18 +14,6 @@ namespace plssvm_mi {
 
 namespace {
 
-template <typename T>
-ncclDataType_t nccl_type() {
-    return sizeof(T) == 8 ? ncclFloat64 : ncclFloat32;
-}
-
-#define MI_NCCL_CHECK(expr)                                                                                          \
-    do {                                                                                                             \
-        ncclResult_t r_ = (expr);                                                                                    \
-        if (r_ != ncclSuccess) {                                                                                     \
-            throw ::plssvm_mi::mi_error(-3, std::string("RCCL error '") + ncclGetErrorString(r_) + "' (" #expr ")"); \
-        }                                                                                                            \
-    } while (0)
 
 // host kernel_function<k> (include/plssvm/kernel_types.hpp:63-85) for QA_cost = k(x_m, x_m) + 1/C
 template <typename T>
@@ -108,6 +96,9 @@ engine<T>::~engine() {
     if (stream) (void) hipStreamSynchronize(stream);
     graph_reset();
     if (comm) (void) ncclCommDestroy(comm);
+    for (auto &e : cev)
+        if (e) (void) hipEventDestroy(e);
+    if (cstream) (void) hipStreamDestroy(cstream);
     if (blas) (void) rocblas_destroy_handle(blas);
     XT.reset();
     partial.reset();
@@ -152,6 +143,10 @@ void engine<T>::comm_init(int rank_, int world_, const void *uid) {
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
     MI_NCCL_CHECK(ncclCommInitRank(&comm, world, id, rank));
+    if (cstream == nullptr) {
+        MI_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+        for (auto &e : cev) MI_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
 }
 
 template <typename T>
@@ -178,7 +173,9 @@ template <typename T>
 void engine<T>::allreduce(T *buf, int64_t count) {
     if (count <= 0) return;
     if (comm != nullptr) {
+        psum_group_begin(stream);
         MI_NCCL_CHECK(ncclAllReduce(buf, buf, (size_t) count, nccl_type<T>(), ncclSum, comm, stream));
+        psum_group_end();
     } else if (xchg != nullptr) {
         xbuf.resize((size_t) count);
         MI_HIP_CHECK(hipMemcpyAsync(xbuf.data(), buf, sizeof(T) * (size_t) count, hipMemcpyDeviceToHost, stream));
@@ -193,7 +190,7 @@ void engine<T>::allreduce(T *buf, int64_t count) {
 // consumers sum them in rank order. Unsharded or a single rank: the local partials.
 template <typename T>
 const T *engine<T>::gather_partials(T *local, int slot) {
-    if (G <= 1) return local;
+    if (!gathered) return local;
     const int64_t K = 2 * RED_BLOCKS;
     T *out = cgp_g.get() + (int64_t) slot * G * K;
     if (comm != nullptr) {
@@ -210,15 +207,38 @@ const T *engine<T>::gather_partials(T *local, int slot) {
 }
 
 template <typename T>
+void engine<T>::psum_group_begin(hipStream_t s) {
+    if (!psum_pending || comm == nullptr) return;
+    MI_NCCL_CHECK(ncclGroupStart());
+    MI_NCCL_CHECK(ncclAllGather(cgp.get(), cgp_g.get(), (size_t) (2 * RED_BLOCKS), nccl_type<T>(), comm, s));
+}
+
+template <typename T>
+void engine<T>::psum_group_end() {
+    if (!psum_pending || comm == nullptr) return;
+    MI_NCCL_CHECK(ncclGroupEnd());
+    psum_pending = false;
+}
+
+template <typename T>
+void engine<T>::flush_psum() {
+    if (!psum_pending) return;
+    psum_pending = false;
+    gather_partials(cgp.get(), 0);
+}
+
+template <typename T>
 void engine<T>::gather_input(const T *p) {
-    if (shard && in_group()) allgather_rows(const_cast<T *>(p));
+    if (gathered) allgather_rows(const_cast<T *>(p));
 }
 
 template <typename T>
 void engine<T>::reduce_scatter_rows(T *buf) {
     if (comm != nullptr) {
+        psum_group_begin(stream);
         MI_NCCL_CHECK(ncclReduceScatter(buf, buf + (int64_t) rank * chunk, (size_t) chunk, nccl_type<T>(), ncclSum, comm,
                                         stream));
+        psum_group_end();
     } else if (xchg != nullptr) {
         allreduce(buf, chunk * world);  // the host transport sums everything; the own rows are used
     }
@@ -227,7 +247,9 @@ void engine<T>::reduce_scatter_rows(T *buf) {
 template <typename T>
 void engine<T>::allgather_rows(T *buf) {
     if (comm != nullptr) {
+        psum_group_begin(stream);
         MI_NCCL_CHECK(ncclAllGather(buf + (int64_t) rank * chunk, buf, (size_t) chunk, nccl_type<T>(), comm, stream));
+        psum_group_end();
     } else if (xchg != nullptr) {
         const int64_t total = chunk * world;
         xbuf.resize((size_t) total);
@@ -306,11 +328,15 @@ void engine<T>::finish_setup() {
     {
         const char *se = std::getenv("PLSSVM_MI_SHARD");
         const int opt = se != nullptr ? std::atoi(se) : -1;
-        shard = (in_group() && (opt == 1 || (opt < 0 && sparse))) || (sim_world > 0 && opt == 1);
+        // a one-rank RCCL group with PLSSVM_MI_SHARD=1 runs every sharded collective through RCCL on one GPU
+        // (the test path of the sharded RCCL code on a one-GPU box)
+        const bool grp = (comm != nullptr || xchg != nullptr) && sim_world == 0;
+        shard = (grp && (opt == 1 || (opt < 0 && sparse && world > 1))) || (sim_world > 0 && opt == 1);
+        gathered = shard && grp;
         v0 = shard ? r0 : 0;
         vn = shard ? r1 - r0 : m;
-        G = (shard && in_group()) ? world : 1;
-        if (G > 1) cgp_g.alloc(4 * (int64_t) G * 2 * RED_BLOCKS, stream);
+        G = gathered ? world : 1;
+        if (gathered) cgp_g.alloc(4 * (int64_t) G * 2 * RED_BLOCKS, stream);
     }
     tiles_upload();
     if (!sparse && !factored()) {
@@ -425,7 +451,7 @@ void engine<T>::kp_host(const T *q_host, const T *p, T *ret_host, T add) {
         MI_HIP_CHECK(hipMemcpyAsync(pv.get(), p, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
         MI_HIP_CHECK(hipMemcpyAsync(ret.get(), ret_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
         kp_device(pv.get(), ret.get(), add, false, nullptr);
-        if (shard && in_group()) allgather_rows(ret.get());  // device_reduction's result on every rank
+        if (gathered) allgather_rows(ret.get());  // device_reduction's result on every rank
         MI_HIP_CHECK(hipMemcpyAsync(ret_host, ret.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
@@ -446,7 +472,7 @@ void engine<T>::kp_part(const T *p_host, T *out_host, int part) {
         MI_HIP_CHECK(hipMemcpyAsync(pv.get(), p_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
         if (part == 1) sparse_kp_raw(pv.get(), nullptr, false);
         else kp_raw(pv.get(), nullptr);
-        if (shard && in_group()) allgather_rows(raw.get());
+        if (gathered) allgather_rows(raw.get());
         MI_HIP_CHECK(hipMemcpyAsync(out_host, raw.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));
@@ -475,7 +501,8 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
     // d = r, with sum d / sum q d for the first Q~d
     launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, q.get() + v0, nullptr, 1, 1, nullptr, 0, vn, cgp.get(), sc.get(),
                           stream);
-    gather_partials(cgp.get(), 0);
+    if (gathered && comm != nullptr) psum_pending = true;  // gathered with the first K·p's collective
+    else gather_partials(cgp.get(), 0);
     run = 0;
     cg_active = true;
     // a solve that can reach a whole block captures it now (capture launches nothing; the
@@ -495,7 +522,7 @@ void engine<T>::cg_iter(int reset) {
     const cg_scalars<T> *st = sc.get();
     T *psum = cgp.get(), *pdad = psum + 2 * RED_BLOCKS, *prr = psum + 4 * RED_BLOCKS;
     // sharded: the partials the previous step gathered (slot 0: sum d / sum q d)
-    const T *psum_in = G > 1 ? cgp_g.get() : psum;
+    const T *psum_in = gathered ? cgp_g.get() : psum;
     const int raw_only = (sim_world > 0 && sim_rank != 0 && !shard) ? 1 : 0;
     // Ad = Q~ d (:111-113); alpha = delta / (d . Ad) (:116) in the next kernel
     const T *slabs = nullptr;
@@ -515,6 +542,7 @@ void engine<T>::cg_iter(int reset) {
     } else {
         kp_raw(dv.get(), st);
     }
+    flush_psum();  // no collective of the K·p carried it
     if (!(sparse_stored() && factored() && world == 1 && sim_world == 0 && csr.rb_csr.nblk > 0))
         launch_cg_fin_dad<T>(raw.get() + v0, slabs, P, m, q.get() + v0, dv.get() + v0, psum_in, G, QA_cost, cost_inv(),
                              raw_only, vn, Ad.get() + v0, pdad, sc.get(), stream);
@@ -528,7 +556,8 @@ void engine<T>::cg_iter(int reset) {
     // delta = r.r ; stop test ; beta (:135-146); d = beta d + r (:149-151), with sum d / sum q d
     launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, q.get() + v0, gather_partials(prr, 2), G, 0, trace.get(), trace_cap,
                           vn, psum, sc.get(), stream);
-    gather_partials(psum, 0);
+    if (gathered && comm != nullptr) psum_pending = true;  // gathered with the next K·p's first collective
+    else gather_partials(psum, 0);
 }
 
 // Iteration blocks of CG_RESET (the reset period) starting at a multiple of it are replayed from one
@@ -610,7 +639,7 @@ void engine<T>::cg_result(T *x_out, double *trace_out, int64_t trace_len, int64_
     cg_scalars<T> h{};
     MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));
     if (x_out && m > 0) {
-        if (shard && in_group()) allgather_rows(x.get());  // every rank's rows of the solution
+        if (gathered) allgather_rows(x.get());  // every rank's rows of the solution
         MI_HIP_CHECK(hipMemcpyAsync(x_out, x.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
     }
     MI_HIP_CHECK(hipStreamSynchronize(stream));

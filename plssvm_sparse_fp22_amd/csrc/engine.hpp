@@ -15,6 +15,19 @@
 
 namespace plssvm_mi {
 
+template <typename T>
+inline ncclDataType_t nccl_type() {
+    return sizeof(T) == 8 ? ncclFloat64 : ncclFloat32;
+}
+
+#define MI_NCCL_CHECK(expr)                                                                                          \
+    do {                                                                                                             \
+        ncclResult_t r_ = (expr);                                                                                    \
+        if (r_ != ncclSuccess) {                                                                                     \
+            throw ::plssvm_mi::mi_error(-3, std::string("RCCL error '") + ncclGetErrorString(r_) + "' (" #expr ")"); \
+        }                                                                                                            \
+    } while (0)
+
 void partition_superblocks(int64_t nb, int rank, int world, int64_t &s0, int64_t &s1, int64_t &s_total,
                            int64_t &tiles_total, int64_t &tiles_local);
 
@@ -64,11 +77,22 @@ struct engine : engine_base {
     // summed from the G ranks' gathered partials in rank order (the same bits everywhere); a K·p input the
     // path needs whole is gathered first, a path's full-length partial result reduce-scattered
     bool shard = false;
+    bool gathered = false;  // sharded in a real group (any size, also a one-rank RCCL group): partials and
+                            // inputs move through the group's transport
     int64_t v0 = 0, vn = 0;
     int G = 1;
     dev_buf<T> cgp_g;      // gathered partials, slots [4][G][2 RED_BLOCKS]: sum d / sum q d, d.Ad, r.r, kp sums
     std::vector<T> xpart;  // host staging of the host exchange's partial gathers
     const T *gather_partials(T *local, int slot);
+    // RCCL group: the sum d / sum q d partials of a CG step ride with the next collective of the K·p
+    // (one launch, one latency) instead of a collective of their own
+    bool psum_pending = false;
+    void psum_group_begin(hipStream_t s);
+    void psum_group_end();
+    void flush_psum();
+    // second stream for collectives that overlap kernels of the same K·p (kernel expansion, sharded RCCL group)
+    hipStream_t cstream = nullptr;
+    hipEvent_t cev[4] = { nullptr, nullptr, nullptr, nullptr };
     void gather_input(const T *p);   // sharded group: p's rows of every rank, in place
     void reduce_scatter_rows(T *buf);  // sharded group: own rows of the sum over ranks
 
@@ -143,6 +167,7 @@ struct engine : engine_base {
     void expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);
     void expansion_dominant(const T *p, const cg_scalars<T> *status);  // the remainder stream
     void expansion_moments(const T *w, const cg_scalars<T> *status);   // column moments (SELL CSC pass)
+    void expansion_mscale(const cg_scalars<T> *status);                 // moments -> Horner coefficients
     // predict through the expansion (expand.hip); false: not applicable, predict brute force
     bool expansion_predict(const T *alpha_dev, T alpha_m, T bias, const int64_t *zr_dev, const int32_t *zc_dev,
                            const T *zv_dev, int64_t np, int64_t max_nnz_z, double zabs_max, double znorm_max, T nlast,

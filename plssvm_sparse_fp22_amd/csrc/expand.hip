@@ -1534,14 +1534,22 @@ void engine<T>::expansion_moments(const T *w, const cg_scalars<T> *status) {
         // (a real group: each rank's rows, then one all-reduce of the d x K moments)
         launch_panel_spmv<T>(csr.spmv_csc, w + csr.csc_r0, csr.csc_r1 - csr.csc_r0, ex.mom.get(), status, stream, ex.KM, 1);
         if (csr.csc_r1 - csr.csc_r0 < m) allreduce(ex.mom.get(), d * ex.KM);
-        coefs cf;
-        std::memcpy(cf.c, ex.coef, sizeof(cf.c));
-        if (exp_ablate() & 2)
-            for (int k = 2; k <= EXP_KMAX; ++k) cf.c[k] = 0.0;
-        hipLaunchKernelGGL(exp_mscale_kernel<T>, dim3((unsigned) ceil_div(d * ex.KM, 256)), dim3(256), 0, stream,
-                           ex.mom.get(), d, ex.KM, cf, ex.M.get(), status);
-        MI_LAUNCH_CHECK();
+        expansion_mscale(status);
     }
+}
+
+// M[f][k] = coef_{k+1} mom[k][f] (after the group's all-reduce of the moments)
+template <typename T>
+void engine<T>::expansion_mscale(const cg_scalars<T> *status) {
+    auto &ex = csr.ex;
+    if (d <= 0) return;
+    coefs cf;
+    std::memcpy(cf.c, ex.coef, sizeof(cf.c));
+    if (exp_ablate() & 2)
+        for (int k = 2; k <= EXP_KMAX; ++k) cf.c[k] = 0.0;
+    hipLaunchKernelGGL(exp_mscale_kernel<T>, dim3((unsigned) ceil_div(d * ex.KM, 256)), dim3(256), 0, stream,
+                       ex.mom.get(), d, ex.KM, cf, ex.M.get(), status);
+    MI_LAUNCH_CHECK();
 }
 
 template <typename T>
@@ -1558,11 +1566,35 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
         MI_LAUNCH_CHECK();
         w = ex.wv.get();
     }
-    gather_input(w);
-    launch_dot2<T>(w, nullptr, nullptr, nullptr, m, red.get(), status, stream);  // S = sum_j w_j
-    launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
-    expansion_moments(w, status);
-    expansion_dominant(w, status);
+    if (shard && comm != nullptr && cstream != nullptr && d > 0) {
+        // sharded RCCL group: the all-gather of w (with the pending CG partials) and the all-reduce of the
+        // moments run on the collective stream, overlapping the moments pass and the remainder stream
+        MI_HIP_CHECK(hipEventRecord(cev[0], stream));
+        MI_HIP_CHECK(hipStreamWaitEvent(cstream, cev[0], 0));
+        psum_group_begin(cstream);
+        MI_NCCL_CHECK(ncclAllGather(const_cast<T *>(w) + (int64_t) rank * chunk, const_cast<T *>(w), (size_t) chunk,
+                                    nccl_type<T>(), comm, cstream));
+        psum_group_end();
+        MI_HIP_CHECK(hipEventRecord(cev[1], cstream));
+        launch_panel_spmv<T>(csr.spmv_csc, w + csr.csc_r0, csr.csc_r1 - csr.csc_r0, ex.mom.get(), status, stream, ex.KM, 1);
+        MI_HIP_CHECK(hipEventRecord(cev[2], stream));
+        MI_HIP_CHECK(hipStreamWaitEvent(cstream, cev[2], 0));
+        MI_NCCL_CHECK(ncclAllReduce(ex.mom.get(), ex.mom.get(), (size_t) (d * ex.KM), nccl_type<T>(), ncclSum,
+                                    comm, cstream));
+        MI_HIP_CHECK(hipEventRecord(cev[3], cstream));
+        MI_HIP_CHECK(hipStreamWaitEvent(stream, cev[1], 0));  // w of every rank
+        launch_dot2<T>(w, nullptr, nullptr, nullptr, m, red.get(), status, stream);  // S = sum_j w_j
+        launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+        expansion_dominant(w, status);
+        MI_HIP_CHECK(hipStreamWaitEvent(stream, cev[3], 0));  // the group's moments
+        expansion_mscale(status);
+    } else {
+        gather_input(w);
+        launch_dot2<T>(w, nullptr, nullptr, nullptr, m, red.get(), status, stream);  // S = sum_j w_j
+        launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+        expansion_moments(w, status);
+        expansion_dominant(w, status);
+    }
     T kappa = 0;
     if (kernel == 1) {
         kappa = 1;
@@ -1861,6 +1893,7 @@ bool engine<T>::expansion_predict(const T *alpha_dev, T alpha_m, T bias, const i
     template void engine<T>::build_expansion(const int64_t *, int64_t);                      \
     template void engine<T>::expansion_dominant(const T *, const cg_scalars<T> *);           \
     template void engine<T>::expansion_moments(const T *, const cg_scalars<T> *);            \
+    template void engine<T>::expansion_mscale(const cg_scalars<T> *);                        \
     template void engine<T>::expansion_kp_raw(const T *, const cg_scalars<T> *, bool);      \
     template bool engine<T>::expansion_predict(const T *, T, T, const int64_t *, const int32_t *, const T *, int64_t, \
                                                int64_t, double, double, T, T *);

@@ -373,47 +373,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
     if (h == 0) partial[wg * KP_REC + q] = a;  // row sums of the I rows
 }
 
-// The slab record of tile (I, J), I >= J, of the rank's super-blocks [s0, s1): its workgroup index
-// (kp_tile_offsets' table + the tile's place in its super-block), or -1 when another rank owns it.
-__device__ __forceinline__ int64_t kp_tile_record(int64_t I, int64_t J, int64_t nb, int64_t s0, int64_t s1,
-                                                  const int32_t *__restrict__ wg_off) {
-    const int64_t SI = I / KP_SUPER, SJ = J / KP_SUPER, sb = tri_index(SI, SJ);
-    if (sb < s0 || sb >= s1) return -1;
-    const int64_t ta = I - SI * KP_SUPER, tb = J - SJ * KP_SUPER;
-    const int64_t local = SI == SJ ? ta * (ta + 1) / 2 + tb : ta * min<int64_t>(KP_SUPER, nb - SJ * KP_SUPER) + tb;
-    return (int64_t) wg_off[sb - s0] + local;
-}
-
-// value of column block c for row i (block Ib): tile (Ib, c)'s row sums when c <= Ib, tile (c, Ib)'s column
-// sums when c > Ib; 0 for a tile of another rank
+// Slab values of row i (row block Ib, offset q) for the column blocks c of column super-block CS, in c
+// order: tile (Ib, c)'s row sums when c <= Ib, tile (c, Ib)'s column sums when c > Ib. base = the first
+// record of the super-block holding those tiles (kp_tile_offsets' table); tiles inside a super-block are
+// numbered row-major (a diagonal one: its lower triangle, ta (ta + 1) / 2 + tb).
 template <typename T>
-__device__ __forceinline__ T kp_slab_value(const T *__restrict__ partial, int64_t Ib, int64_t q, int64_t c, int64_t nb,
-                                           int64_t s0, int64_t s1, const int32_t *__restrict__ wg_off) {
-    const int64_t rec = c <= Ib ? kp_tile_record(Ib, c, nb, s0, s1, wg_off) : kp_tile_record(c, Ib, nb, s0, s1, wg_off);
-    return rec < 0 ? T(0) : partial[rec * KP_REC + (c <= Ib ? 0 : KP_TILE) + q];
+__device__ __forceinline__ void kp_sb_values(const T *__restrict__ partial, int64_t Ib, int64_t q, int64_t CS,
+                                             int64_t nb, int64_t base, T *v, int cnt) {
+    const int64_t RS = Ib / KP_SUPER;
+    for (int u = 0; u < cnt; ++u) {
+        const int64_t c = CS * KP_SUPER + u;
+        const int64_t I = c <= Ib ? Ib : c, J = c <= Ib ? c : Ib;
+        const int64_t SI = c <= Ib ? RS : CS, SJ = c <= Ib ? CS : RS;
+        const int64_t ta = I - SI * KP_SUPER, tb = J - SJ * KP_SUPER;
+        const int64_t local = SI == SJ ? ta * (ta + 1) / 2 + tb : ta * min<int64_t>(KP_SUPER, nb - SJ * KP_SUPER) + tb;
+        v[u] = partial[(base + local) * KP_REC + (c <= Ib ? 0 : KP_TILE) + q];
+    }
 }
 
-// raw[i] = sum over the column blocks c = 0 .. nb-1 of the slab values of row i (kp_slab_value), in c order:
-// the whole triangle on one rank. 8 records in flight per step (one thread per i: memory parallelism sets the
-// speed); a row's 64-lane group reads 64 consecutive values of each record
+// raw[i] = sum over the column blocks c = 0 .. nb-1 (in order) of row i's slab values: the whole
+// triangle on one rank. One thread per row; a wave's 64 rows share their row block, so the record
+// arithmetic is wave-uniform; a super-block's 8 records in flight per step
 template <typename T>
 __global__ __launch_bounds__(256) void kp_reduce_kernel(const T *__restrict__ partial, int64_t nb, int64_t m,
                                                         const int32_t *__restrict__ wg_off, T *__restrict__ raw,
                                                         const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t Ib = __builtin_amdgcn_readfirstlane((int) (((int64_t) blockIdx.x * blockDim.x + (threadIdx.x & ~63)) / KP_TILE));
     if (i >= m) return;
-    const int64_t Ib = i / KP_TILE, q = i % KP_TILE, s_all = INT64_MAX;
+    const int64_t q = i % KP_TILE, RS = Ib / KP_SUPER, ns = (nb + KP_SUPER - 1) / KP_SUPER;
     T s = 0;
-    int64_t c = 0;
-    for (; c + 8 <= nb; c += 8) {
-        T v[8];
+    for (int64_t CS = 0; CS < ns; ++CS) {
+        const int64_t sb = RS >= CS ? tri_index(RS, CS) : tri_index(CS, RS);
+        const int64_t base = wg_off[sb];
+        const int cnt = (int) min<int64_t>(KP_SUPER, nb - CS * KP_SUPER);
+        T v[KP_SUPER];
+        if (cnt == KP_SUPER) {
+            kp_sb_values(partial, Ib, q, CS, nb, base, v, KP_SUPER);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = kp_slab_value(partial, Ib, q, c + u, nb, 0, s_all, wg_off);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s += v[u];
+            for (int u = 0; u < KP_SUPER; ++u) s += v[u];
+        } else {
+            kp_sb_values(partial, Ib, q, CS, nb, base, v, cnt);
+            for (int u = 0; u < cnt; ++u) s += v[u];
+        }
     }
-    for (; c < nb; ++c) s += kp_slab_value(partial, Ib, q, c, nb, 0, s_all, wg_off);
     raw[i] = s;
 }
 
@@ -434,22 +438,24 @@ __global__ __launch_bounds__(64 * KP_RED_G) void kp_reduce_share_kernel(const T 
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int64_t i = (int64_t) blockIdx.x * 64 + lane;
     const int64_t ns = (nb + KP_SUPER - 1) / KP_SUPER;
+    const int64_t Ib = __builtin_amdgcn_readfirstlane((int) (((int64_t) blockIdx.x * 64) / KP_TILE));
     T s = 0;
     if (i < m) {
-        const int64_t Ib = i / KP_TILE, q = i % KP_TILE, RS = Ib / KP_SUPER;
+        const int64_t q = i % KP_TILE, RS = Ib / KP_SUPER;
         const int64_t cs0 = g * ns / KP_RED_G, cs1 = (g + 1) * ns / KP_RED_G;
         for (int64_t CS = cs0; CS < cs1; ++CS) {
             const int64_t sb = (RS >= CS) ? tri_index(RS, CS) : tri_index(CS, RS);
             if (sb < s0 || sb >= s1) continue;
-            const int64_t c0 = CS * KP_SUPER, c1 = min(nb, c0 + KP_SUPER);
-            if (c1 - c0 == KP_SUPER) {
-                T v[KP_SUPER];
-#pragma unroll
-                for (int u = 0; u < KP_SUPER; ++u) v[u] = kp_slab_value(partial, Ib, q, c0 + u, nb, s0, s1, wg_off);
+            const int64_t base = wg_off[sb - s0];
+            const int cnt = (int) min<int64_t>(KP_SUPER, nb - CS * KP_SUPER);
+            T v[KP_SUPER];
+            if (cnt == KP_SUPER) {
+                kp_sb_values(partial, Ib, q, CS, nb, base, v, KP_SUPER);
 #pragma unroll
                 for (int u = 0; u < KP_SUPER; ++u) s += v[u];
             } else {
-                for (int64_t c = c0; c < c1; ++c) s += kp_slab_value(partial, Ib, q, c, nb, s0, s1, wg_off);
+                kp_sb_values(partial, Ib, q, CS, nb, base, v, cnt);
+                for (int u = 0; u < cnt; ++u) s += v[u];
             }
         }
     }

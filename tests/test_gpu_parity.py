@@ -277,3 +277,43 @@ def test_single_rank_rccl_group(layout, kernel, kp_mode):
         svm.close()
     for a, b in zip(outs[0], outs[1]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("layout,kernel,kp_mode,algo", [("csr", "rbf", "auto", "auto"), ("csr", "polynomial", "auto", "auto"),
+                                                        ("csr", "linear", "auto", "auto"),
+                                                        ("csr", "rbf", "auto", "onthefly"), ("csr", "rbf", "auto", "pattern"),
+                                                        ("dense", "rbf", "auto", "auto")])
+def test_single_rank_rccl_group_sharded(layout, kernel, kp_mode, algo, monkeypatch):
+    """The sharded CG's RCCL code (PLSSVM_MI_SHARD=1 in a one-rank RCCL group): dot partials all-gathered
+    (the step's sum d / sum q d partials grouped with the next K·p's first collective), K·p inputs
+    all-gathered, the expansion's w all-gather and moment all-reduce on the collective stream overlapping
+    the moments pass and the remainder stream, reduce-scatter of the pattern / tile partial sums. With one
+    rank every gathered sum is the local one, so K·p, the CG trace and the alphas must equal the context
+    without a communicator bit for bit."""
+    n, d = 3000, 64
+    if layout == "dense":
+        X, y = datagen.blobs(n, d, seed=3)
+    else:
+        csr, y = datagen.sparse_csr(n, 5000, 20, seed=3, dtype=np.float64)
+    outs = []
+    for uid in (None, pm.unique_id()):
+        if uid is None:
+            monkeypatch.delenv("PLSSVM_MI_SHARD", raising=False)
+        else:
+            monkeypatch.setenv("PLSSVM_MI_SHARD", "1")
+        p = pm.Parameter(kernel, gamma=1.0 / d, coef0=1.0 if kernel == "polynomial" else 0.0, real_type=np.float64)
+        if layout == "dense":
+            p.data = X
+        else:
+            p.csr = csr
+        p.labels = y
+        svm = pm.CSVM(p, kp_mode=kp_mode, uid=uid, sparse_algo=algo)
+        svm.setup_data_on_device()
+        svm.generate_q()
+        x = np.linspace(1, 2, n - 1)
+        ret = svm.run_device_kernel(None, np.zeros(n - 1), x, 1.0)
+        svm.learn(imax=60)  # crosses the every-50th explicit residual
+        outs.append((ret, np.array(svm.trace), svm.alpha.copy()))
+        svm.close()
+    for a, b in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, b)
