@@ -340,10 +340,12 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
         # kernel expansion: the dominant kernel is the remainder stream of the pairs sharing
         # two or more features (uint16 j + H per slot, uint16 row per 4-slot chunk), read once per K·p;
         # the column-moment and Horner passes are the two SELL SpMV passes of the linear path
-        rem = info["pair_slots"] * (2 + es) + info["exp_chunks"] * 2
+        hb = info["exp_hbytes"] or es
+        rem = info["pair_slots"] * (2 + hb) + info["exp_chunks"] * 2
         return dict(bound="hbm", achieved=rem / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
                     frac=rem / s / PEAKS["hbm"], traffic=None, kernel="exp_hcell_kernel", launch_ms=ms_dom,
-                    alg_bytes=rem, alg_bytes_def="remainder stream: slots x (2 + sizeof(real)) + chunks x 2 (run layout: chunks = 0, slots = entries + dummies)",
+                    alg_bytes=rem, alg_bytes_def="remainder stream: slots x (2 + bytes per stored H) + chunks x 2 (run layout: chunks = 0, slots = entries + dummies)",
+                    h_storage="bfloat16 (precision bound, DESIGN §5.1.2)" if hb == 2 else f"real ({hb} B)",
                     stream_layout="runs" if info["exp_chunks"] == 0 else "4-slot chunks",
                     exp_terms=info["exp_terms"], multi_pairs=info["pairs"], pair_slots=info["pair_slots"],
                     spmv_bytes=info["spmv_bytes"], survey_alg_bytes=survey,

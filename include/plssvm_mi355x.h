@@ -255,6 +255,8 @@ typedef struct {
     int exp_terms;      /* kernel expansion: polynomial degree K of the per-feature pair function */
     int exp_waves;      /* kernel expansion: waves of the remainder stream */
     int64_t exp_chunks; /* kernel expansion: 4-slot chunks of the remainder stream (this rank's rows); 0 = run layout */
+    int exp_hbytes;     /* kernel expansion: bytes of a stored remainder value (2 = bfloat16 under the precision
+                           bound of expand.hip "H storage", else sizeof(real)) */
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
 

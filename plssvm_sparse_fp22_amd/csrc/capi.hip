@@ -389,6 +389,7 @@ int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
         info->exp_terms = e.csr.ex.on ? e.csr.ex.K : 0;
         info->exp_waves = (int) (e.csr.ex.nblk * EXP_NWV_C);
         info->exp_chunks = e.csr.ex.nchunks;
+        info->exp_hbytes = e.csr.ex.on ? (e.csr.ex.hbf16 ? 2 : (int) sizeof(e.gamma)) : 0;
     });
 }
 

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 
 #include "../../include/plssvm_mi355x.h"
 #include "engine.hpp"
@@ -363,9 +364,10 @@ template <typename T>
 __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__restrict__ rowptr,
                                                                const int32_t *__restrict__ col,
                                                                const T *__restrict__ val, int64_t r0, phi_fn phi,
-                                                               const int64_t *__restrict__ off8, int32_t *__restrict__ sj,
-                                                               T *__restrict__ sv,
-                                                               unsigned long long *__restrict__ lower_nz) {
+                                                               double kbase, const int64_t *__restrict__ off8,
+                                                               int32_t *__restrict__ sj, T *__restrict__ sv,
+                                                               unsigned long long *__restrict__ lower_nz,
+                                                               unsigned long long *__restrict__ ratio_bits) {
     __shared__ int32_t zcol[RJ_ECAP];
     __shared__ T zval[RJ_ECAP];
     __shared__ unsigned long long lnz_s;
@@ -377,6 +379,7 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
     if (tid == 0) lnz_s = 0ull;
     __syncthreads();
     unsigned long long lnz = 0ull;
+    double rmax = 0.0;
     const int64_t q0 = off8[r], q1 = off8[r + 1];
     constexpr int NW = RJH_NT / 64;
     int64_t q = q0 + wave;
@@ -421,13 +424,19 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
                 sphi += __shfl(pa, b);
             }
         }
-        const T h = (T) (phi(sd) - sphi);
+        const double ps = phi(sd);
+        const T h = (T) (ps - sphi);
+        // |H| relative to the pair's kernel value without the e_i e_j factor (rbf 1 + E(s), poly kappa + c(s))
+        const double kv = fabs(kbase + ps);
+        const double ratio = h == T(0) ? 0.0 : (kv > 0.0 ? fabs((double) h) / kv : 1e300);
         if (lane == 0) {
             sv[q] = h;
             if (j < i && h != T(0)) ++lnz;
+            rmax = fmax(rmax, ratio);
         }
     }
     if (lane == 0 && lnz) atomicAdd(&lnz_s, lnz);
+    if (lane == 0 && rmax > 0.0) atomicMax(ratio_bits, (unsigned long long) __double_as_longlong(rmax));  // >= 0: bit order
     __syncthreads();
     if (tid == 0 && lnz_s) atomicAdd(lower_nz, lnz_s);
 }
@@ -489,13 +498,20 @@ __global__ __launch_bounds__(256) void exp_cell_count_kernel(const int64_t *__re
     if (Wc >= 0) cnt[exp_cidx(r, Wc, nW, RB)] = (k + 3) & ~int64_t(3);
 }
 
+// bfloat16 of a float, round to nearest even (finite values)
+__device__ __forceinline__ uint16_t bf16_rne(float f) {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t) (u >> 16);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__restrict__ off8,
                                                                const int32_t *__restrict__ sj, const T *__restrict__ sv,
                                                                int64_t R, int64_t nW, int64_t CW, int64_t RB,
                                                                const int64_t *__restrict__ coff,
                                                                uint16_t *__restrict__ hjl, T *__restrict__ hv,
-                                                               uint16_t *__restrict__ hrow) {
+                                                               uint16_t *__restrict__ hv16, uint16_t *__restrict__ hrow) {
     const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
     const uint16_t rl = (uint16_t) (r % RB);
@@ -514,7 +530,8 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__
             k = 0;
         }
         hjl[base + k] = (uint16_t) (sj[s] - W * CW);
-        hv[base + k] = h;
+        if (hv16 != nullptr) hv16[base + k] = bf16_rne((float) h);
+        else hv[base + k] = h;
         ++k;
     }
     if (Wc >= 0) close();
@@ -628,11 +645,12 @@ __device__ __forceinline__ void seg_step(double &v, int k) {
 // software-pipelined one step ahead, also across window boundaries), gathers w_j from LDS and adds its
 // rows' partial sums (segmented shuffle reduction) into an LDS row accumulator only it writes.
 // Fixed order, no atomics: bitwise reproducible.
-template <typename T, int RBB>
+template <typename T, int RBB, bool HB>
 __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *__restrict__ woff,
                                                                  const uint16_t *__restrict__ hrow,
                                                                  const uint16_t *__restrict__ hjl,
-                                                                 const T *__restrict__ hv, const T *__restrict__ w,
+                                                                 const T *__restrict__ hv,
+                                                                 const uint16_t *__restrict__ hv16, const T *__restrict__ w,
                                                                  int64_t m, int64_t r0, int64_t R, int64_t nW,
                                                                  int64_t RB, int64_t nI, int G, T *__restrict__ hs,
                                                                  T *__restrict__ hslab,
@@ -683,12 +701,15 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     int rl_n = 0;
     u32x2 jj_n = { 0u, 0u };
     T h_n[4] = { T(0), T(0), T(0), T(0) };
+    u32x2 hb_n = { 0u, 0u };  // bfloat16 H, kept raw until the step uses it (a conversion here would wait for the load)
     auto fetch = [&](int64_t c) {
         if (s_end == wo[W0]) return;  // empty stream (wave-uniform)
         const int64_t cl = c < s_end ? c : s_end - 1;
         rl_n = (int) __builtin_nontemporal_load(hrow + cl);
         jj_n = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hjl + 4 * cl));
-        if constexpr (sizeof(T) == 4) {
+        if constexpr (HB) {
+            hb_n = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hv16 + 4 * cl));
+        } else if constexpr (sizeof(T) == 4) {
             const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(hv + 4 * cl));
             h_n[0] = v.x, h_n[1] = v.y, h_n[2] = v.z, h_n[3] = v.w;
         } else {
@@ -711,8 +732,13 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             const bool have = cb + lane < c_end;
             const int rl = have ? rl_n : -1;
             const u32x2 jj = jj_n;
-            const T h0 = h_n[0], h1 = h_n[1], h2 = h_n[2], h3 = h_n[3];
+            T h0 = h_n[0], h1 = h_n[1], h2 = h_n[2], h3 = h_n[3];
+            const u32x2 hb = hb_n;
             fetch((cb + 64 < c_end ? cb + 64 : c_end) + lane);  // next step (next window's first at c_end)
+            if constexpr (HB) {  // bfloat16 H: the float's top 16 bits
+                h0 = (T) __uint_as_float(hb.x << 16), h1 = (T) __uint_as_float(hb.x & 0xFFFF0000u);
+                h2 = (T) __uint_as_float(hb.y << 16), h3 = (T) __uint_as_float(hb.y & 0xFFFF0000u);
+            }
             T acc = T(0);
             if (have) {
                 acc = h0 * wb[jj.x & 0xFFFFu];
@@ -1304,7 +1330,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         dev_buf<unsigned long long> lnz;
         cnt.alloc(std::max<int64_t>(R, 1), stream);
         cnt8.alloc(R + 1, stream);
-        lnz.alloc(1, stream);
+        lnz.alloc(2, stream);  // [0] lower pairs with H != 0, [1] max |H| / kernel value (double bits)
         if (R > 0) {
             hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
                                csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(),
@@ -1330,14 +1356,23 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
             hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
                                csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(), off8.get(), sj.get());
             MI_LAUNCH_CHECK();
+            double kbase = 1.0;  // rbf: 1 + E(s); poly: kappa + c(s)
+            if (kernel == 1) {
+                kbase = 1.0;
+                for (int q2 = 0; q2 < degree; ++q2) kbase *= (double) coef0;
+            }
             hipLaunchKernelGGL(exp_rowjoin_h_kernel<T>, dim3((unsigned) R), dim3(RJH_NT), 0, stream, csr.rowptr.get(),
-                               csr.col.get(), csr.val.get(), r0, phi, off8.get(), sj.get(), sv.get(), lnz.get());
+                               csr.col.get(), csr.val.get(), r0, phi, kbase, off8.get(), sj.get(), sv.get(), lnz.get(),
+                               lnz.get() + 1);
             MI_LAUNCH_CHECK();
         }
-        unsigned long long np = 0;
-        MI_HIP_CHECK(hipMemcpyAsync(&np, lnz.get(), sizeof(np), hipMemcpyDeviceToHost, stream));
+        unsigned long long np[2] = { 0ull, 0ull };
+        MI_HIP_CHECK(hipMemcpyAsync(np, lnz.get(), sizeof(np), hipMemcpyDeviceToHost, stream));
         MI_HIP_CHECK(hipStreamSynchronize(stream));
-        ex.pairs = (int64_t) np;
+        ex.pairs = (int64_t) np[0];
+        double rm = 0.0;
+        std::memcpy(&rm, &np[1], sizeof(rm));
+        ex.hratio = rm;
         pt.mark("expansion: row join (rows)");
     } else {
         sort_join();
@@ -1449,12 +1484,20 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
             scan(ncnt);
             ex.nchunks = ex.slots / 4;
             ex.hjl.alloc(std::max<int64_t>(ex.slots, 4), stream);
-            ex.hv.alloc(std::max<int64_t>(ex.slots, 4), stream);
+            // H storage (float contexts): bfloat16 when every stored |H_ij| is at most 2^-15 of its pair's kernel
+            // value (row join's hratio) — rounding H to 8 mantissa bits (relative error <= 2^-9) then moves each
+            // pair's term by at most 2^-24 of the pair's kernel value, below the float rounding of that value
+            // itself; PLSSVM_MI_EXP_HFMT=full keeps the real type
+            const char *hf = std::getenv("PLSSVM_MI_EXP_HFMT");
+            ex.hbf16 = sizeof(T) == 4 && ex.hratio >= 0.0 && ex.hratio <= std::ldexp(1.0, -15) &&
+                       !(hf != nullptr && std::strcmp(hf, "full") == 0);
+            if (ex.hbf16) ex.hv16.alloc(std::max<int64_t>(ex.slots, 4), stream);
+            else ex.hv.alloc(std::max<int64_t>(ex.slots, 4), stream);
             ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
             if (R > 0) {
                 hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
                                    off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
-                                   ex.hv.get(), ex.hrow.get());
+                                   ex.hv.get(), ex.hv16.get(), ex.hrow.get());
                 MI_LAUNCH_CHECK();
             }
             ex.woff.alloc(std::max<int64_t>(nbv * (ex.nW + 1), 1), stream);
@@ -1493,8 +1536,8 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
     if (ex.nblk > 0 && !(exp_ablate() & 1)) {
         auto launch = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned) (ex.nblk * ex.G)), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
-                               ex.hrow.get(), ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, (int64_t) ex.RB,
-                               ex.nblk, ex.G, ex.hs.get(), ex.hslab.get(), status);
+                               ex.hrow.get(), ex.hjl.get(), ex.hv.get(), ex.hv16.get(), w, m, r0, r1 - r0, ex.nW,
+                               (int64_t) ex.RB, ex.nblk, ex.G, ex.hs.get(), ex.hslab.get(), status);
         };
         auto launch_run = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned) (ex.nblk * ex.G)), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
@@ -1509,11 +1552,20 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
                 default: launch_run(exp_hrun_kernel<T, 16384>);
             }
         } else {
-            switch (ex.RBB) {
-                case 4096: launch(exp_hcell_kernel<T, 4096>); break;
-                case 8192: launch(exp_hcell_kernel<T, 8192>); break;
-                case 32768: launch(exp_hcell_kernel<T, 32768>); break;
-                default: launch(exp_hcell_kernel<T, 16384>);
+            auto pick = [&](auto hb) {
+                constexpr bool HB = decltype(hb)::value;
+                switch (ex.RBB) {
+                    case 4096: launch(exp_hcell_kernel<T, 4096, HB>); break;
+                    case 8192: launch(exp_hcell_kernel<T, 8192, HB>); break;
+                    case 32768: launch(exp_hcell_kernel<T, 32768, HB>); break;
+                    default: launch(exp_hcell_kernel<T, 16384, HB>);
+                }
+            };
+            if constexpr (sizeof(T) == 4) {
+                if (ex.hbf16) pick(std::true_type{});
+                else pick(std::false_type{});
+            } else {
+                pick(std::false_type{});
             }
         }
         MI_LAUNCH_CHECK();

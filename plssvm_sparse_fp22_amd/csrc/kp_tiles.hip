@@ -17,6 +17,8 @@
 //     so a fixed-order second pass makes K·p bitwise reproducible;
 //   * tiles are visited in 8x8 super-blocks (16 panels = 4 MiB in fp64: one XCD's L2) and the
 //     workgroup ids are remapped so each XCD walks a contiguous range of super-blocks.
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace plssvm_mi {
@@ -421,11 +423,10 @@ __global__ __launch_bounds__(256) void kp_reduce_kernel(const T *__restrict__ pa
     raw[i] = s;
 }
 
-// one rank's share (s0, s1 not the whole triangle): raw[i] = sum of the slab values of the rank's own
-// super-blocks. A rank owning the bottom rows of the triangle sees up to nb records per row i, so the
-// column super-blocks are split over the 16 waves of a block (64 rows per block, lanes = rows: coalesced)
-// and the 16 partial sums are added in wave order: a fixed order, deterministic; the critical path per
-// thread is 1/16 of the row (one thread per row made the last rank of 8 4 % slower than the others)
+// raw[i] = sum of the slab values of the super-blocks [s0, s1) (a rank's share, or the whole triangle): the
+// column super-blocks of a row are dealt to the 16 waves of a block (64 rows per block, lanes = rows:
+// coalesced) and the 16 partial sums are added in wave order — a fixed order, deterministic; the critical
+// path per thread is 1/16 of the row (one thread per row is latency-bound)
 constexpr int KP_RED_G = 16;
 template <typename T>
 __global__ __launch_bounds__(64 * KP_RED_G) void kp_reduce_share_kernel(const T *__restrict__ partial, int64_t nb,
@@ -442,8 +443,9 @@ __global__ __launch_bounds__(64 * KP_RED_G) void kp_reduce_share_kernel(const T 
     T s = 0;
     if (i < m) {
         const int64_t q = i % KP_TILE, RS = Ib / KP_SUPER;
-        const int64_t cs0 = g * ns / KP_RED_G, cs1 = (g + 1) * ns / KP_RED_G;
-        for (int64_t CS = cs0; CS < cs1; ++CS) {
+        // column super-blocks dealt round-robin to the waves: a rank's owned super-blocks of a row (often a
+        // short run of CS) spread over the waves instead of landing in one
+        for (int64_t CS = g; CS < ns; CS += KP_RED_G) {
             const int64_t sb = (RS >= CS) ? tri_index(RS, CS) : tri_index(CS, RS);
             if (sb < s0 || sb >= s1) continue;
             const int64_t base = wg_off[sb - s0];
@@ -497,12 +499,19 @@ void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *par
     MI_LAUNCH_CHECK();
 }
 
+// Both the whole triangle and a rank's share use the wave-split reduction (16 waves per 64 rows, each a
+// range of column super-blocks, partial sums added in wave order): one thread per row walking all nb
+// records (kp_reduce_kernel, PLSSVM_MI_KP_REDUCE=1) is latency-bound — 0.43 ms for config 2's 627 MB slab.
 template <typename T>
 void launch_kp_reduce(const T *partial, int64_t nb, int64_t m, int64_t s0, int64_t s1, const int32_t *wg_off, T *raw,
                       const cg_scalars<T> *status, hipStream_t s) {
     if (m <= 0) return;
+    static const bool serial = [] {
+        const char *e = std::getenv("PLSSVM_MI_KP_REDUCE");
+        return e != nullptr && std::atoi(e) == 1;
+    }();
     const int64_t ns = ceil_div(nb, KP_SUPER);
-    if (s0 == 0 && s1 == ns * (ns + 1) / 2) {
+    if (serial && s0 == 0 && s1 == ns * (ns + 1) / 2) {
         hipLaunchKernelGGL(kp_reduce_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, partial, nb, m,
                            wg_off, raw, status);
     } else {

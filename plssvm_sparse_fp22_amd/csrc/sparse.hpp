@@ -72,11 +72,14 @@ struct exp_data {
     bool runs = false;                 // run layout (exp_hrun_kernel): no padding / chunk rows, see expand.hip
     dev_buf<T> hslab;                  // [G][rows] partial row sums of the window groups
     dev_buf<uint16_t> hjl;            // [slots] j - W * CW
-    dev_buf<T> hv;                    // [slots] H_ij
+    dev_buf<T> hv;                    // [slots] H_ij (the real type)
+    dev_buf<uint16_t> hv16;           // [slots] H_ij as bfloat16 (hbf16: see expand.hip, "H storage")
+    bool hbf16 = false;
+    double hratio = -1.0;             // row join: max |H_ij| / |kernel value of the pair| (< 0: unknown)
     dev_buf<uint16_t> hrow;           // [nchunks] block-local row of each 4-slot chunk
     dev_buf<int64_t> woff;            // [nblk][EXP_NWV][nW + 1] first chunk of each (block, wave, window)
     int64_t bytes() const {
-        return mom.bytes() + M.bytes() + hdiag.bytes() + phin.bytes() + wv.bytes() + hs.bytes() + hjl.bytes() + hv.bytes() +
+        return mom.bytes() + M.bytes() + hdiag.bytes() + phin.bytes() + wv.bytes() + hs.bytes() + hjl.bytes() + hv.bytes() + hv16.bytes() +
                hrow.bytes() + woff.bytes() + hslab.bytes();
     }
 };

@@ -469,3 +469,34 @@ def test_expansion_row_join_equals_sort_join(kernel, shape, sim, dtype, monkeypa
     a, b = out["row"][0].astype(np.float64), out["sort"][0].astype(np.float64)
     tol = 1e-14 if dtype == np.float64 else 1e-6
     assert np.abs(a - b).max() <= tol * max(np.abs(b).max(), 1e-300), np.abs(a - b).max()
+
+
+@pytest.mark.parametrize("gamma,want_hbytes", [(None, 2), (0.2, 4)])
+def test_expansion_bf16_remainder_bound(gamma, want_hbytes, monkeypatch):
+    """Remainder storage (expand.hip "H storage"): in a float context H is stored as bfloat16
+    when every stored |H_ij| is at most 2^-15 of its pair's kernel value (1 + E(s) for rbf), so rounding H
+    (relative error <= 2^-9) moves each pair's term by at most 2^-24 of that kernel value — below the float
+    rounding of the kernel value itself. Checked: the default layout is bfloat16 on the BASELINE-like set and
+    the real type when the bound fails (large gamma: H comparable to the kernel value); the kernel sums
+    sum_j k_ij p_j (all terms positive) of both layouts agree to 2^-20 relative, and the overlap sums to
+    2^-9 of sum_j |H_ij| w_j + float rounding."""
+    csr, _ = datagen.sparse_csr(20000, 3000, 20, seed=17, dtype=np.float32)
+    m = csr[3] - 1
+    x = np.random.default_rng(5).uniform(1, 2, m).astype(np.float32)
+    out = {}
+    for fmt in ("auto", "full"):
+        if fmt == "full":
+            monkeypatch.setenv("PLSSVM_MI_EXP_HFMT", "full")
+        else:
+            monkeypatch.delenv("PLSSVM_MI_EXP_HFMT", raising=False)
+        with sparse_svm(csr, "rbf", np.float32, gamma=gamma, algo="expansion") as svm:
+            svm.setup_data_on_device()
+            info = svm.info()
+            out[fmt] = (info["exp_hbytes"], svm.kp_part(x, "kernel").astype(np.float64),
+                        svm.kp_part(x, "overlap").astype(np.float64))
+    assert out["full"][0] == 4
+    assert out["auto"][0] == want_hbytes
+    a, b = out["auto"][1], out["full"][1]
+    assert np.all(np.abs(a - b) <= 2.0 ** -20 * np.abs(b)), np.max(np.abs(a - b) / np.abs(b))
+    if want_hbytes == 4:  # same layout: bitwise
+        np.testing.assert_array_equal(out["auto"][2], out["full"][2])

@@ -7,13 +7,20 @@ which one GPU cannot measure. They are modelled per collective as  t = alpha + b
 algorithms over xGMI; bytes = what one GPU sends: all-gather (G-1)/G x total, all-reduce 2 (G-1)/G x
 total) for a range of RCCL latencies alpha and bus bandwidths beta — an assumption, stated as such.
 
-Collectives per CG iteration (engine.hip / sparse.hip / expand.hip):
-  dense pairwise (replicated CG):   all-reduce of raw (m reals)
-  sparse expansion (sharded CG):    all-gather of w (m reals), all-reduce of the column moments
-                                    (d x KM reals), 3 all-gathers of 2 x 512 dot partials per rank
-  sparse factored linear (sharded): all-reduce of w (d reals), 3 partial all-gathers
+Collectives per CG iteration (engine.hip / sparse.hip / expand.hip) and what hides them:
+  dense pairwise (replicated CG):   all-reduce of raw (m reals), exposed
+  sparse expansion (sharded CG):    all-gather of w (m reals; carries the pending direction partials),
+                                    overlapping the rank's column-moment pass (expansion_kp_raw: the pass
+                                    needs only the rank's own w) -> exposed max(0, t - t_moments);
+                                    all-reduce of the column moments (d x KM reals) on the collective
+                                    stream under the remainder stream -> exposed max(0, t - t_stream);
+                                    2 all-gathers of 2 x 512 dot partials per rank, exposed
+  sparse factored linear (sharded): all-reduce of w (d reals), 2 partial all-gathers, exposed
+t_stream is the share's exp_hcell_kernel launch (roofline.launch_ms of the share record), t_moments the
+column-moment pass of one share (optional argument, microseconds, from the share's kernel stats; 0 = no
+credit).
 
-usage: tools/predict_scaling.py <shares.jsonl> <one-GPU ms per iteration> [KM]
+usage: tools/predict_scaling.py <shares.jsonl> <one-GPU ms per iteration> [KM] [t_moments_us]
 """
 import json
 import sys
@@ -22,15 +29,17 @@ MODELS = [("fast", 8e-6, 200e9), ("mid", 12e-6, 150e9), ("slow", 20e-6, 100e9)]
 
 
 def collectives(rec, G, km):
+    """(kind, bytes of the collective's whole buffer, name of the share's work that hides it or None)"""
     cfg = rec["config"]
     m, d = cfg["N"] - 1, cfg["d"]
     s = 8 if rec["dtype"] == "f64" else 4
     tiny = 2 * 512 * s * G  # gathered partials (bytes of the gathered buffer)
     if cfg["layout"] == "dense" and cfg["kp_mode"] == "pairwise":
-        return [("allreduce", m * s)]
+        return [("allreduce", m * s, None)]
     if cfg["kp_mode"] == "factored":
-        return [("allreduce", d * s)] + [("allgather", tiny)] * 3
-    return [("allgather", m * s), ("allreduce", d * km * s)] + [("allgather", tiny)] * 3
+        return [("allreduce", d * s, None)] + [("allgather", tiny, None)] * 2
+    return [("allgather", m * s + tiny, "moments"), ("allreduce", d * km * s, "stream")] + \
+        [("allgather", tiny, None)] * 2
 
 
 def t_coll(kind, total, G, alpha, beta):
@@ -42,13 +51,20 @@ def main():
     rows = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")]
     one = float(sys.argv[2])
     km = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    t_mom = float(sys.argv[4]) * 1e-6 if len(sys.argv) > 4 else 0.0
     G = len(rows)
     ms = [r["ms_per_step"] for r in rows]
     out = {"config": rows[0]["config"]["workload"], "W": G, "ms_per_step_by_rank": ms, "max_share_ms": max(ms),
            "one_gpu_ms": one, "predictions": {}}
     for name, alpha, beta in MODELS:
-        c = sum(t_coll(k, b, G, alpha, beta) for k, b in collectives(rows[0], G, km)) * 1e3
-        t = max(ms) + c
+        c = 0.0
+        for r in rows:  # the slowest rank's share + its exposed collective time
+            hide = {"moments": t_mom, "stream": r["roofline"].get("launch_ms", 0.0) * 1e-3
+                    if r["roofline"].get("kernel") == "exp_hcell_kernel" else 0.0, None: 0.0}
+            exp = sum(max(0.0, t_coll(k, b, G, alpha, beta) - hide[h]) for k, b, h in collectives(r, G, km))
+            c = max(c, r["ms_per_step"] + exp * 1e3)
+        t = c
+        c = t - max(ms)
         out["predictions"][name] = {"alpha_us": alpha * 1e6, "beta_GBps": beta / 1e9, "collectives_ms": round(c, 4),
                                     "iteration_ms": round(t, 4), "speedup": round(one / t, 2)}
     print(json.dumps(out))
