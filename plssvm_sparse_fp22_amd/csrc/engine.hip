@@ -336,7 +336,7 @@ void engine<T>::finish_setup() {
         v0 = shard ? r0 : 0;
         vn = shard ? r1 - r0 : m;
         G = gathered ? world : 1;
-        if (gathered) cgp_g.alloc(4 * (int64_t) G * 2 * RED_BLOCKS, stream);
+        if (gathered) cgp_g.alloc(5 * (int64_t) G * 2 * RED_BLOCKS, stream);
     }
     tiles_upload();
     if (!sparse && !factored()) {

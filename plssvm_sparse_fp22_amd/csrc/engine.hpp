@@ -81,7 +81,7 @@ struct engine : engine_base {
                             // inputs move through the group's transport
     int64_t v0 = 0, vn = 0;
     int G = 1;
-    dev_buf<T> cgp_g;      // gathered partials, slots [4][G][2 RED_BLOCKS]: sum d / sum q d, d.Ad, r.r, kp sums
+    dev_buf<T> cgp_g;      // gathered partials, slots [5][G][2 RED_BLOCKS]: sum d / sum q d, d.Ad, r.r, kp sums, S
     std::vector<T> xpart;  // host staging of the host exchange's partial gathers
     const T *gather_partials(T *local, int slot);
     // RCCL group: the sum d / sum q d partials of a CG step ride with the next collective of the K·p
@@ -168,6 +168,8 @@ struct engine : engine_base {
     void expansion_dominant(const T *p, const cg_scalars<T> *status);  // the remainder stream
     void expansion_moments(const T *w, const cg_scalars<T> *status);   // column moments (SELL CSC pass)
     void expansion_mscale(const cg_scalars<T> *status);                 // moments -> Horner coefficients
+    bool expansion_moment_pass(const T *w, const cg_scalars<T> *status); // true: reduced straight into M
+    coefs expansion_coefs() const;
     // predict through the expansion (expand.hip); false: not applicable, predict brute force
     bool expansion_predict(const T *alpha_dev, T alpha_m, T bias, const int64_t *zr_dev, const int32_t *zc_dev,
                            const T *zv_dev, int64_t np, int64_t max_nnz_z, double zabs_max, double znorm_max, T nlast,

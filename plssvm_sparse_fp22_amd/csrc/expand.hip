@@ -34,6 +34,7 @@ namespace plssvm_mi {
 namespace {
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 // phi in double: the exact per-pair function (rbf: expm1(2 g a); poly: sum_k bin_k a^k, no cancellation)
@@ -47,10 +48,6 @@ struct phi_fn {
         for (int k = deg; k >= 1; --k) h = (h + bin[k]) * a;
         return h;
     }
-};
-
-struct coefs {
-    double c[EXP_KMAX + 1];
 };
 
 struct d2sum {
@@ -468,6 +465,42 @@ __global__ __launch_bounds__(256) void exp_mscale_kernel(const T *__restrict__ m
     M[t] = (T) (cf.c[k + 1] * (double) mom[(int64_t) k * d + f]);
 }
 
+// the moment pass's P panel slabs reduced straight into the Horner coefficients: M[f][k] = coef_{k+1} sum_q
+// partial[q][k d + f], the sum in panel_reduce_kernel's order (quarters combined in order when split), so M is
+// bitwise that of panel_reduce + exp_mscale_kernel — one launch fewer per K·p
+template <typename T>
+__global__ __launch_bounds__(256) void exp_mom_reduce_kernel(const T *__restrict__ partial, int64_t P, int64_t d, int kc,
+                                                             int split, coefs cf, T *__restrict__ M,
+                                                             const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    __shared__ T part[3][64];
+    const int64_t ns = d * kc;
+    const int lane = split ? (threadIdx.x & 63) : threadIdx.x, quarter = split ? (threadIdx.x >> 6) : 0;
+    const int64_t s = (int64_t) blockIdx.x * (split ? 64 : 256) + lane;
+    const int64_t per = split ? (P + 3) / 4 : P, q0 = quarter * per, q1 = min(P, q0 + per);
+    T a = 0;
+    if (s < ns) {
+        int64_t q = q0;
+        for (; q + 8 <= q1; q += 8) {
+            T v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = partial[(q + u) * ns + s];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a += v[u];
+        }
+        for (; q < q1; ++q) a += partial[q * ns + s];
+    }
+    if (split) {
+        if (quarter > 0) part[quarter - 1][lane] = a;
+        __syncthreads();
+        if (quarter != 0) return;
+        a = ((a + part[0][lane]) + part[1][lane]) + part[2][lane];
+    }
+    if (s >= ns) return;
+    const int64_t k = s / d, f = s % d;
+    M[f * kc + k] = (T) (cf.c[k + 1] * (double) a);
+}
+
 // ---- remainder stream layout (built from the padded symmetric rows) ---------------------------------------
 // count index of (row r, window W): ((I NWV + v) nW + W) RPW + rr,  r = I RB + v RPW + rr
 __device__ __forceinline__ int64_t exp_cidx(int64_t r, int64_t W, int64_t nW, int64_t RB) {
@@ -503,6 +536,62 @@ __device__ __forceinline__ uint16_t bf16_rne(float f) {
     uint32_t u = __float_as_uint(f);
     u += 0x7FFFu + ((u >> 16) & 1u);
     return (uint16_t) (u >> 16);
+}
+
+// S = sum_j w_j as RED_BLOCKS block partials in dot2_kernel's grid, order and block reduction (bitwise the
+// same partials), writing the remainder stream's bfloat16 copy of w on the way (w16 non-null: hbf16 layouts)
+template <typename T>
+__global__ __launch_bounds__(256) void exp_wsum_kernel(const T *__restrict__ w, int64_t n, uint16_t *__restrict__ w16,
+                                                       T *__restrict__ partials, const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    __shared__ T red[4];
+    T s1 = 0;
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        const T v = w[i];
+        s1 += v;
+        if (w16 != nullptr) w16[i] = bf16_rne((float) v);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s1 += __shfl_xor(s1, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T t = 0;
+        for (int v = 0; v < 4; ++v) t += red[v];
+        partials[blockIdx.x] = t;
+        partials[RED_BLOCKS + blockIdx.x] = T(0);
+    }
+}
+
+// sharded groups with bfloat16 windows: the rank's rows only — w_i = e_i p_i (rbf; e null: w = p, nothing
+// written), its bfloat16 copy, and the rows' share of S = sum_j w_j as RED_BLOCKS block partials (gathered
+// with the group's other partials and summed in rank order: the same S on every rank)
+template <typename T>
+__global__ __launch_bounds__(256) void exp_wown_kernel(const T *__restrict__ e, const T *__restrict__ p, int64_t ib,
+                                                       int64_t ie, T *__restrict__ w, uint16_t *__restrict__ w16,
+                                                       T *__restrict__ partials, const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    __shared__ T red[4];
+    T s1 = 0;
+    for (int64_t i = ib + (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < ie; i += (int64_t) gridDim.x * blockDim.x) {
+        T v = p[i];
+        if (e != nullptr) {
+            v = e[i] * v;
+            w[i] = v;
+        }
+        s1 += v;
+        w16[i] = bf16_rne((float) v);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) s1 += __shfl_xor(s1, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        T t = 0;
+        for (int v = 0; v < 4; ++v) t += red[v];
+        partials[blockIdx.x] = t;
+        partials[RED_BLOCKS + blockIdx.x] = T(0);
+    }
 }
 
 template <typename T>
@@ -651,18 +740,24 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
                                                                  const uint16_t *__restrict__ hjl,
                                                                  const T *__restrict__ hv,
                                                                  const uint16_t *__restrict__ hv16, const T *__restrict__ w,
+                                                                 const uint16_t *__restrict__ w16,
                                                                  int64_t m, int64_t r0, int64_t R, int64_t nW,
                                                                  int64_t RB, int64_t nI, int G, T *__restrict__ hs,
                                                                  T *__restrict__ hslab,
                                                                  const cg_scalars<T> *__restrict__ status) {
     // RB (rows per block, a multiple of 16) <= RBC, the accumulator's capacity. G > 1 window groups:
     // block (I, g) streams only windows [g nW / G, (g + 1) nW / G) of its rows and writes its row sums
-    // to hslab[g][rows] (summed in g order by exp_hslab_reduce_kernel); the blocks of one XCD share g,
+    // to hslab[g][rows] (summed in g order by exp_combine_kernel); the blocks of one XCD share g,
     // so they share w's windows in L2
-    constexpr int CW = exp_cw_of<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64;
+    // HB: H and the window of w in bfloat16 (twice the partners per window; expand.hip "H storage")
+    using WT = std::conditional_t<HB, uint16_t, T>;
+    constexpr int CW = HB ? exp_cw16_of<RBB>() : exp_cw_of<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64;
     static_assert(CW <= 65536, "window-local partner indices are 16-bit");
-    __shared__ __attribute__((aligned(16))) T wl[CW];
+    __shared__ __attribute__((aligned(16))) WT wl[CW];
     __shared__ T racc[RBC];
+    const WT *wsrc;
+    if constexpr (HB) wsrc = w16;
+    else wsrc = w;
     if (status != nullptr && status->converged) return;
     const int64_t bx = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t I = bx % nI, g = bx / nI;
@@ -670,8 +765,8 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int t = tid; t < RB; t += NT) racc[t] = T(0);
     // the window of w moves as 16-byte vectors: thread tid takes vectors tid, tid + NT, ... (PV of them)
-    constexpr int VE = 16 / (int) sizeof(T), NV = CW / VE, PV = (NV + NT - 1) / NT;
-    using wvec = __attribute__((ext_vector_type(VE))) T;
+    constexpr int VE = 16 / (int) sizeof(WT), NV = CW / VE, PV = (NV + NT - 1) / NT;
+    using wvec = __attribute__((ext_vector_type(VE))) WT;
     wvec reg[PV];
     auto load_win = [&](int64_t W) {
 #pragma unroll
@@ -680,13 +775,17 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             if (NV % NT == 0 || v < NV) {
                 const int64_t idx = W * CW + (int64_t) v * VE;
                 if (idx + VE <= m) {
-                    reg[q] = *reinterpret_cast<const wvec *>(w + idx);
+                    reg[q] = *reinterpret_cast<const wvec *>(wsrc + idx);
                 } else {
 #pragma unroll
-                    for (int e = 0; e < VE; ++e) reg[q][e] = idx + e < m ? w[idx + e] : T(0);
+                    for (int e = 0; e < VE; ++e) reg[q][e] = idx + e < m ? wsrc[idx + e] : WT(0);
                 }
             }
         }
+    };
+    auto wat = [&](uint32_t j) -> T {  // w_j from the staged window
+        if constexpr (HB) return (T) __uint_as_float((uint32_t) wl[j] << 16);
+        else return wl[j];
     };
     auto store_win = [&]() {
 #pragma unroll
@@ -727,7 +826,6 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     for (int64_t W = W0; W < W1; ++W) {
         if (W + 1 < W1) load_win(W + 1);  // lands in registers while this window is processed
         const int64_t c_end = wo[W + 1];
-        const T *wb = wl;
         for (int64_t cb = wo[W]; cb < c_end; cb += 64) {  // wave-uniform trip count
             const bool have = cb + lane < c_end;
             const int rl = have ? rl_n : -1;
@@ -741,10 +839,10 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             }
             T acc = T(0);
             if (have) {
-                acc = h0 * wb[jj.x & 0xFFFFu];
-                acc = fma(h1, wb[jj.x >> 16], acc);
-                acc = fma(h2, wb[jj.y & 0xFFFFu], acc);
-                acc = fma(h3, wb[jj.y >> 16], acc);
+                acc = h0 * wat(jj.x & 0xFFFFu);
+                acc = fma(h1, wat(jj.x >> 16), acc);
+                acc = fma(h2, wat(jj.y & 0xFFFFu), acc);
+                acc = fma(h3, wat(jj.y >> 16), acc);
             }
 #if EXP_DPP
             // segmented inclusive prefix sums over the lanes by DPP (rows are non-decreasing in lane order):
@@ -804,6 +902,8 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *_
                                                                 T *__restrict__ hslab,
                                                                 const cg_scalars<T> *__restrict__ status) {
     constexpr int CW = exp_cw_run<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64;
+    using WT = T;  // the run layout keeps the real type
+    const T *wsrc = w;
     __shared__ __attribute__((aligned(16))) T wl[CW];
     __shared__ T racc[RBC];
     if (status != nullptr && status->converged) return;
@@ -815,8 +915,8 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *_
     for (int t = tid; t < RB; t += NT) racc[t] = T(0);
     T *ra = racc + wave * RPW;
     // the window of w moves as 16-byte vectors: thread tid takes vectors tid, tid + NT, ... (PV of them)
-    constexpr int VE = 16 / (int) sizeof(T), NV = CW / VE, PV = (NV + NT - 1) / NT;
-    using wvec = __attribute__((ext_vector_type(VE))) T;
+    constexpr int VE = 16 / (int) sizeof(WT), NV = CW / VE, PV = (NV + NT - 1) / NT;
+    using wvec = __attribute__((ext_vector_type(VE))) WT;
     wvec reg[PV];
     auto load_win = [&](int64_t W) {
 #pragma unroll
@@ -825,10 +925,10 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *_
             if (NV % NT == 0 || v < NV) {
                 const int64_t idx = W * CW + (int64_t) v * VE;
                 if (idx + VE <= m) {
-                    reg[q] = *reinterpret_cast<const wvec *>(w + idx);
+                    reg[q] = *reinterpret_cast<const wvec *>(wsrc + idx);
                 } else {
 #pragma unroll
-                    for (int e = 0; e < VE; ++e) reg[q][e] = idx + e < m ? w[idx + e] : T(0);
+                    for (int e = 0; e < VE; ++e) reg[q][e] = idx + e < m ? wsrc[idx + e] : WT(0);
                 }
             }
         }
@@ -944,24 +1044,13 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *_
     }
 }
 
-// hs[r0 + i] = sum_g hslab[g][i], g in order
-template <typename T>
-__global__ __launch_bounds__(256) void exp_hslab_reduce_kernel(const T *__restrict__ hslab, int64_t R, int G, int64_t r0,
-                                                               T *__restrict__ hs, const cg_scalars<T> *__restrict__ status) {
-    if (status != nullptr && status->converged) return;
-    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= R) return;
-    T a = 0;
-    for (int g = 0; g < G; ++g) a += hslab[g * R + i];
-    hs[r0 + i] = a;
-}
-
 // raw_i for rows [r0, r1) (0 elsewhere), raw holding J_i there (the CSR pass): base + scale (J_i +
-// H_ii w_i + hs_i) [- the diagonal's pair part when only the overlap part is asked for], in fp64
+// H_ii w_i + hs_i, hs_i = the remainder stream's row sum) [- the diagonal's pair part when only the overlap part is asked for], in fp64
 template <typename T>
 __global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ e, const T *__restrict__ w,
                                                           const T *__restrict__ hdiag, const T *__restrict__ phin,
-                                                          const T *__restrict__ hs, const T *__restrict__ ssc, T kappa,
+                                                          const T *__restrict__ hs, const T *__restrict__ hslab, int G,
+                                                          const T *__restrict__ ssc, T kappa,
                                                           int64_t ib, int64_t ie, int64_t r0, int64_t r1, int overlap_only,
                                                           T *__restrict__ raw, const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
@@ -972,7 +1061,13 @@ __global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ 
         return;
     }
     const double wi = (double) w[i];
-    const double t = (double) raw[i] + (double) hdiag[i] * wi + (double) hs[i];
+    T h = 0;  // the remainder stream's row sum (G window groups: their slabs in g order)
+    if (G > 1) {
+        for (int g = 0; g < G; ++g) h += hslab[(int64_t) g * (r1 - r0) + (i - r0)];
+    } else {
+        h = hs[i];
+    }
+    const double t = (double) raw[i] + (double) hdiag[i] * wi + (double) h;
     const double sc = e != nullptr ? (double) e[i] : 1.0;
     double v;
     if (overlap_only) {
@@ -1471,7 +1566,15 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
             }
         }
         if (!ex.runs) {
-            ex.CW = exp_cw_host(ex.RBB, (int) sizeof(T));
+            // H storage (float contexts): bfloat16 H and bfloat16 windows of w when every stored |H_ij| is at most
+            // 2^-16 of its pair's kernel value (row join's hratio). H_ij w_j is then formed from two values with
+            // relative error <= 2^-9 each, so each pair's term moves by at most ~2^-8 |H_ij w_j| <= 2^-24 of
+            // the pair's k_ij w_j — the float rounding of that term itself. PLSSVM_MI_EXP_HFMT=full keeps the
+            // real type. The bfloat16 window holds twice the partners (fewer windows, fewer padded cells).
+            const char *hf = std::getenv("PLSSVM_MI_EXP_HFMT");
+            ex.hbf16 = sizeof(T) == 4 && ex.hratio >= 0.0 && ex.hratio <= std::ldexp(1.0, -16) &&
+                       !(hf != nullptr && std::strcmp(hf, "full") == 0);
+            ex.CW = ex.hbf16 ? exp_cw16_host(ex.RBB) : exp_cw_host(ex.RBB, (int) sizeof(T));
             ex.nW = ceil_div(std::max<int64_t>(m, 1), (int64_t) ex.CW);
             const int64_t CW = ex.CW, ncnt = ex.nblk * RB * ex.nW;
             cnt.alloc(ncnt + 1, stream);
@@ -1484,14 +1587,10 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
             scan(ncnt);
             ex.nchunks = ex.slots / 4;
             ex.hjl.alloc(std::max<int64_t>(ex.slots, 4), stream);
-            // H storage (float contexts): bfloat16 when every stored |H_ij| is at most 2^-15 of its pair's kernel
-            // value (row join's hratio) — rounding H to 8 mantissa bits (relative error <= 2^-9) then moves each
-            // pair's term by at most 2^-24 of the pair's kernel value, below the float rounding of that value
-            // itself; PLSSVM_MI_EXP_HFMT=full keeps the real type
-            const char *hf = std::getenv("PLSSVM_MI_EXP_HFMT");
-            ex.hbf16 = sizeof(T) == 4 && ex.hratio >= 0.0 && ex.hratio <= std::ldexp(1.0, -15) &&
-                       !(hf != nullptr && std::strcmp(hf, "full") == 0);
-            if (ex.hbf16) ex.hv16.alloc(std::max<int64_t>(ex.slots, 4), stream);
+            if (ex.hbf16) {
+                ex.hv16.alloc(std::max<int64_t>(ex.slots, 4), stream);
+                ex.wv16.alloc(round_up(std::max<int64_t>({ m, chunk * G, 8 }), (int64_t) 8), stream);
+            }
             else ex.hv.alloc(std::max<int64_t>(ex.slots, 4), stream);
             ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
             if (R > 0) {
@@ -1536,7 +1635,7 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
     if (ex.nblk > 0 && !(exp_ablate() & 1)) {
         auto launch = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned) (ex.nblk * ex.G)), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
-                               ex.hrow.get(), ex.hjl.get(), ex.hv.get(), ex.hv16.get(), w, m, r0, r1 - r0, ex.nW,
+                               ex.hrow.get(), ex.hjl.get(), ex.hv.get(), ex.hv16.get(), w, ex.wv16.get(), m, r0, r1 - r0, ex.nW,
                                (int64_t) ex.RB, ex.nblk, ex.G, ex.hs.get(), ex.hslab.get(), status);
         };
         auto launch_run = [&](auto kern) {
@@ -1568,26 +1667,49 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
                 pick(std::false_type{});
             }
         }
-        MI_LAUNCH_CHECK();
-        if (ex.G > 1 && r1 > r0) {
-            hipLaunchKernelGGL(exp_hslab_reduce_kernel<T>, dim3((unsigned) ceil_div(r1 - r0, 256)), dim3(256), 0, stream,
-                               ex.hslab.get(), r1 - r0, ex.G, r0, ex.hs.get(), status);
-            MI_LAUNCH_CHECK();
-        }
+        MI_LAUNCH_CHECK();  // G > 1: the row sums stay in hslab, summed in g order by exp_combine_kernel
     } else if (r1 > r0) {
         MI_HIP_CHECK(hipMemsetAsync(ex.hs.get() + r0, 0, sizeof(T) * (size_t) (r1 - r0), stream));
+        if (ex.G > 1) MI_HIP_CHECK(hipMemsetAsync(ex.hslab.get(), 0, sizeof(T) * (size_t) (ex.G * (r1 - r0)), stream));
     }
+}
+
+// the column-moment pass (SELL CSC pass, mode 1) over rows [csc_r0, csc_r1); several panels: their slabs are
+// reduced straight into the scaled Horner coefficients M (returns true), one panel: the pass wrote the raw
+// moments mom, scaled by expansion_mscale after the group's all-reduce (returns false)
+template <typename T>
+bool engine<T>::expansion_moment_pass(const T *w, const cg_scalars<T> *status) {
+    auto &ex = csr.ex;
+    const auto &pl = csr.spmv_csc;
+    const bool fused = pl.P > 1 && pl.nseg == d && pl.nblocks > 0;
+    launch_panel_spmv<T>(pl, w + csr.csc_r0, csr.csc_r1 - csr.csc_r0, ex.mom.get(), status, stream, ex.KM, 1, !fused);
+    if (fused) {
+        const int split = pl.P >= 16 ? 1 : 0;
+        hipLaunchKernelGGL(exp_mom_reduce_kernel<T>, dim3((unsigned) ceil_div(d * ex.KM, split ? 64 : 256)), dim3(256), 0,
+                           stream, pl.partial.get(), pl.P, d, ex.KM, split, expansion_coefs(), ex.M.get(), status);
+        MI_LAUNCH_CHECK();
+    }
+    return fused;
 }
 
 template <typename T>
 void engine<T>::expansion_moments(const T *w, const cg_scalars<T> *status) {
     auto &ex = csr.ex;
-    if (d > 0) {  // column moments: one SELL pass over the CSC (mode 1), then the coefficients
-        // (a real group: each rank's rows, then one all-reduce of the d x K moments)
-        launch_panel_spmv<T>(csr.spmv_csc, w + csr.csc_r0, csr.csc_r1 - csr.csc_r0, ex.mom.get(), status, stream, ex.KM, 1);
-        if (csr.csc_r1 - csr.csc_r0 < m) allreduce(ex.mom.get(), d * ex.KM);
-        expansion_mscale(status);
+    if (d > 0) {  // column moments, then the coefficients (a real group: each rank's rows, then one
+        // all-reduce of the d x K values — linear, so the scaled coefficients are all-reduced when fused)
+        const bool fused = expansion_moment_pass(w, status);
+        if (csr.csc_r1 - csr.csc_r0 < m) allreduce(fused ? ex.M.get() : ex.mom.get(), d * ex.KM);
+        if (!fused) expansion_mscale(status);
     }
+}
+
+template <typename T>
+coefs engine<T>::expansion_coefs() const {
+    coefs cf;
+    std::memcpy(cf.c, csr.ex.coef, sizeof(cf.c));
+    if (exp_ablate() & 2)
+        for (int k = 2; k <= EXP_KMAX; ++k) cf.c[k] = 0.0;
+    return cf;
 }
 
 // M[f][k] = coef_{k+1} mom[k][f] (after the group's all-reduce of the moments)
@@ -1595,12 +1717,8 @@ template <typename T>
 void engine<T>::expansion_mscale(const cg_scalars<T> *status) {
     auto &ex = csr.ex;
     if (d <= 0) return;
-    coefs cf;
-    std::memcpy(cf.c, ex.coef, sizeof(cf.c));
-    if (exp_ablate() & 2)
-        for (int k = 2; k <= EXP_KMAX; ++k) cf.c[k] = 0.0;
     hipLaunchKernelGGL(exp_mscale_kernel<T>, dim3((unsigned) ceil_div(d * ex.KM, 256)), dim3(256), 0, stream,
-                       ex.mom.get(), d, ex.KM, cf, ex.M.get(), status);
+                       ex.mom.get(), d, ex.KM, expansion_coefs(), ex.M.get(), status);
     MI_LAUNCH_CHECK();
 }
 
@@ -1611,38 +1729,70 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     // all rows); the raw of this rank's rows stays local (no row gather)
     const int64_t ib = shard ? r0 : 0, ie = shard ? r1 : m;
     const T *w = p;
-    if (kernel == 2) {
+    // sharded RCCL group with bfloat16 windows: the bfloat16 w (2 B per row) is what the group gathers
+    // (a simulated rank of such a group runs the same kernels without the collectives: timing only)
+    const bool rgrp = shard && comm != nullptr && cstream != nullptr && d > 0;
+    const bool g16 = shard && d > 0 && ex.hbf16 && (rgrp || sim_world > 0);
+    if (g16) {
+        hipLaunchKernelGGL(exp_wown_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, stream, kernel == 2 ? csr.e.get() : nullptr,
+                           p, ib, ie, ex.wv.get(), ex.wv16.get(), red.get(), status);
+        MI_LAUNCH_CHECK();
+        if (kernel == 2) w = ex.wv.get();
+    } else if (kernel == 2) {
         if (ie > ib)
             hipLaunchKernelGGL(exp_w_kernel<T>, dim3((unsigned) ceil_div(ie - ib, 256)), dim3(256), 0, stream,
                                csr.e.get() + ib, p + ib, ie - ib, ex.wv.get() + ib, status);
         MI_LAUNCH_CHECK();
         w = ex.wv.get();
     }
-    if (shard && comm != nullptr && cstream != nullptr && d > 0) {
+    if (rgrp) {
         // sharded RCCL group: the all-gather of w (with the pending CG partials) and the all-reduce of the
         // moments run on the collective stream, overlapping the moments pass and the remainder stream
         MI_HIP_CHECK(hipEventRecord(cev[0], stream));
         MI_HIP_CHECK(hipStreamWaitEvent(cstream, cev[0], 0));
-        psum_group_begin(cstream);
-        MI_NCCL_CHECK(ncclAllGather(const_cast<T *>(w) + (int64_t) rank * chunk, const_cast<T *>(w), (size_t) chunk,
-                                    nccl_type<T>(), comm, cstream));
-        psum_group_end();
+        MI_NCCL_CHECK(ncclGroupStart());
+        if (psum_pending) {  // the previous CG step's direction partials ride along
+            MI_NCCL_CHECK(ncclAllGather(cgp.get(), cgp_g.get(), (size_t) (2 * RED_BLOCKS), nccl_type<T>(), comm, cstream));
+            psum_pending = false;
+        }
+        T *sg = cgp_g.get() + (int64_t) 4 * G * 2 * RED_BLOCKS;  // slot 4: the ranks' S partials
+        if (g16) {
+            MI_NCCL_CHECK(ncclAllGather(ex.wv16.get() + (int64_t) rank * chunk, ex.wv16.get(), (size_t) chunk, ncclBfloat16,
+                                        comm, cstream));
+            MI_NCCL_CHECK(ncclAllGather(red.get(), sg, (size_t) (2 * RED_BLOCKS), nccl_type<T>(), comm, cstream));
+        } else {
+            MI_NCCL_CHECK(ncclAllGather(const_cast<T *>(w) + (int64_t) rank * chunk, const_cast<T *>(w), (size_t) chunk,
+                                        nccl_type<T>(), comm, cstream));
+        }
+        MI_NCCL_CHECK(ncclGroupEnd());
         MI_HIP_CHECK(hipEventRecord(cev[1], cstream));
-        launch_panel_spmv<T>(csr.spmv_csc, w + csr.csc_r0, csr.csc_r1 - csr.csc_r0, ex.mom.get(), status, stream, ex.KM, 1);
+        const bool fused = expansion_moment_pass(w, status);
+        T *mt = fused ? ex.M.get() : ex.mom.get();
         MI_HIP_CHECK(hipEventRecord(cev[2], stream));
         MI_HIP_CHECK(hipStreamWaitEvent(cstream, cev[2], 0));
-        MI_NCCL_CHECK(ncclAllReduce(ex.mom.get(), ex.mom.get(), (size_t) (d * ex.KM), nccl_type<T>(), ncclSum,
-                                    comm, cstream));
+        MI_NCCL_CHECK(ncclAllReduce(mt, mt, (size_t) (d * ex.KM), nccl_type<T>(), ncclSum, comm, cstream));
         MI_HIP_CHECK(hipEventRecord(cev[3], cstream));
         MI_HIP_CHECK(hipStreamWaitEvent(stream, cev[1], 0));  // w of every rank
-        launch_dot2<T>(w, nullptr, nullptr, nullptr, m, red.get(), status, stream);  // S = sum_j w_j
-        launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+        if (g16) {  // S from the ranks' partials, in rank order
+            launch_dot_final<T>(sg, sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream, G);
+        } else {
+            hipLaunchKernelGGL(exp_wsum_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, stream, w, m,
+                               ex.hbf16 ? ex.wv16.get() : nullptr, red.get(), status);  // S = sum_j w_j (+ bf16 w)
+            MI_LAUNCH_CHECK();
+            launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+        }
         expansion_dominant(w, status);
         MI_HIP_CHECK(hipStreamWaitEvent(stream, cev[3], 0));  // the group's moments
-        expansion_mscale(status);
+        if (!fused) expansion_mscale(status);
+    } else if (g16) {
+        launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+        expansion_moments(w, status);
+        expansion_dominant(w, status);
     } else {
         gather_input(w);
-        launch_dot2<T>(w, nullptr, nullptr, nullptr, m, red.get(), status, stream);  // S = sum_j w_j
+        hipLaunchKernelGGL(exp_wsum_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, stream, w, m,
+                           ex.hbf16 ? ex.wv16.get() : nullptr, red.get(), status);  // S = sum_j w_j (+ bf16 w)
+        MI_LAUNCH_CHECK();
         launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
         expansion_moments(w, status);
         expansion_dominant(w, status);
@@ -1657,6 +1807,7 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     if (ie > ib)
         hipLaunchKernelGGL(exp_combine_kernel<T>, dim3((unsigned) ceil_div(ie - ib, 256)), dim3(256), 0, stream,
                            kernel == 2 ? csr.e.get() : nullptr, w, ex.hdiag.get(), ex.phin.get(), ex.hs.get(),
+                           ex.G > 1 ? ex.hslab.get() : nullptr, ex.G,
                            csr.ssc.get(), kappa, ib, ie, r0, r1, with_base ? 0 : 1, raw.get(), status);
     MI_LAUNCH_CHECK();
     if (!shard) allgather_rows(raw.get());
@@ -1946,6 +2097,8 @@ bool engine<T>::expansion_predict(const T *alpha_dev, T alpha_m, T bias, const i
     template void engine<T>::expansion_dominant(const T *, const cg_scalars<T> *);           \
     template void engine<T>::expansion_moments(const T *, const cg_scalars<T> *);            \
     template void engine<T>::expansion_mscale(const cg_scalars<T> *);                        \
+    template bool engine<T>::expansion_moment_pass(const T *, const cg_scalars<T> *);        \
+    template coefs engine<T>::expansion_coefs() const;                                       \
     template void engine<T>::expansion_kp_raw(const T *, const cg_scalars<T> *, bool);      \
     template bool engine<T>::expansion_predict(const T *, T, T, const int64_t *, const int32_t *, const T *, int64_t, \
                                                int64_t, double, double, T, T *);

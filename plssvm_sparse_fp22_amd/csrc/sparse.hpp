@@ -45,10 +45,20 @@ constexpr int exp_rb_of() { return RBB / (int) sizeof(T); }
 template <typename T, int RBB>
 constexpr int exp_cw_of() { return (EXP_LDS - RBB) / (int) sizeof(T) / 1024 * 1024; }
 inline int exp_cw_host(int rbb, int es) { return (EXP_LDS - rbb) / es / 1024 * 1024; }
+// bfloat16 windows (hbf16, expand.hip "H storage"): twice the partners in the same LDS, at most 65536
+// (16-bit window-local j)
+template <int RBB>
+constexpr int exp_cw16_of() { return (EXP_LDS - RBB) / 2 / 1024 * 1024 < 65536 ? (EXP_LDS - RBB) / 2 / 1024 * 1024 : 65536; }
+inline int exp_cw16_host(int rbb) { return std::min((EXP_LDS - rbb) / 2 / 1024 * 1024, 65536); }
 // the run layout keeps a flag in bit 15 of the window-local j: windows of at most 32768 partners
 template <typename T, int RBB>
 constexpr int exp_cw_run() { return exp_cw_of<T, RBB>() < 32768 ? exp_cw_of<T, RBB>() : 32768; }
 inline int exp_cw_run_host(int rbb, int es) { return exp_cw_host(rbb, es) < 32768 ? exp_cw_host(rbb, es) : 32768; }
+
+// phi's polynomial coefficients (kernel argument of the moment / Horner kernels)
+struct coefs {
+    double c[EXP_KMAX + 1];
+};
 
 template <typename T>
 struct exp_data {
@@ -74,12 +84,13 @@ struct exp_data {
     dev_buf<uint16_t> hjl;            // [slots] j - W * CW
     dev_buf<T> hv;                    // [slots] H_ij (the real type)
     dev_buf<uint16_t> hv16;           // [slots] H_ij as bfloat16 (hbf16: see expand.hip, "H storage")
+    dev_buf<uint16_t> wv16;           // [m] the stream's partner weights w_j as bfloat16 (hbf16)
     bool hbf16 = false;
     double hratio = -1.0;             // row join: max |H_ij| / |kernel value of the pair| (< 0: unknown)
     dev_buf<uint16_t> hrow;           // [nchunks] block-local row of each 4-slot chunk
     dev_buf<int64_t> woff;            // [nblk][EXP_NWV][nW + 1] first chunk of each (block, wave, window)
     int64_t bytes() const {
-        return mom.bytes() + M.bytes() + hdiag.bytes() + phin.bytes() + wv.bytes() + hs.bytes() + hjl.bytes() + hv.bytes() + hv16.bytes() +
+        return mom.bytes() + M.bytes() + hdiag.bytes() + phin.bytes() + wv.bytes() + hs.bytes() + hjl.bytes() + hv.bytes() + hv16.bytes() + wv16.bytes() +
                hrow.bytes() + woff.bytes() + hslab.bytes();
     }
 };
