@@ -159,8 +159,8 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
         it, conv, batch = 0, False, 4
         while not conv and it < d and time.perf_counter() - t_cg0 < solve_cap_s:
             # solve_cg's polling: batches of 4, 8, 16, ... up to the first reset, then 50-iteration blocks
-            n = min(batch, 50 - it % 50, d - it) if it < 50 else min(50 - it % 50, d - it)
-            it, conv = svm.cg_step(n)
+            nstep = min(batch, 50 - it % 50, d - it) if it < 50 else min(50 - it % 50, d - it)
+            it, conv = svm.cg_step(nstep)
             batch *= 2
         t_cg = time.perf_counter() - t_cg0
         _, tr, _ = svm.cg_result(min(it + 1, 4096))
@@ -327,7 +327,8 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
             moved = info["spmv_bytes"]  # what the two SELL passes actually stream (16-bit panel indices)
             return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
                         frac=alg / s / PEAKS["hbm"], traffic=None, kernel=kname, launch_ms=ms_dom, alg_bytes=alg,
-                        stream_bytes_per_launch=moved, stream_GBps=moved / s / 1e9)
+                        stream_bytes_per_launch=moved, stream_GBps=moved / s / 1e9,
+                        stream_frac=moved / s / PEAKS["hbm"])  # on the bytes the passes move
         return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
                     frac=alg / s / PEAKS["hbm"], traffic=None, kernel=kname, launch_ms=ms_dom, alg_bytes=alg)
     # sparse Gram pattern (poly / rbf): SURVEY §8(d) 3-RBF / 5 figure, this rank's share of the pairs

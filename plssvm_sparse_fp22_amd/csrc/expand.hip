@@ -708,6 +708,9 @@ __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__res
 #ifndef EXP_DPP
 #define EXP_DPP 1  // remainder stream: segmented row sums by DPP row shifts / broadcasts (0: ds_bpermute shuffles)
 #endif
+#ifndef EXP_NH
+#define EXP_NH 2  // remainder stream: groups of 64 chunks per lane step (bytes in flight per wave)
+#endif
 
 // one step of a segmented inclusive lane scan keyed by k (keys non-decreasing in lane order): v += the DPP
 // source lane's v when that lane holds the same key (lanes without a source keep v)
@@ -762,7 +765,8 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     const int64_t bx = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t I = bx % nI, g = bx / nI;
     const int64_t W0 = g * nW / G, W1 = (g + 1) * nW / G;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the wave's offsets are scalar loads
     for (int t = tid; t < RB; t += NT) racc[t] = T(0);
     // the window of w moves as 16-byte vectors: thread tid takes vectors tid, tid + NT, ... (PV of them)
     constexpr int VE = 16 / (int) sizeof(WT), NV = CW / VE, PV = (NV + NT - 1) / NT;
@@ -796,26 +800,77 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     };
     const int64_t *wo = woff + (I * EXP_NWV + wave) * (nW + 1);
     const int64_t s_end = wo[W1];
-    // one step of the stream in registers: chunk cp (= step start + lane), loads clamped to the stream
-    int rl_n = 0;
-    u32x2 jj_n = { 0u, 0u };
-    T h_n[4] = { T(0), T(0), T(0), T(0) };
-    u32x2 hb_n = { 0u, 0u };  // bfloat16 H, kept raw until the step uses it (a conversion here would wait for the load)
+    // one step of the stream in registers: EXP_NH groups of 64 chunks (group h: chunk step start + 64 h +
+    // lane), loads clamped to the stream; prefetched one step ahead
+    struct group_regs {
+        int rl = 0;
+        u32x2 jj = { 0u, 0u };
+        T h[4] = { T(0), T(0), T(0), T(0) };
+        u32x2 hb = { 0u, 0u };  // bfloat16 H, kept raw until the step uses it (a conversion here would wait for the load)
+    };
+    group_regs nx[EXP_NH];
+    const bool empty = s_end == wo[W0];
     auto fetch = [&](int64_t c) {
-        if (s_end == wo[W0]) return;  // empty stream (wave-uniform)
-        const int64_t cl = c < s_end ? c : s_end - 1;
-        rl_n = (int) __builtin_nontemporal_load(hrow + cl);
-        jj_n = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hjl + 4 * cl));
-        if constexpr (HB) {
-            hb_n = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hv16 + 4 * cl));
-        } else if constexpr (sizeof(T) == 4) {
-            const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(hv + 4 * cl));
-            h_n[0] = v.x, h_n[1] = v.y, h_n[2] = v.z, h_n[3] = v.w;
-        } else {
-            const f64x2 v0 = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(hv + 4 * cl));
-            const f64x2 v1 = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(hv + 4 * cl + 2));
-            h_n[0] = v0.x, h_n[1] = v0.y, h_n[2] = v1.x, h_n[3] = v1.y;
+        if (empty) return;  // empty stream (wave-uniform)
+#pragma unroll
+        for (int hh = 0; hh < EXP_NH; ++hh) {
+            const int64_t cc = c + 64 * hh, cl = cc < s_end ? cc : s_end - 1;
+            group_regs &g = nx[hh];
+            g.rl = (int) __builtin_nontemporal_load(hrow + cl);
+            g.jj = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hjl + 4 * cl));
+            if constexpr (HB) {
+                g.hb = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hv16 + 4 * cl));
+            } else if constexpr (sizeof(T) == 4) {
+                const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(hv + 4 * cl));
+                g.h[0] = v.x, g.h[1] = v.y, g.h[2] = v.z, g.h[3] = v.w;
+            } else {
+                const f64x2 v0 = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(hv + 4 * cl));
+                const f64x2 v1 = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(hv + 4 * cl + 2));
+                g.h[0] = v0.x, g.h[1] = v0.y, g.h[2] = v1.x, g.h[3] = v1.y;
+            }
         }
+    };
+    // one group of 64 chunks: the 4 slots times w from the window, then the rows' sums into racc
+    auto group = [&](const group_regs &g, bool have) {
+        const int rl = have ? g.rl : -1;
+        const u32x2 jj = g.jj;
+        T h0 = g.h[0], h1 = g.h[1], h2 = g.h[2], h3 = g.h[3];
+        if constexpr (HB) {  // bfloat16 H: the float's top 16 bits
+            h0 = (T) __uint_as_float(g.hb.x << 16), h1 = (T) __uint_as_float(g.hb.x & 0xFFFF0000u);
+            h2 = (T) __uint_as_float(g.hb.y << 16), h3 = (T) __uint_as_float(g.hb.y & 0xFFFF0000u);
+        }
+        T acc = T(0);
+        if (have) {
+            acc = h0 * wat(jj.x & 0xFFFFu);
+            acc = fma(h1, wat(jj.x >> 16), acc);
+            acc = fma(h2, wat(jj.y & 0xFFFFu), acc);
+            acc = fma(h3, wat(jj.y >> 16), acc);
+        }
+#if EXP_DPP
+        // segmented inclusive prefix sums over the lanes by DPP (rows are non-decreasing in lane order):
+        // row_shr 1/2/4/8 inside each 16-lane row, then row_bcast 15 / 31 across rows; the total of a
+        // row's run lands on its last lane, which adds it to the row accumulator
+        T sacc = acc;
+        seg_step<0x111, 0xF>(sacc, rl);  // row_shr:1
+        seg_step<0x112, 0xF>(sacc, rl);  // row_shr:2
+        seg_step<0x114, 0xF>(sacc, rl);  // row_shr:4
+        seg_step<0x118, 0xF>(sacc, rl);  // row_shr:8
+        seg_step<0x142, 0xA>(sacc, rl);  // row_bcast:15 (rows 1, 3)
+        seg_step<0x143, 0xC>(sacc, rl);  // row_bcast:31 (rows 2, 3)
+        const int rnext = __builtin_amdgcn_update_dpp(-2, rl, 0x130, 0xF, 0xF, false);  // wave_shl:1
+        if (rl >= 0 && (lane == 63 || rnext != rl)) racc[rl] += sacc;  // rows of this wave only
+#else
+        // segmented suffix sums: rows are non-decreasing in lane order
+        T sacc = acc;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const T so = __shfl_down(sacc, off);
+            const int rr = __shfl_down(rl, off);
+            if (lane + off < 64 && rr == rl) sacc += so;
+        }
+        const int rprev = __shfl_up(rl, 1);
+        if (rl >= 0 && (lane == 0 || rprev != rl)) racc[rl] += sacc;  // rows of this wave only
+#endif
     };
     if (W0 < W1) {
         load_win(W0);
@@ -823,52 +878,19 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
         fetch(wo[W0] + lane);
     }
     __syncthreads();
+    constexpr int STEP = 64 * EXP_NH;
     for (int64_t W = W0; W < W1; ++W) {
         if (W + 1 < W1) load_win(W + 1);  // lands in registers while this window is processed
         const int64_t c_end = wo[W + 1];
-        for (int64_t cb = wo[W]; cb < c_end; cb += 64) {  // wave-uniform trip count
-            const bool have = cb + lane < c_end;
-            const int rl = have ? rl_n : -1;
-            const u32x2 jj = jj_n;
-            T h0 = h_n[0], h1 = h_n[1], h2 = h_n[2], h3 = h_n[3];
-            const u32x2 hb = hb_n;
-            fetch((cb + 64 < c_end ? cb + 64 : c_end) + lane);  // next step (next window's first at c_end)
-            if constexpr (HB) {  // bfloat16 H: the float's top 16 bits
-                h0 = (T) __uint_as_float(hb.x << 16), h1 = (T) __uint_as_float(hb.x & 0xFFFF0000u);
-                h2 = (T) __uint_as_float(hb.y << 16), h3 = (T) __uint_as_float(hb.y & 0xFFFF0000u);
-            }
-            T acc = T(0);
-            if (have) {
-                acc = h0 * wat(jj.x & 0xFFFFu);
-                acc = fma(h1, wat(jj.x >> 16), acc);
-                acc = fma(h2, wat(jj.y & 0xFFFFu), acc);
-                acc = fma(h3, wat(jj.y >> 16), acc);
-            }
-#if EXP_DPP
-            // segmented inclusive prefix sums over the lanes by DPP (rows are non-decreasing in lane order):
-            // row_shr 1/2/4/8 inside each 16-lane row, then row_bcast 15 / 31 across rows; the total of a
-            // row's run lands on its last lane, which adds it to the row accumulator
-            T sacc = acc;
-            seg_step<0x111, 0xF>(sacc, rl);  // row_shr:1
-            seg_step<0x112, 0xF>(sacc, rl);  // row_shr:2
-            seg_step<0x114, 0xF>(sacc, rl);  // row_shr:4
-            seg_step<0x118, 0xF>(sacc, rl);  // row_shr:8
-            seg_step<0x142, 0xA>(sacc, rl);  // row_bcast:15 (rows 1, 3)
-            seg_step<0x143, 0xC>(sacc, rl);  // row_bcast:31 (rows 2, 3)
-            const int rnext = __builtin_amdgcn_update_dpp(-2, rl, 0x130, 0xF, 0xF, false);  // wave_shl:1
-            if (rl >= 0 && (lane == 63 || rnext != rl)) racc[rl] += sacc;  // rows of this wave only
-#else
-            // segmented suffix sums: rows are non-decreasing in lane order
-            T sacc = acc;
+        for (int64_t cb = wo[W]; cb < c_end; cb += STEP) {  // wave-uniform trip count
+            group_regs cur[EXP_NH];
 #pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const T so = __shfl_down(sacc, off);
-                const int rr = __shfl_down(rl, off);
-                if (lane + off < 64 && rr == rl) sacc += so;
-            }
-            const int rprev = __shfl_up(rl, 1);
-            if (rl >= 0 && (lane == 0 || rprev != rl)) racc[rl] += sacc;  // rows of this wave only
-#endif
+            for (int hh = 0; hh < EXP_NH; ++hh) cur[hh] = nx[hh];
+            // next step (next window's first at c_end; groups past a window's end are loaded, masked, and
+            // loaded again as the next window's)
+            fetch((cb + STEP < c_end ? cb + STEP : c_end) + lane);
+#pragma unroll
+            for (int hh = 0; hh < EXP_NH; ++hh) group(cur[hh], cb + 64 * hh + lane < c_end);  // groups in order
         }
         if (W + 1 < W1) {
             __syncthreads();  // every wave is done with window W

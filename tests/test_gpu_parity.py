@@ -317,3 +317,33 @@ def test_single_rank_rccl_group_sharded(layout, kernel, kp_mode, algo, monkeypat
         svm.close()
     for a, b in zip(outs[0], outs[1]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("kernel", ["rbf", "polynomial"])
+def test_single_rank_rccl_group_sharded_bf16(kernel, monkeypatch):
+    """The sharded expansion with bfloat16 windows (fp32): the group gathers the rows'
+    bfloat16 w and the ranks' S partials instead of w (expansion_kp_raw). With one rank the gathered
+    partials are the local ones in dot2's grid order, so K·p, trace and alphas equal the context without a
+    communicator bit for bit."""
+    n, nf = 3000, 5000
+    csr, y = datagen.sparse_csr(n, nf, 20, seed=3, dtype=np.float32)
+    outs = []
+    for uid in (None, pm.unique_id()):
+        if uid is None:
+            monkeypatch.delenv("PLSSVM_MI_SHARD", raising=False)
+        else:
+            monkeypatch.setenv("PLSSVM_MI_SHARD", "1")
+        p = pm.Parameter(kernel, gamma=1.0 / nf, coef0=1.0 if kernel == "polynomial" else 0.0, real_type=np.float32)
+        p.csr = csr
+        p.labels = y
+        svm = pm.CSVM(p, uid=uid, sparse_algo="expansion")
+        svm.setup_data_on_device()
+        assert svm.info()["exp_hbytes"] == 2
+        svm.generate_q()
+        x = np.linspace(1, 2, n - 1).astype(np.float32)
+        ret = svm.run_device_kernel(None, np.zeros(n - 1, np.float32), x, 1.0)
+        svm.learn(imax=60)
+        outs.append((ret, np.array(svm.trace), svm.alpha.copy()))
+        svm.close()
+    for a, b in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, b)

@@ -9,7 +9,8 @@ total) for a range of RCCL latencies alpha and bus bandwidths beta — an assump
 
 Collectives per CG iteration (engine.hip / sparse.hip / expand.hip) and what hides them:
   dense pairwise (replicated CG):   all-reduce of raw (m reals), exposed
-  sparse expansion (sharded CG):    all-gather of w (m reals; carries the pending direction partials),
+  sparse expansion (sharded CG):    all-gather of w (m reals, or m bfloat16 + the ranks' S partials with
+                                    bfloat16 windows; carries the pending direction partials),
                                     overlapping the rank's column-moment pass (expansion_kp_raw: the pass
                                     needs only the rank's own w) -> exposed max(0, t - t_moments);
                                     all-reduce of the column moments (d x KM reals) on the collective
@@ -38,7 +39,10 @@ def collectives(rec, G, km):
         return [("allreduce", m * s, None)]
     if cfg["kp_mode"] == "factored":
         return [("allreduce", d * s, None)] + [("allgather", tiny, None)] * 2
-    return [("allgather", m * s + tiny, "moments"), ("allreduce", d * km * s, "stream")] + \
+    # bfloat16 windows: the group gathers w as bfloat16 plus the ranks' S partials
+    ws = 2 if "bfloat16" in str(rec["roofline"].get("h_storage", "")) else s
+    extra = tiny if ws == 2 else 0
+    return [("allgather", m * ws + tiny + extra, "moments"), ("allreduce", d * km * s, "stream")] + \
         [("allgather", tiny, None)] * 2
 
 
