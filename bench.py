@@ -174,7 +174,10 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
     roof = roofline(cfg, info, n, d, share, ms_dom, extra)
     dts = "f64" if dt == np.float64 else "f32"
     tkey = name + (f"_sim{sim[0]}of{sim[1]}" if sim else "")
-    roof["traffic"], roof["traffic_source"] = pmc_traffic(tkey, n, d, world, roof["kernel"], dts, kern, cfg is CONFIGS[name])
+    hs = roof.get("h_storage")
+    tag = None if hs is None else ("bf16" if hs.startswith("bfloat16") else "real")
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(tkey, n, d, world, roof["kernel"], dts, kern,
+                                                          cfg is CONFIGS[name], tag)
     if roof["traffic"] and roof["bound"] == "hbm":
         roof["traffic_GBps"] = roof["traffic"] / (ms_dom * 1e-3) / 1e9
         roof["traffic_frac"] = roof["traffic_GBps"] * 1e9 / PEAKS["hbm"]
@@ -372,13 +375,16 @@ def _pmc_match(t, n, d, world, dtype, kfun, default_cfg):
     return default_cfg
 
 
-def pmc_traffic(config, n, d, world, kernel, dtype, kfun, default_cfg):
+def pmc_traffic(config, n, d, world, kernel, dtype, kfun, default_cfg, tag=None):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC pass of this exact
-    workload (profiles/*_<config>_traffic.json, written by tools/pmc_traffic.py), else None."""
+    workload (profiles/*_<config>_traffic.json, written by tools/pmc_traffic.py), else None. tag: the
+    expansion's remainder layout ('bf16' / 'real'; files written before the tag existed measured 'real')."""
     import glob
 
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{config}_traffic.json")), reverse=True):
         t = json.load(open(path))
+        if tag is not None and (t.get("layout_tag") or "real") != tag:
+            continue
         if kernel == t["kernel"] and _pmc_match(t, n, d, world, dtype, kfun, default_cfg):
             return t["hbm_read_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None, None

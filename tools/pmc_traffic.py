@@ -22,6 +22,12 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def layout_tag(roof):
+    """'bf16' / 'real' for the kernel expansion's remainder stream (roofline.h_storage), else None"""
+    hs = roof.get("h_storage")
+    return None if hs is None else ("bf16" if hs.startswith("bfloat16") else "real")
+
+
 def find(pattern):
     hits = sorted(glob.glob(pattern, recursive=True))
     if not hits:
@@ -66,6 +72,8 @@ def main():
         "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 counts half of wide streaming reads)",
         "rocprof_avg_ms": None if avg_ns is None else avg_ns * 1e-6,
         "bench_launch_ms": bench["roofline"].get("launch_ms"),
+        # the stream layout the counters saw (bench.py matches it: a bfloat16 remainder moves other bytes)
+        "layout_tag": layout_tag(bench["roofline"]),
     }
     with open(os.path.join(prof, f"{rnd}_{config}_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
