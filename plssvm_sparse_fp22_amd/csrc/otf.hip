@@ -204,6 +204,74 @@ __device__ __forceinline__ void otf_batch(T *__restrict__ s, const otf_jv<T> *__
     }
 }
 
+#ifndef OTF_V2
+#define OTF_V2 1  // segment loads through per-feature buffer descriptors (0: per-lane 64-bit addresses)
+#endif
+
+// A feature's segment through a buffer descriptor whose base is the segment's first entry and whose size
+// is its byte length: lane l reads entry o + l at the constant offset (o + l) * sizeof(entry), lanes past
+// the end read zeros without touching memory, and the descriptor is built from wave-uniform values with
+// scalar instructions — no per-lane address arithmetic or past-the-end clamping per feature.
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t otf_seg_rsrc(const otf_jv<T> *cjv, int64_t lo, int len) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *) (cjv + lo), (short) 0, len * (int) sizeof(otf_jv<T>), 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ otf_jv<T> otf_seg_load(__amdgpu_buffer_rsrc_t rs, int k) {
+    if constexpr (sizeof(T) == 4) {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b64(rs, k * 8, 0, 0);
+        return otf_jv<T>{ (int32_t) r[0], __uint_as_float(r[1]) };
+    } else {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 16, 0, 0);
+        return otf_jv<T>{ (int32_t) r[0], __longlong_as_double((long long) (((uint64_t) r[3] << 32) | r[2])) };
+    }
+}
+
+// otf_batch with the segments read through otf_seg_rsrc and the prefetch ping-ponged between two register
+// sets (no loop-carried copies that wait for the loads): the same entries, updates and update order
+template <typename T>
+__device__ __forceinline__ void otf_batch2(T *__restrict__ s, const otf_jv<T> *__restrict__ cjv, int j0, int nk,
+                                           int64_t lo, int len, T v, int lane) {
+    struct grp {
+        __amdgpu_buffer_rsrc_t rs[OTF_U];
+        int len[OTF_U];
+        T v[OTF_U];
+        otf_jv<T> e[OTF_U];
+    };
+    T *sb = s - j0;  // s[j - j0]
+    nk = __builtin_amdgcn_readfirstlane(nk);
+    auto fetch = [&](grp &g, int u) {
+#pragma unroll
+        for (int x = 0; x < OTF_U; ++x) {
+            const int k = (u + x) & 63;  // past the batch: a zero-length segment (nothing is read)
+            const int n = u + x < nk ? rl32(len, k) : 0;
+            g.len[x] = n;
+            g.v[x] = rlT(v, k);
+            g.rs[x] = otf_seg_rsrc<T>(cjv, rl64(lo, k), n);
+            g.e[x] = otf_seg_load<T>(g.rs[x], lane);
+        }
+    };
+    auto process = [&](const grp &g) {
+#pragma unroll
+        for (int x = 0; x < OTF_U; ++x) {
+            if (lane < g.len[x]) otf_add(sb + g.e[x].j, g.v[x] * g.e[x].v);
+            for (int o = 64; o < g.len[x]; o += 64) {  // segments longer than a wave (dense columns)
+                const otf_jv<T> e = otf_seg_load<T>(g.rs[x], o + lane);
+                if (o + lane < g.len[x]) otf_add(sb + e.j, g.v[x] * e.v);
+            }
+        }
+    };
+    grp A, B;
+    fetch(A, 0);
+    for (int u = 0; u < nk; u += 2 * OTF_U) {
+        fetch(B, u + OTF_U);
+        process(A);
+        if (u + OTF_U >= nk) break;  // wave-uniform
+        fetch(A, u + 2 * OTF_U);
+        process(B);
+    }
+}
+
 // raw[i] = sum_{j != i, s_ij != 0} c_ij p_j for this rank's rows i in [r0, r1)
 template <typename T, int CWB>
 __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
@@ -216,7 +284,8 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
     constexpr int CW = otf_cw<T, CWB>();
     __shared__ T S[OTF_NT / 64][CW];
     if (status != nullptr && status->converged) return;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave-uniform row (scalar loads of its row pointers, counts and segment descriptors)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int64_t i = r0 + (int64_t) blockIdx.x * (OTF_NT / 64) + wave;
     if (i >= r1) return;  // waves never synchronise: each owns its accumulator row
     T *s = S[wave];
@@ -236,7 +305,8 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
         if (nz > 0) {
             const int2 sg = sg0;
             sg0 = h0 && W + 1 < Wb ? seg[(int64_t) f0 * nW + W + 1] : make_int2(0, 0);
-            otf_batch<T>(s, cjv, j0, (int) (nz < 64 ? nz : 64), c0 + sg.x, sg.y, v0, lane);
+            if constexpr (OTF_V2) otf_batch2<T>(s, cjv, j0, (int) (nz < 64 ? nz : 64), c0 + sg.x, sg.y, v0, lane);
+            else otf_batch<T>(s, cjv, j0, (int) (nz < 64 ? nz : 64), c0 + sg.x, sg.y, v0, lane);
         }
         for (int64_t q0 = 64; q0 < nz; q0 += 64) {  // further features: reloaded per window
             const int64_t k = q0 + lane;
@@ -250,7 +320,8 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
                 lo = ecb[b0 + k] + sg.x;
                 len = sg.y;
             }
-            otf_batch<T>(s, cjv, j0, (int) (nz - q0 < 64 ? nz - q0 : 64), lo, len, v, lane);
+            if constexpr (OTF_V2) otf_batch2<T>(s, cjv, j0, (int) (nz - q0 < 64 ? nz - q0 : 64), lo, len, v, lane);
+            else otf_batch<T>(s, cjv, j0, (int) (nz - q0 < 64 ? nz - q0 : 64), lo, len, v, lane);
         }
         // the window's pair terms, lane-strided (fixed order); the accumulators are left zeroed. The partners'
         // (p_j, |x_j|^2, e_j) come as one packed load per lane, OTF_SCAN steps issued before their use (the
