@@ -175,7 +175,8 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
     dts = "f64" if dt == np.float64 else "f32"
     tkey = name + (f"_sim{sim[0]}of{sim[1]}" if sim else "")
     hs = roof.get("h_storage")
-    tag = None if hs is None else ("bf16" if hs.startswith("bfloat16") else "real")
+    tag = None if hs is None else ("bf16" if hs.startswith("bfloat16") else "real") + \
+        ("_flags" if "flags" in roof.get("stream_layout", "") else "")
     roof["traffic"], roof["traffic_source"] = pmc_traffic(tkey, n, d, world, roof["kernel"], dts, kern,
                                                           cfg is CONFIGS[name], tag)
     if roof["traffic"] and roof["bound"] == "hbm":
@@ -345,12 +346,15 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
         # two or more features (uint16 j + H per slot, uint16 row per 4-slot chunk), read once per K·p;
         # the column-moment and Horner passes are the two SELL SpMV passes of the linear path
         hb = info["exp_hbytes"] or es
-        rem = info["pair_slots"] * (2 + hb) + info["exp_chunks"] * 2
+        # the stored row index: 2 B per 4-slot chunk in the indexed layout (exp_layout 1); none with row-start
+        # flags (2: the dummies of empty cells are in pair_slots) or runs (3)
+        rem = info["pair_slots"] * (2 + hb) + (info["exp_chunks"] * 2 if info["exp_layout"] == 1 else 0)
         return dict(bound="hbm", achieved=rem / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
                     frac=rem / s / PEAKS["hbm"], traffic=None, kernel="exp_hcell_kernel", launch_ms=ms_dom,
                     alg_bytes=rem, alg_bytes_def="remainder stream: slots x (2 + bytes per stored H) + chunks x 2 (run layout: chunks = 0, slots = entries + dummies)",
                     h_storage="bfloat16 (precision bound, DESIGN §5.1.2)" if hb == 2 else f"real ({hb} B)",
-                    stream_layout="runs" if info["exp_chunks"] == 0 else "4-slot chunks",
+                    stream_layout={1: "4-slot chunks + row index", 2: "4-slot chunks, row-start flags",
+                                   3: "runs"}.get(info["exp_layout"], "?"),
                     exp_terms=info["exp_terms"], multi_pairs=info["pairs"], pair_slots=info["pair_slots"],
                     spmv_bytes=info["spmv_bytes"], survey_alg_bytes=survey,
                     survey_effective_GBps=survey / s / 1e9, survey_effective_frac=survey / s / PEAKS["hbm"])

@@ -257,6 +257,9 @@ typedef struct {
     int64_t exp_chunks; /* kernel expansion: 4-slot chunks of the remainder stream (this rank's rows); 0 = run layout */
     int exp_hbytes;     /* kernel expansion: bytes of a stored remainder value (2 = bfloat16 under the precision
                            bound of expand.hip "H storage", else sizeof(real)) */
+    int exp_layout;     /* kernel expansion: remainder stream layout — 1 = 4-slot chunks with a stored row index per
+                           chunk, 2 = 4-slot chunks whose rows are numbered by row-start flags (no row index),
+                           3 = runs (no padding); 0 = no expansion */
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
 

@@ -626,6 +626,77 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__
     if (Wc >= 0) close();
 }
 
+// ---- flagged chunks (hbf16 layouts): no per-chunk row index ------------------------------------------------
+// A stored bfloat16 H with |H| < 2 has bit 14 (the exponent's top bit) clear, so the first H of a chunk can
+// carry a flag instead: set on the first chunk of each (row, window) cell. Every row of the rank gets at least
+// one chunk per window (a dummy: j = 0, H = 0, when it has no partners there), so inside a wave's stream of a
+// window the rows follow each other without gaps and a chunk's row is the wave's first row + (the number of
+// flags up to it) - 1: a ballot and a lane count per 64 chunks instead of 2 bytes per chunk.
+
+// stats[0] += windows without entries (the dummies the layout would add), stats[1] |= 1 when a stored H's
+// bfloat16 has bit 14 set (|H| >= 2: the bit is not free)
+template <typename T>
+__global__ __launch_bounds__(256) void exp_cell_stats_kernel(const int64_t *__restrict__ off8, const int32_t *__restrict__ sj,
+                                                             const T *__restrict__ sv, int64_t R, int64_t nW, int64_t CW,
+                                                             unsigned long long *__restrict__ stats) {
+    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long empty = 0, big = 0;
+    if (r < R) {
+        int64_t Wc = -1, nwin = 0;
+        for (int64_t s = off8[r]; s < off8[r + 1]; ++s) {
+            if (sv[s] == T(0)) continue;
+            const int64_t W = sj[s] / CW;
+            if (W != Wc) Wc = W, ++nwin;
+            if (bf16_rne((float) sv[s]) & 0x4000u) big = 1;
+        }
+        empty = (unsigned long long) (nW - nwin);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        empty += __shfl_xor(empty, o);
+        big |= __shfl_xor(big, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (empty) atomicAdd(stats, empty);
+        if (big) atomicOr(stats + 1, big);
+    }
+}
+
+// the dummies: a (row, window) cell without entries takes one 4-slot chunk
+__global__ __launch_bounds__(256) void exp_cell_fill_empty_kernel(int64_t R, int64_t nW, int64_t RB, int64_t *__restrict__ cnt) {
+    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= R * nW) return;
+    const int64_t idx = exp_cidx(t / nW, t % nW, nW, RB);
+    if (cnt[idx] == 0) cnt[idx] = 4;
+}
+
+// exp_cell_scatter_kernel for the flagged layout (bfloat16 H, buffers zeroed): every window of the row in
+// order, its entries (or a dummy), bit 14 set on the cell's first H
+template <typename T>
+__global__ __launch_bounds__(256) void exp_cell_scatter_flag_kernel(const int64_t *__restrict__ off8,
+                                                                    const int32_t *__restrict__ sj, const T *__restrict__ sv,
+                                                                    int64_t R, int64_t nW, int64_t CW, int64_t RB,
+                                                                    const int64_t *__restrict__ coff,
+                                                                    uint16_t *__restrict__ hjl, uint16_t *__restrict__ hv16) {
+    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    int64_t s = off8[r];
+    const int64_t se = off8[r + 1];
+    for (int64_t W = 0; W < nW; ++W) {
+        const int64_t base = coff[exp_cidx(r, W, nW, RB)];
+        int64_t k = 0;
+        for (; s < se; ++s) {  // entries sorted by j: this window's, then stop at the next window's first
+            const T h = sv[s];
+            if (h == T(0)) continue;  // pads
+            if (sj[s] / CW != W) break;
+            hjl[base + k] = (uint16_t) (sj[s] - W * CW);
+            hv16[base + k] = bf16_rne((float) h);
+            ++k;
+        }
+        hv16[base] |= (uint16_t) 0x4000u;  // k == 0: the dummy (j = 0, H = 0)
+    }
+}
+
 // ---- run layout (option, PLSSVM_MI_EXP_RUNS): no padding, no per-chunk row index --------------------
 // Per (row, window) exactly max(count, 1) entries: the first entry of every row carries bit 15 of its
 // window-local j (so CW <= 32768), a row without partners in the window gets one flagged dummy (j = 0,
@@ -737,7 +808,7 @@ __device__ __forceinline__ void seg_step(double &v, int k) {
 // software-pipelined one step ahead, also across window boundaries), gathers w_j from LDS and adds its
 // rows' partial sums (segmented shuffle reduction) into an LDS row accumulator only it writes.
 // Fixed order, no atomics: bitwise reproducible.
-template <typename T, int RBB, bool HB>
+template <typename T, int RBB, bool HB, bool RF = false>
 __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *__restrict__ woff,
                                                                  const uint16_t *__restrict__ hrow,
                                                                  const uint16_t *__restrict__ hjl,
@@ -816,7 +887,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
         for (int hh = 0; hh < EXP_NH; ++hh) {
             const int64_t cc = c + 64 * hh, cl = cc < s_end ? cc : s_end - 1;
             group_regs &g = nx[hh];
-            g.rl = (int) __builtin_nontemporal_load(hrow + cl);
+            if constexpr (!RF) g.rl = (int) __builtin_nontemporal_load(hrow + cl);
             g.jj = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hjl + 4 * cl));
             if constexpr (HB) {
                 g.hb = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hv16 + 4 * cl));
@@ -831,12 +902,24 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
         }
     };
     // one group of 64 chunks: the 4 slots times w from the window, then the rows' sums into racc
+    // RF: the rows of a window's chunks from their row-start flags (carry = the row before the step's first chunk + 1)
+    int carry = 0;
     auto group = [&](const group_regs &g, bool have) {
-        const int rl = have ? g.rl : -1;
+        int rl = have ? g.rl : -1;
+        uint32_t hx = g.hb.x;
+        if constexpr (RF) {
+            const bool fl = have && (hx & 0x4000u) != 0;
+            const unsigned long long bal = __ballot(fl);
+            const int below = (int) __builtin_amdgcn_mbcnt_hi((uint32_t) (bal >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t) bal, 0u));
+            rl = have ? carry + below + (fl ? 1 : 0) - 1 : -1;
+            carry += __popcll(bal);
+            hx &= ~0x4000u;
+        }
         const u32x2 jj = g.jj;
         T h0 = g.h[0], h1 = g.h[1], h2 = g.h[2], h3 = g.h[3];
         if constexpr (HB) {  // bfloat16 H: the float's top 16 bits
-            h0 = (T) __uint_as_float(g.hb.x << 16), h1 = (T) __uint_as_float(g.hb.x & 0xFFFF0000u);
+            h0 = (T) __uint_as_float(hx << 16), h1 = (T) __uint_as_float(hx & 0xFFFF0000u);
             h2 = (T) __uint_as_float(g.hb.y << 16), h3 = (T) __uint_as_float(g.hb.y & 0xFFFF0000u);
         }
         T acc = T(0);
@@ -882,6 +965,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     for (int64_t W = W0; W < W1; ++W) {
         if (W + 1 < W1) load_win(W + 1);  // lands in registers while this window is processed
         const int64_t c_end = wo[W + 1];
+        carry = wave * (int) (RB / EXP_NWV);  // RF: the wave's first row starts every window
         for (int64_t cb = wo[W]; cb < c_end; cb += STEP) {  // wave-uniform trip count
             group_regs cur[EXP_NH];
 #pragma unroll
@@ -1067,11 +1151,14 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *_
 }
 
 // raw_i for rows [r0, r1) (0 elsewhere), raw holding J_i there (the CSR pass): base + scale (J_i +
-// H_ii w_i + hs_i, hs_i = the remainder stream's row sum) [- the diagonal's pair part when only the overlap part is asked for], in fp64
+// H_ii w_i + hs_i, hs_i = the remainder stream's row sum) [- the diagonal's pair part when only the overlap part is asked for], in fp64.
+// jslab != null: the CSR pass left its P < 16 panel slabs (jslab[q][i - r0]) and J_i is their sum from 0 in
+// panel order — panel_reduce_kernel's sum, bit for bit, without its launch
 template <typename T>
 __global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ e, const T *__restrict__ w,
                                                           const T *__restrict__ hdiag, const T *__restrict__ phin,
                                                           const T *__restrict__ hs, const T *__restrict__ hslab, int G,
+                                                          const T *__restrict__ jslab, int P,
                                                           const T *__restrict__ ssc, T kappa,
                                                           int64_t ib, int64_t ie, int64_t r0, int64_t r1, int overlap_only,
                                                           T *__restrict__ raw, const cg_scalars<T> *__restrict__ status) {
@@ -1089,7 +1176,14 @@ __global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ 
     } else {
         h = hs[i];
     }
-    const double t = (double) raw[i] + (double) hdiag[i] * wi + (double) h;
+    T J;
+    if (jslab != nullptr) {
+        J = T(0);
+        for (int q = 0; q < P; ++q) J += jslab[(int64_t) q * (r1 - r0) + (i - r0)];
+    } else {
+        J = raw[i];
+    }
+    const double t = (double) J + (double) hdiag[i] * wi + (double) h;
     const double sc = e != nullptr ? (double) e[i] : 1.0;
     double v;
     if (overlap_only) {
@@ -1606,6 +1700,31 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
                                    off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, cnt.get());
                 MI_LAUNCH_CHECK();
             }
+            // flagged chunks (bfloat16 H only): when every |H| < 2 and the dummies of empty cells (16 B each) cost
+            // at most half of the row indices they replace (2 B per chunk). PLSSVM_MI_EXP_ROWS=index keeps the
+            // row index, =flags forces the flags (when the bit is free)
+            ex.rflags = false;
+            if (ex.hbf16 && R > 0) {
+                const char *rs = std::getenv("PLSSVM_MI_EXP_ROWS");
+                const int ropt = rs == nullptr ? 0 : (std::strcmp(rs, "index") == 0 ? -1 : std::strcmp(rs, "flags") == 0 ? 1 : 0);
+                if (ropt >= 0) {
+                    dev_buf<unsigned long long> st;
+                    st.alloc(2, stream);
+                    hipLaunchKernelGGL(exp_cell_stats_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                                       off8.get(), sj.get(), sv.get(), R, ex.nW, CW, st.get());
+                    MI_LAUNCH_CHECK();
+                    unsigned long long hs2[2] = { 0ull, 0ull };
+                    MI_HIP_CHECK(hipMemcpyAsync(hs2, st.get(), sizeof(hs2), hipMemcpyDeviceToHost, stream));
+                    scan(ncnt);  // synchronises; ex.slots = the indexed layout's slots
+                    const double chunks = (double) ex.slots / 4.0;
+                    ex.rflags = hs2[1] == 0 && (ropt == 1 || 16.0 * (double) hs2[0] <= 0.5 * 2.0 * chunks);
+                    if (ex.rflags) {
+                        hipLaunchKernelGGL(exp_cell_fill_empty_kernel, dim3((unsigned) ceil_div(R * ex.nW, 256)), dim3(256),
+                                           0, stream, R, ex.nW, RB, cnt.get());
+                        MI_LAUNCH_CHECK();
+                    }
+                }
+            }
             scan(ncnt);
             ex.nchunks = ex.slots / 4;
             ex.hjl.alloc(std::max<int64_t>(ex.slots, 4), stream);
@@ -1614,12 +1733,20 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
                 ex.wv16.alloc(round_up(std::max<int64_t>({ m, chunk * G, 8 }), (int64_t) 8), stream);
             }
             else ex.hv.alloc(std::max<int64_t>(ex.slots, 4), stream);
-            ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
-            if (R > 0) {
-                hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+            if (ex.rflags) {
+                ex.hrow.reset();
+                hipLaunchKernelGGL(exp_cell_scatter_flag_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
                                    off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
-                                   ex.hv.get(), ex.hv16.get(), ex.hrow.get());
+                                   ex.hv16.get());
                 MI_LAUNCH_CHECK();
+            } else {
+                ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
+                if (R > 0) {
+                    hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                                       off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
+                                       ex.hv.get(), ex.hv16.get(), ex.hrow.get());
+                    MI_LAUNCH_CHECK();
+                }
             }
             ex.woff.alloc(std::max<int64_t>(nbv * (ex.nW + 1), 1), stream);
             if (nbv > 0) {
@@ -1673,20 +1800,21 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
                 default: launch_run(exp_hrun_kernel<T, 16384>);
             }
         } else {
-            auto pick = [&](auto hb) {
-                constexpr bool HB = decltype(hb)::value;
+            auto pick = [&](auto hb, auto rf) {
+                constexpr bool HB = decltype(hb)::value, RF = decltype(rf)::value;
                 switch (ex.RBB) {
-                    case 4096: launch(exp_hcell_kernel<T, 4096, HB>); break;
-                    case 8192: launch(exp_hcell_kernel<T, 8192, HB>); break;
-                    case 32768: launch(exp_hcell_kernel<T, 32768, HB>); break;
-                    default: launch(exp_hcell_kernel<T, 16384, HB>);
+                    case 4096: launch(exp_hcell_kernel<T, 4096, HB, RF>); break;
+                    case 8192: launch(exp_hcell_kernel<T, 8192, HB, RF>); break;
+                    case 32768: launch(exp_hcell_kernel<T, 32768, HB, RF>); break;
+                    default: launch(exp_hcell_kernel<T, 16384, HB, RF>);
                 }
             };
             if constexpr (sizeof(T) == 4) {
-                if (ex.hbf16) pick(std::true_type{});
-                else pick(std::false_type{});
+                if (ex.hbf16 && ex.rflags) pick(std::true_type{}, std::true_type{});
+                else if (ex.hbf16) pick(std::true_type{}, std::false_type{});
+                else pick(std::false_type{}, std::false_type{});
             } else {
-                pick(std::false_type{});
+                pick(std::false_type{}, std::false_type{});
             }
         }
         MI_LAUNCH_CHECK();  // G > 1: the row sums stay in hslab, summed in g order by exp_combine_kernel
@@ -1825,11 +1953,14 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
         for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
     }
     // J_i = sum_{f in x_i} sum_k x_if^(k+1) M[f][k]: one SELL pass over this rank's CSR rows (mode 2)
-    if (r1 > r0) launch_panel_spmv<T>(csr.spmv_csr, ex.M.get(), d, raw.get() + r0, status, stream, ex.KM, 2);
+    // (few panels: the combine sums the pass's panel slabs itself, one launch fewer)
+    const auto &pc = csr.spmv_csr;
+    const bool jfuse = pc.P > 1 && pc.P < 16 && pc.nseg == r1 - r0 && pc.nblocks > 0;
+    if (r1 > r0) launch_panel_spmv<T>(pc, ex.M.get(), d, raw.get() + r0, status, stream, ex.KM, 2, !jfuse);
     if (ie > ib)
         hipLaunchKernelGGL(exp_combine_kernel<T>, dim3((unsigned) ceil_div(ie - ib, 256)), dim3(256), 0, stream,
                            kernel == 2 ? csr.e.get() : nullptr, w, ex.hdiag.get(), ex.phin.get(), ex.hs.get(),
-                           ex.G > 1 ? ex.hslab.get() : nullptr, ex.G,
+                           ex.G > 1 ? ex.hslab.get() : nullptr, ex.G, jfuse ? pc.partial.get() : nullptr, (int) pc.P,
                            csr.ssc.get(), kappa, ib, ie, r0, r1, with_base ? 0 : 1, raw.get(), status);
     MI_LAUNCH_CHECK();
     if (!shard) allgather_rows(raw.get());

@@ -500,3 +500,41 @@ def test_expansion_bf16_remainder_bound(gamma, want_hbytes, monkeypatch):
     assert np.all(np.abs(a - b) <= 2.0 ** -20 * np.abs(b)), np.max(np.abs(a - b) / np.abs(b))
     if want_hbytes == 4:  # same layout: bitwise
         np.testing.assert_array_equal(out["auto"][2], out["full"][2])
+
+
+@pytest.mark.parametrize("rbb,groups,sim", [("auto", "0", None), ("4096", "1", None), ("8192", "3", None),
+                                             ("32768", "2", None), ("auto", "0", (1, 3)), ("auto", "0", (2, 8))])
+@pytest.mark.parametrize("shape", [(140000, 3000, 20), (150000, 200000, 6)])
+def test_expansion_row_flags_equal_row_index(rbb, groups, sim, shape, monkeypatch):
+    """Flagged chunks (expand.hip: no per-chunk row index; bit 14 of a chunk's first bfloat16 H marks a row's
+    first chunk of a window, rows without partners in a window get a zero dummy chunk, the kernel numbers rows
+    by a ballot of the flags) against the indexed 4-slot chunks: the same stored values in the same order, so
+    the K·p and its overlap part are equal bit for bit — across accumulator classes, window groups and
+    simulated ranks, with three partner windows (m > 2 x 65536), and on a very sparse set (150000 x 200000 @ 6
+    per row) where nearly every (row, window) cell is empty (dummies; auto would keep the row index there)."""
+    n, d, k = shape
+    csr, _ = datagen.sparse_csr(n, d, k, seed=23, dtype=np.float32)
+    x = np.random.default_rng(9).uniform(-1, 2, n - 1).astype(np.float32)
+    if rbb != "auto":
+        monkeypatch.setenv("PLSSVM_MI_EXP_RBB", rbb)
+        monkeypatch.setenv("PLSSVM_MI_EXP_G", groups)
+    out = {}
+    for rows in ("index", "flags"):
+        monkeypatch.setenv("PLSSVM_MI_EXP_ROWS", rows)
+        with sparse_svm(csr, "rbf", np.float32, sim=sim, algo="expansion") as svm:
+            svm.setup_data_on_device()
+            info = svm.info()
+            assert info["exp_hbytes"] == 2
+            out[rows] = (info["exp_layout"], svm.kp_part(x, "kernel"), svm.kp_part(x, "overlap"))
+    assert out["index"][0] == 1 and out["flags"][0] == 2
+    np.testing.assert_array_equal(out["flags"][1], out["index"][1])
+    np.testing.assert_array_equal(out["flags"][2], out["index"][2])
+
+
+def test_expansion_row_flags_default_and_oracle(oracle):
+    """The default layout on a BASELINE-like set is the flagged one, and its K·p equals the oracle (fp32 bar)."""
+    csr, _ = datagen.sparse_csr(20000, 3000, 20, seed=17, dtype=np.float32)
+    with sparse_svm(csr, "rbf", np.float32, algo="expansion") as svm:
+        svm.setup_data_on_device()
+        assert svm.info()["exp_layout"] == 2
+    check_sparse_kp(oracle, csr, "rbf", np.float32, algo="expansion")

@@ -25,7 +25,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def layout_tag(roof):
     """'bf16' / 'real' for the kernel expansion's remainder stream (roofline.h_storage), else None"""
     hs = roof.get("h_storage")
-    return None if hs is None else ("bf16" if hs.startswith("bfloat16") else "real")
+    if hs is None:
+        return None
+    return ("bf16" if hs.startswith("bfloat16") else "real") + ("_flags" if "flags" in roof.get("stream_layout", "") else "")
 
 
 def find(pattern):
