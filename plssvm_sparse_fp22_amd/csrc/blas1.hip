@@ -5,7 +5,7 @@
 // Operation order follows openmp::csvm::solver_CG (src/plssvm/backends/OpenMP/csvm.cpp:82-170):
 // x = x + (alpha*d), r = r - (alpha*Ad), d = (beta*d) + r, each product rounded before the add
 // (no contraction). Dots are two-stage tree reductions with a fixed grid: bitwise reproducible.
-#include "kernels.hpp"
+#include "cg_common.hpp"
 
 #pragma clang fp contract(off)
 
@@ -13,22 +13,7 @@ namespace plssvm_mi {
 
 namespace {
 
-// fused CG kernels: RED_BLOCKS blocks of CG_NT threads (16 waves per block: memory parallelism for
-// the vector streams; one partial per block as for dot2_kernel)
-constexpr int CG_NT = 1024;
-
-template <typename T>
-__device__ __forceinline__ T block_sum(T v, T *red) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    T s = 0;
-    if (threadIdx.x == 0) {
-        for (int w = 0; w < (int) (blockDim.x >> 6); ++w) s += red[w];
-    }
-    return s;
-}
+using namespace cgk;
 
 // partials[blockIdx] = sum a*b (b null: sum a); second pair (c, e) into partials[RED_BLOCKS + blockIdx]
 template <typename T>
@@ -155,46 +140,6 @@ __global__ __launch_bounds__(256) void cg_direction_kernel(T *__restrict__ d, co
     d[i] = t + r[i];
 }
 
-// block_sum with the total broadcast to every thread
-template <typename T>
-__device__ __forceinline__ T block_sum_all(T v, T *red, T *bc) {
-    const T s = block_sum(v, red);
-    if (threadIdx.x == 0) *bc = s;
-    __syncthreads();
-    const T out = *bc;
-    __syncthreads();
-    return out;
-}
-
-// the RED_BLOCKS partial pairs of a dot2_kernel-shaped producer (G gathered sets of a sharded group),
-// summed as dot_final_kernel does
-template <typename T>
-__device__ __forceinline__ void partials_total(const T *__restrict__ partials, int G, T *red, T *bc, T &r1, T &r2) {
-    T s1 = 0, s2 = 0;
-    for (int i = threadIdx.x; i < RED_BLOCKS; i += blockDim.x) {
-        T a = partials[i], b = partials[RED_BLOCKS + i];
-        for (int g = 1; g < G; ++g) {
-            a += partials[g * 2 * RED_BLOCKS + i];
-            b += partials[g * 2 * RED_BLOCKS + RED_BLOCKS + i];
-        }
-        s1 += a;
-        s2 += b;
-    }
-    r1 = block_sum_all(s1, red, bc);
-    r2 = block_sum_all(s2, red, bc);
-}
-
-template <typename T>
-__device__ __forceinline__ void store_partials(T v1, T v2, T *red, T *__restrict__ partials) {
-    const T r1 = block_sum(v1, red);
-    __syncthreads();
-    const T r2 = block_sum(v2, red);
-    if (threadIdx.x == 0) {
-        partials[blockIdx.x] = r1;
-        partials[RED_BLOCKS + blockIdx.x] = r2;
-    }
-}
-
 // The fused CG kernels are short (a few MB per launch): each thread loads its first CG_PRE grid-stride
 // elements before summing the previous step's partials, so that reduction overlaps the loads; the
 // per-thread element order (and every sum) is unchanged.
@@ -241,14 +186,9 @@ __global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__
     if (blockIdx.x == 0 && threadIdx.x == 0) sc->sp = sp, sc->sqp = sqp;
     T s1 = 0;
     auto one = [&](int64_t i, T r_, T q_, T d_) {
-        T v;
-        {
-#pragma clang fp contract(fast)  // kp_finalize_kernel's expression, contracted as in dense.hip
-            v = raw_only ? r_ : r_ + (QA_cost - q_) * sp - sqp + cost_inv * d_;
-            v = T(0) + T(1) * v;
-        }
+        const T v = cg_fin_value(r_, q_, d_, sp, sqp, QA_cost, cost_inv, raw_only);
         Ad[i] = v;
-        s1 += d_ * v;
+        s1 = cg_acc(s1, d_, v);
     };
 #pragma unroll
     for (int e = 0; e < CG_PRE; ++e) {

@@ -1,0 +1,86 @@
+// Device helpers shared by the fused CG kernels (blas1.hip) and the kernels that fuse a CG step into the
+// producer of its input (expand.hip: the expansion's combine + finalize): one definition, so the fused and
+// unfused sequences compile the same arithmetic and give the same bits.
+#pragma once
+
+#include "kernels.hpp"
+
+namespace plssvm_mi {
+namespace cgk {
+
+// fused CG kernels: RED_BLOCKS blocks of CG_NT threads (16 waves per block: memory parallelism for
+// the vector streams; one partial per block as for dot2_kernel)
+constexpr int CG_NT = 1024;
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T *red) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    T s = 0;
+    if (threadIdx.x == 0) {
+        for (int w = 0; w < (int) (blockDim.x >> 6); ++w) s += red[w];
+    }
+    return s;
+}
+
+// block_sum with the total broadcast to every thread
+template <typename T>
+__device__ __forceinline__ T block_sum_all(T v, T *red, T *bc) {
+    const T s = block_sum(v, red);
+    if (threadIdx.x == 0) *bc = s;
+    __syncthreads();
+    const T out = *bc;
+    __syncthreads();
+    return out;
+}
+
+// the RED_BLOCKS partial pairs of a dot2_kernel-shaped producer (G gathered sets of a sharded group),
+// summed as dot_final_kernel does
+template <typename T>
+__device__ __forceinline__ void partials_total(const T *__restrict__ partials, int G, T *red, T *bc, T &r1, T &r2) {
+    T s1 = 0, s2 = 0;
+    for (int i = threadIdx.x; i < RED_BLOCKS; i += blockDim.x) {
+        T a = partials[i], b = partials[RED_BLOCKS + i];
+        for (int g = 1; g < G; ++g) {
+            a += partials[g * 2 * RED_BLOCKS + i];
+            b += partials[g * 2 * RED_BLOCKS + RED_BLOCKS + i];
+        }
+        s1 += a;
+        s2 += b;
+    }
+    r1 = block_sum_all(s1, red, bc);
+    r2 = block_sum_all(s2, red, bc);
+}
+
+template <typename T>
+__device__ __forceinline__ void store_partials(T v1, T v2, T *red, T *__restrict__ partials) {
+    const T r1 = block_sum(v1, red);
+    __syncthreads();
+    const T r2 = block_sum(v2, red);
+    if (threadIdx.x == 0) {
+        partials[blockIdx.x] = r1;
+        partials[RED_BLOCKS + blockIdx.x] = r2;
+    }
+}
+
+// Ad_i of the CG finalize: raw_i + (QA - q_i) sum(d) - sum(q d) + d_i / C (kp_finalize_kernel's
+// expression, contracted as in dense.hip)
+template <typename T>
+__device__ __forceinline__ T cg_fin_value(T r_, T q_, T d_, T sp, T sqp, T QA_cost, T cost_inv, int raw_only) {
+#pragma clang fp contract(fast)
+    T v = raw_only ? r_ : r_ + (QA_cost - q_) * sp - sqp + cost_inv * d_;
+    v = T(0) + T(1) * v;
+    return v;
+}
+
+// s + a * b with the product rounded before the add (the dot partials of the CG kernels)
+template <typename T>
+__device__ __forceinline__ T cg_acc(T s, T a, T b) {
+#pragma clang fp contract(off)
+    return s + a * b;
+}
+
+}  // namespace cgk
+}  // namespace plssvm_mi

@@ -540,12 +540,19 @@ void engine<T>::cg_iter(int reset) {
         slabs = csr.spmv_csr.partial.get();
         P = csr.spmv_csr.P;
     } else {
+        const kp_fin_t fin{ q.get(), dv.get(), psum_in, G, QA_cost, cost_inv(), Ad.get(), pdad };
+        kp_fin_req = raw_only ? nullptr : &fin;
+        kp_fin_done = false;
         kp_raw(dv.get(), st);
+        kp_fin_req = nullptr;
     }
     flush_psum();  // no collective of the K·p carried it
-    if (!(sparse_stored() && factored() && world == 1 && sim_world == 0 && csr.rb_csr.nblk > 0))
+    if (kp_fin_done) {
+        kp_fin_done = false;  // the K·p's last kernel formed Ad and the d.Ad partials
+    } else if (!(sparse_stored() && factored() && world == 1 && sim_world == 0 && csr.rb_csr.nblk > 0)) {
         launch_cg_fin_dad<T>(raw.get() + v0, slabs, P, m, q.get() + v0, dv.get() + v0, psum_in, G, QA_cost, cost_inv(),
                              raw_only, vn, Ad.get() + v0, pdad, sc.get(), stream);
+    }
     // x += alpha d; r = b - Q~x every 50th iteration, else r -= alpha Ad   (:119-132)
     launch_cg_upd_rr<T>(x.get() + v0, r.get() + v0, dv.get() + v0, Ad.get() + v0, b.get() + v0, reset,
                         gather_partials(pdad, 1), G, vn, prr, sc.get(), stream);

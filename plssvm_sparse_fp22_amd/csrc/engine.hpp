@@ -108,6 +108,16 @@ struct engine : engine_base {
     bool cg_active = false;
     static constexpr int CG_RESET = 50;  // r = b - Q~x every 50th iteration (csvm.cpp:119-132)
     hipGraphExec_t cg_graph = nullptr;   // one captured block of CG_RESET iterations (graph_block)
+    // a CG iteration's finalize (Ad, d.Ad partials) offered to the K·p: a path that can form it in its own last
+    // kernel (the kernel expansion's combine) does so and sets kp_fin_done; cg_iter launches it otherwise
+    struct kp_fin_t {
+        const T *q, *d, *psum;
+        int G;
+        T QA_cost, cost_inv;
+        T *Ad, *pdad;
+    };
+    const kp_fin_t *kp_fin_req = nullptr;
+    bool kp_fin_done = false;
     cg_scalars<T> polled{};               // the CG scalars read by the last cg_step poll
     // plssvm_mi_set_progress: called by solve_cg after each polled batch of iterations
     void (*progress)(int64_t, int64_t, const double *, double, double, void *) = nullptr;

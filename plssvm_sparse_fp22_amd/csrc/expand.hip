@@ -27,6 +27,7 @@
 #include <type_traits>
 
 #include "../../include/plssvm_mi355x.h"
+#include "cg_common.hpp"
 #include "engine.hpp"
 
 namespace plssvm_mi {
@@ -670,6 +671,14 @@ __global__ __launch_bounds__(256) void exp_cell_fill_empty_kernel(int64_t R, int
     if (cnt[idx] == 0) cnt[idx] = 4;
 }
 
+#ifndef EXP_JH
+#define EXP_JH 1  // flagged layout: a chunk's 4 indices and 4 bfloat16 H side by side (one 16-byte load per lane)
+#endif
+// flagged layout, EXP_JH: slot t of chunk c = t / 4 keeps its index at 8 c + t % 4 and its H at 8 c + 4 + t % 4
+// of the one array (0: two arrays, index and H at t)
+__device__ __forceinline__ int64_t exp_jh_j(int64_t t) { return EXP_JH ? ((t & ~int64_t(3)) << 1) + (t & 3) : t; }
+__device__ __forceinline__ int64_t exp_jh_h(int64_t t) { return EXP_JH ? ((t & ~int64_t(3)) << 1) + 4 + (t & 3) : t; }
+
 // exp_cell_scatter_kernel for the flagged layout (bfloat16 H, buffers zeroed): every window of the row in
 // order, its entries (or a dummy), bit 14 set on the cell's first H
 template <typename T>
@@ -689,11 +698,11 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_flag_kernel(const int64_
             const T h = sv[s];
             if (h == T(0)) continue;  // pads
             if (sj[s] / CW != W) break;
-            hjl[base + k] = (uint16_t) (sj[s] - W * CW);
-            hv16[base + k] = bf16_rne((float) h);
+            hjl[exp_jh_j(base + k)] = (uint16_t) (sj[s] - W * CW);
+            hv16[exp_jh_h(base + k)] = bf16_rne((float) h);
             ++k;
         }
-        hv16[base] |= (uint16_t) 0x4000u;  // k == 0: the dummy (j = 0, H = 0)
+        hv16[exp_jh_h(base)] |= (uint16_t) 0x4000u;  // k == 0: the dummy (j = 0, H = 0)
     }
 }
 
@@ -888,6 +897,12 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             const int64_t cc = c + 64 * hh, cl = cc < s_end ? cc : s_end - 1;
             group_regs &g = nx[hh];
             if constexpr (!RF) g.rl = (int) __builtin_nontemporal_load(hrow + cl);
+            if constexpr (RF && EXP_JH) {  // indices and H of the chunk in one 16-byte load
+                const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(hjl + 8 * cl));
+                g.jj = u32x2{ v.x, v.y };
+                g.hb = u32x2{ v.z, v.w };
+                continue;
+            }
             g.jj = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hjl + 4 * cl));
             if constexpr (HB) {
                 g.hb = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hv16 + 4 * cl));
@@ -1154,21 +1169,14 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *_
 // H_ii w_i + hs_i, hs_i = the remainder stream's row sum) [- the diagonal's pair part when only the overlap part is asked for], in fp64.
 // jslab != null: the CSR pass left its P < 16 panel slabs (jslab[q][i - r0]) and J_i is their sum from 0 in
 // panel order — panel_reduce_kernel's sum, bit for bit, without its launch
+// one row of the combine (rows [r0, r1)): the body of exp_combine_kernel, shared with the fused combine +
+// CG finalize so both compile the same arithmetic
 template <typename T>
-__global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ e, const T *__restrict__ w,
-                                                          const T *__restrict__ hdiag, const T *__restrict__ phin,
-                                                          const T *__restrict__ hs, const T *__restrict__ hslab, int G,
-                                                          const T *__restrict__ jslab, int P,
-                                                          const T *__restrict__ ssc, T kappa,
-                                                          int64_t ib, int64_t ie, int64_t r0, int64_t r1, int overlap_only,
-                                                          T *__restrict__ raw, const cg_scalars<T> *__restrict__ status) {
-    if (status != nullptr && status->converged) return;
-    const int64_t i = ib + (int64_t) blockIdx.x * blockDim.x + threadIdx.x;  // rows [ib, ie)
-    if (i >= ie) return;
-    if (i < r0 || i >= r1) {
-        raw[i] = T(0);
-        return;
-    }
+__device__ __forceinline__ T exp_combine_row(const T *__restrict__ e, const T *__restrict__ w, const T *__restrict__ hdiag,
+                                             const T *__restrict__ phin, const T *__restrict__ hs,
+                                             const T *__restrict__ hslab, int G, const T *__restrict__ jslab, int P,
+                                             const T *__restrict__ raw, const T *__restrict__ ssc, T kappa, int64_t i,
+                                             int64_t r0, int64_t r1, int overlap_only) {
     const double wi = (double) w[i];
     T h = 0;  // the remainder stream's row sum (G window groups: their slabs in g order)
     if (G > 1) {
@@ -1192,7 +1200,53 @@ __global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ 
         const double base = (e != nullptr ? (double) e[i] : (double) kappa) * (double) ssc[0];
         v = base + sc * t;
     }
-    raw[i] = (T) v;
+    return (T) v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ e, const T *__restrict__ w,
+                                                          const T *__restrict__ hdiag, const T *__restrict__ phin,
+                                                          const T *__restrict__ hs, const T *__restrict__ hslab, int G,
+                                                          const T *__restrict__ jslab, int P,
+                                                          const T *__restrict__ ssc, T kappa,
+                                                          int64_t ib, int64_t ie, int64_t r0, int64_t r1, int overlap_only,
+                                                          T *__restrict__ raw, const cg_scalars<T> *__restrict__ status) {
+    if (status != nullptr && status->converged) return;
+    const int64_t i = ib + (int64_t) blockIdx.x * blockDim.x + threadIdx.x;  // rows [ib, ie)
+    if (i >= ie) return;
+    if (i < r0 || i >= r1) {
+        raw[i] = T(0);
+        return;
+    }
+    raw[i] = exp_combine_row<T>(e, w, hdiag, phin, hs, hslab, G, jslab, P, raw, ssc, kappa, i, r0, r1, overlap_only);
+}
+
+// the combine of a CG iteration's K·p fused with the iteration's finalize (cg_fin_dad_kernel): rows [r0, r1) =
+// the CG's own rows, in cg_fin_dad_kernel's grid (RED_BLOCKS x CG_NT), element order and partials — Ad and the
+// d.Ad partials bit for bit those of the two launches, raw is not written
+template <typename T>
+__global__ __launch_bounds__(cgk::CG_NT) void exp_combine_fin_kernel(
+    const T *__restrict__ e, const T *__restrict__ w, const T *__restrict__ hdiag, const T *__restrict__ hs,
+    const T *__restrict__ hslab, int G, const T *__restrict__ jslab, int P, const T *__restrict__ raw,
+    const T *__restrict__ ssc, T kappa, int64_t r0, int64_t r1, const T *__restrict__ q, const T *__restrict__ d,
+    const T *__restrict__ psum, int GP, T QA_cost, T cost_inv, T *__restrict__ Ad, T *__restrict__ pdad,
+    cg_scalars<T> *sc) {
+    if (sc->converged) return;
+    __shared__ T red[cgk::CG_NT / 64], bc[1];
+    T sp, sqp;
+    cgk::partials_total(psum, GP, red, bc, sp, sqp);
+    if (blockIdx.x == 0 && threadIdx.x == 0) sc->sp = sp, sc->sqp = sqp;
+    const int64_t st = (int64_t) gridDim.x * blockDim.x;
+    T s1 = 0;
+    for (int64_t k = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; k < r1 - r0; k += st) {
+        const int64_t i = r0 + k;
+        const T rw = exp_combine_row<T>(e, w, hdiag, nullptr, hs, hslab, G, jslab, P, raw, ssc, kappa, i, r0, r1, 0);
+        const T di = d[i];
+        const T v = cgk::cg_fin_value(rw, q[i], di, sp, sqp, QA_cost, cost_inv, 0);
+        Ad[i] = v;
+        s1 = cgk::cg_acc(s1, di, v);
+    }
+    cgk::store_partials(s1, T(0), red, pdad);
 }
 
 template <typename T>
@@ -1727,9 +1781,10 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
             }
             scan(ncnt);
             ex.nchunks = ex.slots / 4;
-            ex.hjl.alloc(std::max<int64_t>(ex.slots, 4), stream);
+            ex.hjl.alloc(std::max<int64_t>(ex.slots, 4) * (ex.rflags && EXP_JH ? 2 : 1), stream);
             if (ex.hbf16) {
-                ex.hv16.alloc(std::max<int64_t>(ex.slots, 4), stream);
+                if (ex.rflags && EXP_JH) ex.hv16.reset();
+                else ex.hv16.alloc(std::max<int64_t>(ex.slots, 4), stream);
                 ex.wv16.alloc(round_up(std::max<int64_t>({ m, chunk * G, 8 }), (int64_t) 8), stream);
             }
             else ex.hv.alloc(std::max<int64_t>(ex.slots, 4), stream);
@@ -1737,7 +1792,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
                 ex.hrow.reset();
                 hipLaunchKernelGGL(exp_cell_scatter_flag_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
                                    off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
-                                   ex.hv16.get());
+                                   EXP_JH ? ex.hjl.get() : ex.hv16.get());
                 MI_LAUNCH_CHECK();
             } else {
                 ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
@@ -1883,7 +1938,10 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     // (a simulated rank of such a group runs the same kernels without the collectives: timing only)
     const bool rgrp = shard && comm != nullptr && cstream != nullptr && d > 0;
     const bool g16 = shard && d > 0 && ex.hbf16 && (rgrp || sim_world > 0);
-    if (g16) {
+    // unsharded with bfloat16 windows: w, its bfloat16 copy and the S partials in one pass (exp_wown_kernel over
+    // all rows: exp_w_kernel's w and exp_wsum_kernel's partials, bit for bit)
+    const bool wown_all = !shard && ex.hbf16;
+    if (g16 || wown_all) {
         hipLaunchKernelGGL(exp_wown_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, stream, kernel == 2 ? csr.e.get() : nullptr,
                            p, ib, ie, ex.wv.get(), ex.wv16.get(), red.get(), status);
         MI_LAUNCH_CHECK();
@@ -1940,9 +1998,11 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
         expansion_dominant(w, status);
     } else {
         gather_input(w);
-        hipLaunchKernelGGL(exp_wsum_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, stream, w, m,
-                           ex.hbf16 ? ex.wv16.get() : nullptr, red.get(), status);  // S = sum_j w_j (+ bf16 w)
-        MI_LAUNCH_CHECK();
+        if (!wown_all) {
+            hipLaunchKernelGGL(exp_wsum_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, stream, w, m,
+                               ex.hbf16 ? ex.wv16.get() : nullptr, red.get(), status);  // S = sum_j w_j (+ bf16 w)
+            MI_LAUNCH_CHECK();
+        }
         launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
         expansion_moments(w, status);
         expansion_dominant(w, status);
@@ -1957,6 +2017,21 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     const auto &pc = csr.spmv_csr;
     const bool jfuse = pc.P > 1 && pc.P < 16 && pc.nseg == r1 - r0 && pc.nblocks > 0;
     if (r1 > r0) launch_panel_spmv<T>(pc, ex.M.get(), d, raw.get() + r0, status, stream, ex.KM, 2, !jfuse);
+    // a CG iteration on its own rows (one GPU, or a sharded rank): the combine and the iteration's finalize in
+    // one launch (the gathered partials it needs are in place: carried by the K·p's collective or flushed here)
+    if (kp_fin_req != nullptr && with_base && r1 > r0 && ib == r0 && ie == r1 && ib == v0 && ie - ib == vn &&
+        (shard || (world == 1 && sim_world == 0))) {
+        flush_psum();
+        const kp_fin_t &f = *kp_fin_req;
+        hipLaunchKernelGGL(exp_combine_fin_kernel<T>, dim3(RED_BLOCKS), dim3(cgk::CG_NT), 0, stream,
+                           kernel == 2 ? csr.e.get() : nullptr, w, ex.hdiag.get(), ex.hs.get(),
+                           ex.G > 1 ? ex.hslab.get() : nullptr, ex.G, jfuse ? pc.partial.get() : nullptr, (int) pc.P,
+                           raw.get(), csr.ssc.get(), kappa, r0, r1, f.q, f.d, f.psum, f.G, f.QA_cost, f.cost_inv, f.Ad,
+                           f.pdad, sc.get());
+        MI_LAUNCH_CHECK();
+        kp_fin_done = true;
+        return;  // sharded (or one rank): nothing to gather
+    }
     if (ie > ib)
         hipLaunchKernelGGL(exp_combine_kernel<T>, dim3((unsigned) ceil_div(ie - ib, 256)), dim3(256), 0, stream,
                            kernel == 2 ? csr.e.get() : nullptr, w, ex.hdiag.get(), ex.phin.get(), ex.hs.get(),
