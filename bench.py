@@ -223,7 +223,10 @@ def main():
     ap.add_argument("--kp-reps", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true",
-                    help="skip the sparse BASELINE rows measured beside the default headline (configs[2], 3-RBF) and its learn() timing (profiling runs: a converged solve's early-exit launches would enter the kernel averages)")
+                    help="skip the sparse BASELINE rows measured beside the default headline (configs[2], 3-RBF)")
+    ap.add_argument("--no-solve", action="store_true",
+                    help="skip the default line's learn() timing (profiling runs: a converged solve's early-exit "
+                         "launches would enter the kernel averages)")
     ap.add_argument("--host-exchange", action="store_true",
                     help="N > 1: exchange through the host over gloo (plssvm_mi_comm_init_host) instead of RCCL")
     ap.add_argument("--sim-rank", default=None, metavar="R/W",
@@ -268,7 +271,7 @@ def main():
     rec = run_config(args.config, args, rank, world, dist, uid, args.steps, args.warmup, not args.no_cpu,
                      args.cpu_seconds, args.kp_reps, sim=sim, kernel=args.kernel, dtype=args.dtype,
                      points=args.points, features=args.features, data_cache=cache,
-                     solve=(args.solve or (default_run and not args.no_extra)) and world == 1)
+                     solve=(args.solve or default_run) and not args.no_solve and world == 1)
     extra = None
     if default_run and not args.no_extra:
         # north_star's sparse target measured under the same clock: configs[2] with RBF (the >= 70 % HBM

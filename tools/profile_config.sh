@@ -12,9 +12,9 @@ mkdir -p "$out"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
-  python3 "$root/bench.py" --config "$config" --steps 5 --warmup 1 --no-cpu --no-extra "$@" > "$out/bench_trace.json" 2> "$out/trace.log"
+  python3 "$root/bench.py" --config "$config" --steps 5 --warmup 1 --no-cpu --no-extra --no-solve "$@" > "$out/bench_trace.json" 2> "$out/trace.log"
 timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc" -o run -- \
-  python3 "$root/bench.py" --config "$config" --steps 2 --warmup 0 --kp-reps 2 --no-cpu --no-extra "$@" > "$out/bench_pmc.json" 2> "$out/pmc.log"
+  python3 "$root/bench.py" --config "$config" --steps 2 --warmup 0 --kp-reps 2 --no-cpu --no-extra --no-solve "$@" > "$out/bench_pmc.json" 2> "$out/pmc.log"
 # keep only the summaries gpurun copies back (traces of long runs exceed its 64 MiB limit)
 find "$out" -type f ! -name '*kernel_stats.csv' ! -name '*counter_collection.csv' ! -name '*.json' ! -name '*.log' -delete
 find "$out" -name '*counter_collection.csv' -size +8M -exec gzip {} \;
