@@ -707,6 +707,17 @@ void engine<T>::learn(const T *y, int64_t imax, T eps, T *alpha_out, double *bia
     if (bias_out) *bias_out = (double) bias;
 }
 
+// time_kp's cache eviction: reads n 16-byte words (their contents are never used; the sink is written only
+// for a value no sweep produces in practice, which keeps the loads)
+__global__ __launch_bounds__(256) void flush_read_kernel(const uint4 *__restrict__ a, int64_t n, unsigned *__restrict__ sink) {
+    unsigned s = 0;
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
+        const uint4 v = a[i];
+        s ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (s == 0x9E3779B9u) sink[0] = s;
+}
+
 template <typename T>
 void engine<T>::time_kp(int reps, double *ms_kp, double *ms_dom) {
     need_data();
@@ -730,8 +741,23 @@ void engine<T>::time_kp(int reps, double *ms_kp, double *ms_dom) {
     MI_HIP_CHECK(hipEventSynchronize(e1));
     float ms = 0;
     MI_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-    // dominant kernel alone, same stream, same launches
+    // dominant kernel alone, same stream, same launches; before each launch a 512 MiB read sweep evicts what
+    // the previous launch left in the L2s and the Infinity Cache (256 MiB), as the other kernels of a CG
+    // iteration do between two launches — back-to-back launches would otherwise re-read part of their stream
+    // from there (a read, not a memset: dirty lines would be written back during the timed launch)
+    dev_buf<uint4> flush;
+    try {
+        flush.alloc(((int64_t) 512 << 20) / 16 + 1, stream, false);
+    } catch (const mi_error &) {
+        flush.reset();  // no room: time without the eviction
+        (void) hipGetLastError();
+    }
     for (int it = 0; it < reps; ++it) {
+        if (flush.get() != nullptr) {
+            hipLaunchKernelGGL(flush_read_kernel, dim3(4096), dim3(256), 0, stream, flush.get(), flush.size() - 1,
+                               reinterpret_cast<unsigned *>(flush.get() + flush.size() - 1));
+            MI_LAUNCH_CHECK();
+        }
         MI_HIP_CHECK(hipEventRecord(d0, stream));
         if (sparse_stored()) {
             sparse_dominant(pv.get(), nullptr);

@@ -43,10 +43,20 @@ constexpr int SELL_WAVES = SELL_NT / 64;
 #endif
 constexpr int SELL_XBYTES = PLSSVM_MI_SELL_XBYTES;  // LDS panel of the gathered vector (all of a CU's LDS)
 constexpr int SELL_SIGMA = 4096;    // sorting window (segments)
+// entries per lane in flight per step: the passes are bound by the bytes in flight per CU (one 1024-thread
+// workgroup per CU, every step's loads issued together). Measured on one box (round 3, CG it/s): real-typed
+// values 4 / 6 / 8 entries: config 3 6 777 / 7 011 / 7 203, 3-RBF 958 / 961 / 969; packed FP22 (8-byte loads
+// per value) config 5 778 / 771 / 761 — so 8 for real values, 4 for FP22 (round 2, before the row-block pass
+// and the 16-bit pair loads, measured 4 best for both)
 #ifndef PLSSVM_MI_SELL_UNROLL
-#define PLSSVM_MI_SELL_UNROLL 4
+#define PLSSVM_MI_SELL_UNROLL 8
 #endif
-constexpr int SELL_UNROLL = PLSSVM_MI_SELL_UNROLL;  // entries per lane in flight per step
+#ifndef PLSSVM_MI_SELL_UNROLL_F22
+#define PLSSVM_MI_SELL_UNROLL_F22 4
+#endif
+template <bool F22>
+constexpr int sell_unroll() { return F22 ? PLSSVM_MI_SELL_UNROLL_F22 : PLSSVM_MI_SELL_UNROLL; }
+constexpr int SELL_UNROLL = PLSSVM_MI_SELL_UNROLL;
 // IDX2: the 16-bit panel indices of entries 2t, 2t+1 of a slot are adjacent, so one 32-bit load per lane
 // (256 B per wave-instruction) fetches two; chunk widths are padded to even
 #ifndef PLSSVM_MI_SELL_IDX2
@@ -61,7 +71,7 @@ constexpr bool SELL_IDX2 = PLSSVM_MI_SELL_IDX2 != 0;
 constexpr bool SELL_VAL2 = SELL_IDX2 && PLSSVM_MI_SELL_VAL2 != 0;
 // storage position of the entry at value position t = off + 64 j + l (off % 128 == 0 when paired)
 inline int64_t sell_pair_pos(int64_t t) { return (t & ~int64_t(127)) + 2 * (t & 63) + ((t >> 6) & 1); }
-static_assert(!SELL_IDX2 || SELL_UNROLL % 2 == 0, "paired indices need an even step");
+static_assert(!SELL_IDX2 || (sell_unroll<false>() % 2 == 0 && sell_unroll<true>() % 2 == 0), "paired indices need an even step");
 template <typename T>
 constexpr int sell_width() { return SELL_XBYTES / (int) sizeof(T); }
 // workgroups per pass: equal-cost chunk ranges, a multiple of the 256 CUs (one resident workgroup per
@@ -149,6 +159,7 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
     constexpr int XC = MODE == 2 ? KC : 1;   // channels of the gathered vector
     constexpr int OC = MODE == 1 ? KC : 1;   // outputs per segment
     constexpr int XW = LDSX ? sell_width<T>() : 1;
+    constexpr int SU = sell_unroll<F22>();
     using idx_t = typename sell_idx<LDSX>::type;
     __shared__ T xs[XW];
     if (status != nullptr && status->converged) return;
@@ -200,17 +211,17 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
             const sell_chunk ch = chunks[c];
             const int seg = perm[(int64_t) c * 64 + lane];
             const int64_t base = ch.off + lane;
-            // steps of SELL_UNROLL entries; a step past the width re-reads the slot's last entry (same
+            // steps of SU entries; a step past the width re-reads the slot's last entry (same
             // cache line) and masks it, so every step issues all of its loads at once
             const int last = max(ch.width - 1, 0);
             T acc[OC];
 #pragma unroll
             for (int k = 0; k < OC; ++k) acc[k] = T(0);
-            for (int j = 0; j < ch.width; j += SELL_UNROLL) {
-                idx_t ci[SELL_UNROLL];
-                T vi[SELL_UNROLL];
+            for (int j = 0; j < ch.width; j += SU) {
+                idx_t ci[SU];
+                T vi[SU];
 #pragma unroll
-                for (int u = 0; u < SELL_UNROLL; ++u) {
+                for (int u = 0; u < SU; ++u) {
                     const int64_t k = base + (int64_t) min(j + u, last) * 64;
                     if constexpr (!(LDSX && SELL_IDX2)) ci[u] = __builtin_nontemporal_load(idx + k);
                     if constexpr (!(LDSX && SELL_VAL2)) {
@@ -225,7 +236,7 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
                     const V2 *vp = reinterpret_cast<const V2 *>(val.v) + (ch.off >> 1) + lane;
                     const int lastp = max((ch.width >> 1) - 1, 0);
 #pragma unroll
-                    for (int u2 = 0; u2 < SELL_UNROLL / 2; ++u2) {
+                    for (int u2 = 0; u2 < SU / 2; ++u2) {
                         const V2 pr = __builtin_nontemporal_load(vp + (int64_t) min((j >> 1) + u2, lastp) * 64);
                         vi[2 * u2] = pr.x;
                         vi[2 * u2 + 1] = pr.y;
@@ -235,14 +246,14 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
                     const uint32_t *ip = reinterpret_cast<const uint32_t *>(idx) + (ch.off >> 1) + lane;
                     const int lastp = max((ch.width >> 1) - 1, 0);
 #pragma unroll
-                    for (int u2 = 0; u2 < SELL_UNROLL / 2; ++u2) {
+                    for (int u2 = 0; u2 < SU / 2; ++u2) {
                         const uint32_t pr = __builtin_nontemporal_load(ip + (int64_t) min((j >> 1) + u2, lastp) * 64);
                         ci[2 * u2] = (idx_t) (pr & 0xFFFFu);
                         ci[2 * u2 + 1] = (idx_t) (pr >> 16);
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < SELL_UNROLL; ++u) {
+                for (int u = 0; u < SU; ++u) {
                     const T v = j + u < ch.width ? vi[u] : T(0);
                     if constexpr (MODE == 0) {
                         acc[0] = fma(v, gx(xg, (int64_t) ci[u]), acc[0]);
@@ -558,6 +569,7 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
     int64_t xn, int64_t nrows, const T *__restrict__ q, const T *__restrict__ d, const T *__restrict__ psum,
     T QA_cost, T cost_inv, T *__restrict__ Ad, T *__restrict__ pdad, const cg_scalars<T> *__restrict__ status) {
     constexpr int XW = rb_width<T>(), RB = rb_rows<T>();
+    constexpr int SU = sell_unroll<F22>();
     __shared__ T xs[XW];
     __shared__ T racc[RB];
     T *red = racc, *bc = racc + SELL_WAVES;  // block-reduction scratch (before / after the accumulator's use)
@@ -623,19 +635,19 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
             const int lastp = max((ch.width >> 1) - 1, 0);
             const uint32_t *ip = reinterpret_cast<const uint32_t *>(idx) + (ch.off >> 1) + lane;
             T acc = T(0);
-            for (int j = 0; j < ch.width; j += SELL_UNROLL) {
-                uint16_t ci[SELL_UNROLL];
-                T vi[SELL_UNROLL];
+            for (int j = 0; j < ch.width; j += SU) {
+                uint16_t ci[SU];
+                T vi[SU];
 #pragma unroll
-                for (int u = 0; u < SELL_UNROLL; ++u) vi[u] = sell_val<T, F22>(val, base + (int64_t) min(j + u, last) * 64);
+                for (int u = 0; u < SU; ++u) vi[u] = sell_val<T, F22>(val, base + (int64_t) min(j + u, last) * 64);
 #pragma unroll
-                for (int u2 = 0; u2 < SELL_UNROLL / 2; ++u2) {
+                for (int u2 = 0; u2 < SU / 2; ++u2) {
                     const uint32_t pr = __builtin_nontemporal_load(ip + (int64_t) min((j >> 1) + u2, lastp) * 64);
                     ci[2 * u2] = (uint16_t) (pr & 0xFFFFu);
                     ci[2 * u2 + 1] = (uint16_t) (pr >> 16);
                 }
 #pragma unroll
-                for (int u = 0; u < SELL_UNROLL; ++u) {
+                for (int u = 0; u < SU; ++u) {
                     const T v = j + u < ch.width ? vi[u] : T(0);
                     acc = fma(v, xs[ci[u]], acc);
                 }
