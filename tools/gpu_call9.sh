@@ -11,3 +11,8 @@ b=json.loads(open('gpurun_out/c9/bench.json').read().strip().splitlines()[-1])
 for n,r in [('headline',b)]+list(b['extra'].items()):
     print(n, round(r['value'],1), round(r['roofline']['launch_ms'],4), round(r['kp_ms'],4), round(r['roofline']['frac'],3))"
 bash tools/profile_config.sh r03_csr_linear_1m csr_linear_1m || exit $?
+for v in int2 s16; do
+  sv=""; [ $v = int2 ] && sv=int2
+  PLSSVM_MI_OTF_SEG=$sv timeout -k 10 300 python tools/density_1pct.py --algo onthefly --reps 3 > gpurun_out/c9/dens_$v.json 2> gpurun_out/c9/dens_$v.err || exit $?
+  python3 -c "import json; d=json.load(open('gpurun_out/c9/dens_$v.json')); print('$v', d['kp_s'], d['max_rel_err'], d['ok'])"
+done
