@@ -16,9 +16,6 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
-#include <cstring>
-#include <type_traits>
-#include <vector>
 
 #include "../../include/plssvm_mi355x.h"
 #include "engine.hpp"
@@ -139,26 +136,6 @@ __global__ __launch_bounds__(256) void otf_seg_kernel(const int64_t *__restrict_
     };
     const int64_t lo = first_at_least(W * CW), hi = first_at_least((W + 1) * CW);
     seg[t] = make_int2((int) (lo - a), (int) (hi - lo));
-}
-
-// segc[f][W] = the first entry of column f with row >= W CW, column-local, W = 0..nW (16-bit: every column has
-// fewer than 65536 entries). A window's segment is [segc[f][W], segc[f][W + 1]): 2 B per (feature, window)
-// instead of seg's 8, so a line holds 32 windows of a feature instead of 8 — the segment table's scattered
-// lookups (one per feature of a row per window) miss the caches 4x less often
-__global__ __launch_bounds__(256) void otf_segc_kernel(const int64_t *__restrict__ colptr,
-                                                       const int32_t *__restrict__ crow, int64_t d, int64_t nW,
-                                                       int64_t CW, uint16_t *__restrict__ segc) {
-    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (nW + 1) * d) return;
-    const int64_t f = t / (nW + 1), W = t - f * (nW + 1);
-    const int64_t a = colptr[f], b = colptr[f + 1], key = W * CW;
-    int64_t lo = a, hi = b;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int64_t) crow[mid] < key) lo = mid + 1;
-        else hi = mid;
-    }
-    segc[t] = (uint16_t) (lo - a);
 }
 
 // ecb[k] = colptr[col[k]]: the CSC start of each CSR entry's column (read coalesced with the row)
@@ -296,11 +273,10 @@ __device__ __forceinline__ void otf_batch2(T *__restrict__ s, const otf_jv<T> *_
 }
 
 // raw[i] = sum_{j != i, s_ij != 0} c_ij p_j for this rank's rows i in [r0, r1)
-template <typename T, int CWB, bool S16>
+template <typename T, int CWB>
 __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
                                                         const T *__restrict__ val, const int64_t *__restrict__ ecb,
-                                                        const otf_jv<T> *__restrict__ cjv, const int2 *__restrict__ seg,
-                                                        const uint16_t *__restrict__ segc, const T *__restrict__ norms,
+                                                        const otf_jv<T> *__restrict__ cjv, const int2 *__restrict__ seg, const T *__restrict__ norms,
                                                         const T *__restrict__ ev, const pne_t<T> *__restrict__ pne, int64_t m,
                                                         int64_t nW, int64_t r0, int64_t r1, otf_pair<T> pf,
                                                         int64_t Wa, int64_t Wb, double *__restrict__ part,
@@ -322,27 +298,13 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
     const int32_t f0 = h0 ? col[b0 + lane] : 0;
     const T v0 = h0 ? val[b0 + lane] : T(0);
     const int64_t c0 = h0 ? ecb[b0 + lane] : 0;
-    int2 sg0 = make_int2(0, 0);
-    int e0 = 0, e1n = 0;  // S16: this window's start and the next window's start (= this window's end)
-    if constexpr (S16) {
-        if (h0) e0 = segc[(int64_t) f0 * (nW + 1) + Wa], e1n = segc[(int64_t) f0 * (nW + 1) + Wa + 1];
-    } else {
-        if (h0) sg0 = seg[(int64_t) f0 * nW + Wa];
-    }
+    int2 sg0 = h0 ? seg[(int64_t) f0 * nW + Wa] : make_int2(0, 0);
     double acc = 0.0;
     for (int64_t W = Wa; W < Wb; ++W) {
         const int j0 = (int) (W * CW);
         if (nz > 0) {
-            int2 sg;
-            if constexpr (S16) {
-                const int e1 = e1n;
-                e1n = h0 && W + 1 < Wb ? (int) segc[(int64_t) f0 * (nW + 1) + W + 2] : 0;
-                sg = make_int2(e0, e1 - e0);
-                e0 = e1;
-            } else {
-                sg = sg0;
-                sg0 = h0 && W + 1 < Wb ? seg[(int64_t) f0 * nW + W + 1] : make_int2(0, 0);
-            }
+            const int2 sg = sg0;
+            sg0 = h0 && W + 1 < Wb ? seg[(int64_t) f0 * nW + W + 1] : make_int2(0, 0);
             if constexpr (OTF_V2) otf_batch2<T>(s, cjv, j0, (int) (nz < 64 ? nz : 64), c0 + sg.x, sg.y, v0, lane);
             else otf_batch<T>(s, cjv, j0, (int) (nz < 64 ? nz : 64), c0 + sg.x, sg.y, v0, lane);
         }
@@ -354,16 +316,9 @@ __global__ __launch_bounds__(OTF_NT) void otf_kp_kernel(const int64_t *__restric
             if (k < nz) {
                 const int32_t f = col[b0 + k];
                 v = val[b0 + k];
-                if constexpr (S16) {
-                    const uint16_t *sc = segc + (int64_t) f * (nW + 1) + W;
-                    const int s0 = sc[0], s1 = sc[1];
-                    lo = ecb[b0 + k] + s0;
-                    len = s1 - s0;
-                } else {
-                    const int2 sg = seg[(int64_t) f * nW + W];
-                    lo = ecb[b0 + k] + sg.x;
-                    len = sg.y;
-                }
+                const int2 sg = seg[(int64_t) f * nW + W];
+                lo = ecb[b0 + k] + sg.x;
+                len = sg.y;
             }
             if constexpr (OTF_V2) otf_batch2<T>(s, cjv, j0, (int) (nz - q0 < 64 ? nz - q0 : 64), lo, len, v, lane);
             else otf_batch<T>(s, cjv, j0, (int) (nz - q0 < 64 ? nz - q0 : 64), lo, len, v, lane);
@@ -420,33 +375,11 @@ void engine<T>::setup_otf(int rbf_fact_ok) {
     const int64_t CW = otf_cwb() / (int64_t) sizeof(T);
     csr.otf_cw = (int) CW;
     csr.otf_nw = ceil_div(std::max<int64_t>(m, 1), CW);
-    // 16-bit cumulative segment table when every column has fewer than 65536 entries (PLSSVM_MI_OTF_SEG=int2
-    // keeps the (start, count) pairs)
-    {
-        std::vector<int64_t> cp((size_t) d + 1, 0);
-        MI_HIP_CHECK(hipMemcpyAsync(cp.data(), csr.colptr.get(), sizeof(int64_t) * (size_t) (d + 1), hipMemcpyDeviceToHost,
-                                    stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-        int64_t cmax = 0;
-        for (int64_t f = 0; f < d; ++f) cmax = std::max(cmax, cp[(size_t) f + 1] - cp[(size_t) f]);
-        const char *se = std::getenv("PLSSVM_MI_OTF_SEG");
-        csr.otf_s16 = cmax < 65536 && !(se != nullptr && std::strcmp(se, "int2") == 0);
-    }
-    if (csr.otf_s16) {
-        const int64_t tc = (csr.otf_nw + 1) * d;
-        csr.seg.reset();
-        csr.segc.alloc(std::max<int64_t>(tc, 1), stream, false);
-        if (tc > 0)
-            hipLaunchKernelGGL(otf_segc_kernel, dim3((unsigned) ceil_div(tc, 256)), dim3(256), 0, stream, csr.colptr.get(),
-                               csr.crow.get(), d, csr.otf_nw, CW, csr.segc.get());
-    } else {
-        const int64_t tot = csr.otf_nw * d;
-        csr.segc.reset();
-        csr.seg.alloc(std::max<int64_t>(tot, 1), stream, false);
-        if (tot > 0)
-            hipLaunchKernelGGL(otf_seg_kernel, dim3((unsigned) ceil_div(tot, 256)), dim3(256), 0, stream, csr.colptr.get(),
-                               csr.crow.get(), d, csr.otf_nw, CW, csr.seg.get());
-    }
+    const int64_t tot = csr.otf_nw * d;
+    csr.seg.alloc(std::max<int64_t>(tot, 1), stream, false);
+    if (tot > 0)
+        hipLaunchKernelGGL(otf_seg_kernel, dim3((unsigned) ceil_div(tot, 256)), dim3(256), 0, stream, csr.colptr.get(),
+                           csr.crow.get(), d, csr.otf_nw, CW, csr.seg.get());
     MI_LAUNCH_CHECK();
     csr.pne.alloc(4 * std::max<int64_t>(m, 1), stream, false);
     csr.otf_part.alloc(std::max<int64_t>(m, 1), stream, false);
@@ -505,21 +438,16 @@ void engine<T>::otf_dominant(const T *p, const cg_scalars<T> *status) {
             const int64_t Wb = std::min(nW, Wa + wpl);
             hipLaunchKernelGGL(kern, dim3((unsigned) ceil_div(r1 - r0, OTF_NT / 64)), dim3(OTF_NT), 0, stream,
                                csr.rowptr.get(), csr.col.get(), csr.val.get(), csr.ecb.get(),
-                               reinterpret_cast<const otf_jv<T> *>(csr.cjv.get()), csr.seg.get(), csr.segc.get(), norms.get(),
+                               reinterpret_cast<const otf_jv<T> *>(csr.cjv.get()), csr.seg.get(), norms.get(),
                                kernel == 2 ? csr.e.get() : nullptr, pne, m, nW, r0, r1, pf, Wa, Wb, csr.otf_part.get(),
                                raw.get(), status);
         }
     };
     const int cwb = csr.otf_cw * (int) sizeof(T);
-    auto pick = [&](auto s16) {
-        constexpr bool S16 = decltype(s16)::value;
-        if (cwb == 32768) launch(otf_kp_kernel<T, 32768, S16>);
-        else if (cwb == 16384) launch(otf_kp_kernel<T, 16384, S16>);
-        else if (cwb == 4096) launch(otf_kp_kernel<T, 4096, S16>);
-        else launch(otf_kp_kernel<T, 8192, S16>);
-    };
-    if (csr.otf_s16) pick(std::true_type{});
-    else pick(std::false_type{});
+    if (cwb == 32768) launch(otf_kp_kernel<T, 32768>);
+    else if (cwb == 16384) launch(otf_kp_kernel<T, 16384>);
+    else if (cwb == 4096) launch(otf_kp_kernel<T, 4096>);
+    else launch(otf_kp_kernel<T, 8192>);
     MI_LAUNCH_CHECK();
 }
 

@@ -892,7 +892,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                 if (fail != 0 && sparse_algo == 4) throw mi_error(fail, why.empty() ? "on-the-fly setup failed on another rank" : why);
                 if (fail != 0) {
                     MI_HIP_CHECK(hipStreamSynchronize(stream));
-                    csr.seg.reset(), csr.segc.reset(), csr.ecb.reset(), csr.pne.reset(), csr.cjv.reset(), csr.otf_part.reset();
+                    csr.seg.reset(), csr.ecb.reset(), csr.pne.reset(), csr.cjv.reset(), csr.otf_part.reset();
                     csr.otf_on = false;
                     otf = false;
                 }

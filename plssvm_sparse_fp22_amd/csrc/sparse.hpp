@@ -140,9 +140,7 @@ struct csr_data {
     int otf_cw = 0;
     int64_t otf_nw = 0;
     int64_t otf_wpl = 0;    // partner windows per launch (0: all; PLSSVM_MI_OTF_WPL at setup)
-    dev_buf<int2> seg;      // [d][otf_nw] (start, count) of each column's window segment
-    dev_buf<uint16_t> segc; // [d][otf_nw + 1] column-local start of each window (otf_s16: every column < 65536 entries)
-    bool otf_s16 = false;
+    dev_buf<int2> seg;      // [d][otf_nw]
     dev_buf<int64_t> ecb;   // [nnz]: colptr[col[k]] per CSR entry
     dev_buf<T> pne;         // [m][4]: p_j, |x_j|^2, e_j, 0 of the current K·p
     dev_buf<T> cjv;         // [nnz][2]: CSC (row, value) pairs (the row as int32 bits in the first slot)
@@ -154,7 +152,7 @@ struct csr_data {
         return rowptr.bytes() + col.bytes() + val.bytes() + colptr.bytes() + crow.bytes() +
                cval.bytes() + spmv_csc.bytes() + spmv_csr.bytes() + rb_csr.bytes() + e.bytes() + pj.bytes() + ps.bytes() +
                rb_base.bytes() + rowoff.bytes() + cells.bytes() + slab_row.bytes() + slab_col.bytes() + ex.bytes() +
-               seg.bytes() + segc.bytes() + ecb.bytes() + pne.bytes() + cjv.bytes() + otf_part.bytes();
+               seg.bytes() + ecb.bytes() + pne.bytes() + cjv.bytes() + otf_part.bytes();
     }
 };
 
