@@ -51,3 +51,25 @@ def test_missing_library_raises(monkeypatch, tmp_path):
     monkeypatch.setattr(_abi, "_lib", None)
     with pytest.raises(ImportError):
         _abi.lib()
+
+
+def test_info_struct_mirrors_the_header(tmp_path):
+    """_abi.Info (ctypes) has the C header's plssvm_mi_info layout: every field at the same offset, same size
+    (a C program compiled against include/plssvm_mi355x.h prints offsetof / sizeof)."""
+    import ctypes
+    import subprocess
+
+    from plssvm_sparse_fp22_amd import _abi
+
+    names = [f[0] for f in _abi.Info._fields_]
+    src = tmp_path / "info.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "plssvm_mi355x.h"\nint main(void) {\n'
+                   + "".join(f'    printf("{n} %zu\\n", offsetof(plssvm_mi_info, {n}));\n' for n in names)
+                   + '    printf("sizeof %zu\\n", sizeof(plssvm_mi_info));\n    return 0;\n}\n')
+    exe = tmp_path / "info"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                       text=True).stdout.splitlines())
+    for n in names:
+        assert int(got[n]) == getattr(_abi.Info, n).offset, n
+    assert int(got["sizeof"]) == ctypes.sizeof(_abi.Info)
