@@ -69,6 +69,13 @@ constexpr bool SELL_IDX2 = PLSSVM_MI_SELL_IDX2 != 0;
 #define PLSSVM_MI_SELL_VAL2 0
 #endif
 constexpr bool SELL_VAL2 = SELL_IDX2 && PLSSVM_MI_SELL_VAL2 != 0;
+// F22PAIR (with IDX2, FP22 streams of the panelled passes only): entries 2t, 2t+1 of a slot adjacent in the packed
+// stream as well, so one 12-byte load per lane (3 words at 4-byte alignment) decodes two values instead of two
+// overlapping 8-byte loads
+#ifndef PLSSVM_MI_SELL_F22PAIR
+#define PLSSVM_MI_SELL_F22PAIR 0
+#endif
+constexpr bool SELL_F22PAIR = SELL_IDX2 && PLSSVM_MI_SELL_F22PAIR != 0;
 // storage position of the entry at value position t = off + 64 j + l (off % 128 == 0 when paired)
 inline int64_t sell_pair_pos(int64_t t) { return (t & ~int64_t(127)) + 2 * (t & 63) + ((t >> 6) & 1); }
 static_assert(!SELL_IDX2 || (sell_unroll<false>() % 2 == 0 && sell_unroll<true>() % 2 == 0), "paired indices need an even step");
@@ -129,6 +136,7 @@ struct spmv_plan {
 // FP22: the two words holding the value come as one 8-byte load at 4-byte alignment (gfx950 global
 // loads take dword-aligned dwordx2; the packed array carries one word of padding)
 typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+typedef uint32_t u32x3_a4 __attribute__((ext_vector_type(3), aligned(4)));
 template <typename T, bool F22>
 __device__ __forceinline__ T sell_val(const vals_t<T> &val, int64_t k) {
     if constexpr (F22) {
@@ -224,11 +232,32 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
                 for (int u = 0; u < SU; ++u) {
                     const int64_t k = base + (int64_t) min(j + u, last) * 64;
                     if constexpr (!(LDSX && SELL_IDX2)) ci[u] = __builtin_nontemporal_load(idx + k);
-                    if constexpr (!(LDSX && SELL_VAL2)) {
+                    if constexpr (LDSX && F22 && SELL_F22PAIR && !SELL_VAL2) {
+                        // paired below
+                    } else if constexpr (!(LDSX && SELL_VAL2)) {
                         vi[u] = sell_val<T, F22>(val, k);
                     } else if constexpr (F22) {
                         const int jj = min(j + u, last);
                         vi[u] = sell_val<T, F22>(val, ch.off + 128 * (int64_t) (jj >> 1) + 2 * lane + (jj & 1));
+                    }
+                }
+                if constexpr (LDSX && F22 && SELL_F22PAIR && !SELL_VAL2) {
+                    // entries jj, jj + 1 (jj even) of this slot at stream positions p, p + 1, p = off + 128 (jj / 2) + 2 lane:
+                    // bits 22 p .. 22 p + 43 lie in the 3 words from (22 p) / 32 (shift 22 p % 32 <= 28)
+                    const int lastp = max((ch.width >> 1) - 1, 0);
+#pragma unroll
+                    for (int u2 = 0; u2 < SU / 2; ++u2) {
+                        const int64_t pp = ch.off + 128 * (int64_t) min((j >> 1) + u2, lastp) + 2 * lane;
+                        const int64_t bit = 22 * pp;
+                        const u32x3_a4 ww = __builtin_nontemporal_load(reinterpret_cast<const u32x3_a4 *>(val.v22 + (bit >> 5)));
+                        const int sh = (int) (bit & 31);
+                        const uint64_t lo = ((uint64_t) ww.y << 32) | ww.x;
+                        const uint32_t c0 = (uint32_t) (lo >> sh) & 0x3FFFFFu;
+                        const int sh1 = sh + 22;  // 22..50: the second value straddles words 1 and 2 when sh1 > 32
+                        const uint64_t hi = ((uint64_t) ww.z << 32) | ww.y;
+                        const uint32_t c1 = (uint32_t) (sh1 >= 32 ? hi >> (sh1 - 32) : lo >> sh1) & 0x3FFFFFu;
+                        vi[2 * u2] = (T) fp22_decode(c0);
+                        vi[2 * u2 + 1] = (T) fp22_decode(c1);
                     }
                 }
                 if constexpr (LDSX && SELL_VAL2 && !F22) {
@@ -370,10 +399,11 @@ inline void launch_panel_spmv(const spmv_plan<T> &pl, const T *x, int64_t xn, T 
     }
 }
 
-// packed FP22 words of v (16 values per 11 words, fp22_words(n) + 1 words), groups on the host threads
+// packed FP22 words of v (16 values per 11 words, fp22_words(n) + 2 words: the paired 3-word loads may read 2 past
+// the last), groups on the host threads
 inline std::vector<uint32_t> fp22_pack_host(const std::vector<float> &v) {
     const int64_t n = (int64_t) v.size(), groups = (n + 15) / 16;
-    std::vector<uint32_t> words((size_t) (fp22_words(n) + 1), 0u);
+    std::vector<uint32_t> words((size_t) (fp22_words(n) + 2), 0u);
     host_parallel(groups, [&](int, int64_t g0, int64_t g1) {
         for (int64_t g = g0; g < g1; ++g)
             for (int k = 0; k < 16 && g * 16 + k < n; ++k) {
@@ -479,7 +509,7 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
                 i16[ti] = (uint16_t) (g - q * W);
             }
             else i32[t] = (int32_t) g;
-            const int64_t tv = (SELL_VAL2 && ldsx) ? sell_pair_pos(t) : t;  // value position
+            const int64_t tv = ((SELL_VAL2 || (fp22 && SELL_F22PAIR)) && ldsx) ? sell_pair_pos(t) : t;  // value position
             if (fp22) vf[tv] = (float) v;
             else vr[tv] = (T) v;
         }, s0, s1);
