@@ -45,19 +45,8 @@ __global__ __launch_bounds__(256) void dot_final_kernel(const T *__restrict__ pa
                                                         T *plain_out) {
     if (op != FIN_PLAIN && sc->converged) return;
     __shared__ T red[8];
-    T s1 = 0, s2 = 0;
-    for (int i = threadIdx.x; i < RED_BLOCKS; i += blockDim.x) {
-        T a = partials[i], b = partials[RED_BLOCKS + i];
-        for (int g = 1; g < G; ++g) {
-            a += partials[g * 2 * RED_BLOCKS + i];
-            b += partials[g * 2 * RED_BLOCKS + RED_BLOCKS + i];
-        }
-        s1 += a;
-        s2 += b;
-    }
-    const T r1 = block_sum(s1, red);
-    __syncthreads();
-    const T r2 = block_sum(s2, red);
+    T r1, r2;
+    partials_final(partials, G, red, r1, r2);
     if (threadIdx.x != 0) return;
     switch (op) {
         case FIN_SP_SQP:

@@ -65,6 +65,25 @@ __device__ __forceinline__ void store_partials(T v1, T v2, T *red, T *__restrict
     }
 }
 
+// dot_final_kernel's sum of the RED_BLOCKS partial pairs (G gathered sets, rank order), for a 256-thread block:
+// every thread its partials, then block_sum — the same bits wherever it runs (thread 0 holds r1, r2)
+template <typename T>
+__device__ __forceinline__ void partials_final(const T *__restrict__ partials, int G, T *red, T &r1, T &r2) {
+    T s1 = 0, s2 = 0;
+    for (int i = threadIdx.x; i < RED_BLOCKS; i += blockDim.x) {
+        T a = partials[i], b = partials[RED_BLOCKS + i];
+        for (int g = 1; g < G; ++g) {
+            a += partials[g * 2 * RED_BLOCKS + i];
+            b += partials[g * 2 * RED_BLOCKS + RED_BLOCKS + i];
+        }
+        s1 += a;
+        s2 += b;
+    }
+    r1 = block_sum(s1, red);
+    __syncthreads();
+    r2 = block_sum(s2, red);
+}
+
 // Ad_i of the CG finalize: raw_i + (QA - q_i) sum(d) - sum(q d) + d_i / C (kp_finalize_kernel's
 // expression, contracted as in dense.hip)
 template <typename T>

@@ -176,9 +176,12 @@ struct engine : engine_base {
     void build_expansion(const int64_t *cpos, int64_t max_inc);   // multi-overlap remainder H, diagonal
     void expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);
     void expansion_dominant(const T *p, const cg_scalars<T> *status);  // the remainder stream
-    void expansion_moments(const T *w, const cg_scalars<T> *status);   // column moments (SELL CSC pass)
+    // column moments (SELL CSC pass); spart: the moment reduce also forms S from w's partials (sG sets)
+    void expansion_moments(const T *w, const cg_scalars<T> *status, const T *spart = nullptr, int sG = 1);
     void expansion_mscale(const cg_scalars<T> *status);                 // moments -> Horner coefficients
-    bool expansion_moment_pass(const T *w, const cg_scalars<T> *status); // true: reduced straight into M
+    bool expansion_moment_pass(const T *w, const cg_scalars<T> *status, const T *spart = nullptr,
+                               int sG = 1);  // true: reduced straight into M
+    bool expansion_moments_fused() const;  // the moment pass has panel slabs (then its reduce can form S)
     coefs expansion_coefs() const;
     // predict through the expansion (expand.hip); false: not applicable, predict brute force
     bool expansion_predict(const T *alpha_dev, T alpha_m, T bias, const int64_t *zr_dev, const int32_t *zc_dev,

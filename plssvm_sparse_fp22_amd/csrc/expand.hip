@@ -472,7 +472,17 @@ __global__ __launch_bounds__(256) void exp_mscale_kernel(const T *__restrict__ m
 template <typename T>
 __global__ __launch_bounds__(256) void exp_mom_reduce_kernel(const T *__restrict__ partial, int64_t P, int64_t d, int kc,
                                                              int split, coefs cf, T *__restrict__ M,
+                                                             const T *__restrict__ spart, int sG, T *__restrict__ sout,
                                                              const cg_scalars<T> *__restrict__ status) {
+    if (spart != nullptr && blockIdx.x == gridDim.x - 1) {
+        // the extra last block: S = sum_j w_j from w's RED_BLOCKS partials, dot_final_kernel's sum (FIN_PLAIN, which
+        // also runs after convergence) — one launch fewer
+        __shared__ T red[8];
+        T r1, r2;
+        cgk::partials_final(spart, sG, red, r1, r2);
+        if (threadIdx.x == 0) sout[0] = r1, sout[1] = r2;
+        return;
+    }
     if (status != nullptr && status->converged) return;
     __shared__ T part[3][64];
     const int64_t ns = d * kc;
@@ -1883,26 +1893,34 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
 // reduced straight into the scaled Horner coefficients M (returns true), one panel: the pass wrote the raw
 // moments mom, scaled by expansion_mscale after the group's all-reduce (returns false)
 template <typename T>
-bool engine<T>::expansion_moment_pass(const T *w, const cg_scalars<T> *status) {
+bool engine<T>::expansion_moments_fused() const {
+    const auto &pl = csr.spmv_csc;
+    return pl.P > 1 && pl.nseg == d && pl.nblocks > 0;
+}
+
+// spart != null (fused passes only): the moment reduce also forms S = csr.ssc from w's partials (sG sets)
+template <typename T>
+bool engine<T>::expansion_moment_pass(const T *w, const cg_scalars<T> *status, const T *spart, int sG) {
     auto &ex = csr.ex;
     const auto &pl = csr.spmv_csc;
-    const bool fused = pl.P > 1 && pl.nseg == d && pl.nblocks > 0;
+    const bool fused = expansion_moments_fused();
     launch_panel_spmv<T>(pl, w + csr.csc_r0, csr.csc_r1 - csr.csc_r0, ex.mom.get(), status, stream, ex.KM, 1, !fused);
     if (fused) {
         const int split = pl.P >= 16 ? 1 : 0;
-        hipLaunchKernelGGL(exp_mom_reduce_kernel<T>, dim3((unsigned) ceil_div(d * ex.KM, split ? 64 : 256)), dim3(256), 0,
-                           stream, pl.partial.get(), pl.P, d, ex.KM, split, expansion_coefs(), ex.M.get(), status);
+        const unsigned nb = (unsigned) ceil_div(d * ex.KM, split ? 64 : 256) + (spart != nullptr ? 1u : 0u);
+        hipLaunchKernelGGL(exp_mom_reduce_kernel<T>, dim3(nb), dim3(256), 0, stream, pl.partial.get(), pl.P, d, ex.KM, split,
+                           expansion_coefs(), ex.M.get(), spart, sG, csr.ssc.get(), status);
         MI_LAUNCH_CHECK();
     }
     return fused;
 }
 
 template <typename T>
-void engine<T>::expansion_moments(const T *w, const cg_scalars<T> *status) {
+void engine<T>::expansion_moments(const T *w, const cg_scalars<T> *status, const T *spart, int sG) {
     auto &ex = csr.ex;
     if (d > 0) {  // column moments, then the coefficients (a real group: each rank's rows, then one
         // all-reduce of the d x K values — linear, so the scaled coefficients are all-reduced when fused)
-        const bool fused = expansion_moment_pass(w, status);
+        const bool fused = expansion_moment_pass(w, status, spart, sG);
         if (csr.csc_r1 - csr.csc_r0 < m) allreduce(fused ? ex.M.get() : ex.mom.get(), d * ex.KM);
         if (!fused) expansion_mscale(status);
     }
@@ -1993,8 +2011,10 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
         MI_HIP_CHECK(hipStreamWaitEvent(stream, cev[3], 0));  // the group's moments
         if (!fused) expansion_mscale(status);
     } else if (g16) {
-        launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
-        expansion_moments(w, status);
+        // S from w's partials: inside the moment reduce when the moment pass has one (one launch fewer)
+        const bool sfold = d > 0 && expansion_moments_fused();
+        if (!sfold) launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+        expansion_moments(w, status, sfold ? red.get() : nullptr, 1);
         expansion_dominant(w, status);
     } else {
         gather_input(w);
@@ -2003,8 +2023,9 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
                                ex.hbf16 ? ex.wv16.get() : nullptr, red.get(), status);  // S = sum_j w_j (+ bf16 w)
             MI_LAUNCH_CHECK();
         }
-        launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
-        expansion_moments(w, status);
+        const bool sfold = d > 0 && expansion_moments_fused();
+        if (!sfold) launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+        expansion_moments(w, status, sfold ? red.get() : nullptr, 1);
         expansion_dominant(w, status);
     }
     T kappa = 0;
@@ -2323,9 +2344,10 @@ bool engine<T>::expansion_predict(const T *alpha_dev, T alpha_m, T bias, const i
     template bool engine<T>::expansion_eligible();                                           \
     template void engine<T>::build_expansion(const int64_t *, int64_t);                      \
     template void engine<T>::expansion_dominant(const T *, const cg_scalars<T> *);           \
-    template void engine<T>::expansion_moments(const T *, const cg_scalars<T> *);            \
+    template void engine<T>::expansion_moments(const T *, const cg_scalars<T> *, const T *, int);            \
     template void engine<T>::expansion_mscale(const cg_scalars<T> *);                        \
-    template bool engine<T>::expansion_moment_pass(const T *, const cg_scalars<T> *);        \
+    template bool engine<T>::expansion_moment_pass(const T *, const cg_scalars<T> *, const T *, int);         \
+    template bool engine<T>::expansion_moments_fused() const;        \
     template coefs engine<T>::expansion_coefs() const;                                       \
     template void engine<T>::expansion_kp_raw(const T *, const cg_scalars<T> *, bool);      \
     template bool engine<T>::expansion_predict(const T *, T, T, const int64_t *, const int32_t *, const T *, int64_t, \
