@@ -803,11 +803,13 @@ __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__res
 #endif
 
 // one step of a segmented inclusive lane scan keyed by k (keys non-decreasing in lane order): v += the DPP
-// source lane's v when that lane holds the same key (lanes without a source keep v)
+// source lane's v when that lane holds the same key. A lane without a source (or in a masked DPP row) reads
+// value 0 and key 0 (bound_ctrl / old = 0: no initialising moves) — a false key match then adds +0, which
+// changes no sum
 template <int CTRL, int ROWS>
 __device__ __forceinline__ void seg_step(float &v, int k) {
-    const float vs = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xF, false));
-    const int ks = __builtin_amdgcn_update_dpp(-2, k, CTRL, ROWS, 0xF, false);
+    const float vs = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xF, true));
+    const int ks = __builtin_amdgcn_update_dpp(0, k, CTRL, ROWS, 0xF, true);
     if (ks == k) v += vs;
 }
 template <int CTRL, int ROWS>
@@ -933,11 +935,11 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
         int rl = have ? g.rl : -1;
         uint32_t hx = g.hb.x;
         if constexpr (RF) {
-            const bool fl = have && (hx & 0x4000u) != 0;
-            const unsigned long long bal = __ballot(fl);
+            const uint32_t fb = (hx >> 14) & 1u;  // the row-start flag as 0 / 1
+            const unsigned long long bal = __ballot(have && fb != 0u);
             const int below = (int) __builtin_amdgcn_mbcnt_hi((uint32_t) (bal >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t) bal, 0u));
-            rl = have ? carry + below + (fl ? 1 : 0) - 1 : -1;
+            rl = have ? carry + below + (int) fb - 1 : -1;
             carry += __popcll(bal);
             hx &= ~0x4000u;
         }
@@ -965,7 +967,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
         seg_step<0x118, 0xF>(sacc, rl);  // row_shr:8
         seg_step<0x142, 0xA>(sacc, rl);  // row_bcast:15 (rows 1, 3)
         seg_step<0x143, 0xC>(sacc, rl);  // row_bcast:31 (rows 2, 3)
-        const int rnext = __builtin_amdgcn_update_dpp(-2, rl, 0x130, 0xF, 0xF, false);  // wave_shl:1
+        const int rnext = __builtin_amdgcn_update_dpp(0, rl, 0x130, 0xF, 0xF, true);  // wave_shl:1 (lane 63: tested apart)
         if (rl >= 0 && (lane == 63 || rnext != rl)) racc[rl] += sacc;  // rows of this wave only
 #else
         // segmented suffix sums: rows are non-decreasing in lane order
