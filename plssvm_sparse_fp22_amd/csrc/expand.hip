@@ -801,6 +801,9 @@ __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__res
 #ifndef EXP_NH
 #define EXP_NH 2  // remainder stream: groups of 64 chunks per lane step (bytes in flight per wave)
 #endif
+#ifndef EXP_DOT2
+#define EXP_DOT2 1  // bfloat16 remainder: a chunk's 4 products as two v_dot2c_f32_bf16 (the stream is VALU-bound)
+#endif
 
 // one step of a segmented inclusive lane scan keyed by k (keys non-decreasing in lane order): v += the DPP
 // source lane's v when that lane holds the same key. A lane without a source (or in a masked DPP row) reads
@@ -950,7 +953,21 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             h2 = (T) __uint_as_float(g.hb.y << 16), h3 = (T) __uint_as_float(g.hb.y & 0xFFFF0000u);
         }
         T acc = T(0);
-        if (have) {
+        if constexpr (HB && EXP_DOT2 && sizeof(T) == 4) {
+            // bfloat16 H and w: the pairs' products (exact in fp32) summed by two bf16 dot instructions, H and w
+            // packed as they are stored (the window holds w's bfloat16 bits)
+            (void) h0, (void) h1, (void) h2, (void) h3;
+            if (have) {
+                const uint32_t w01 = (uint32_t) wl[jj.x & 0xFFFFu] | ((uint32_t) wl[jj.x >> 16] << 16);
+                const uint32_t w23 = (uint32_t) wl[jj.y & 0xFFFFu] | ((uint32_t) wl[jj.y >> 16] << 16);
+                // VOP3P form in inline assembly: the compiler's v_dot2c lowering of two chained
+                // __builtin_amdgcn_fdot2_f32_bf16 calls read the same H register twice here (ROCm 7.2 clang);
+                // the s_nop covers the DPP read of acc that follows (2 wait states after a VALU write)
+                asm("v_dot2_f32_bf16 %0, %1, %2, 0\n\tv_dot2_f32_bf16 %0, %3, %4, %0\n\ts_nop 1"
+                    : "=&v"(acc)
+                    : "v"(hx), "v"(w01), "v"(g.hb.y), "v"(w23));
+            }
+        } else if (have) {
             acc = h0 * wat(jj.x & 0xFFFFu);
             acc = fma(h1, wat(jj.x >> 16), acc);
             acc = fma(h2, wat(jj.y & 0xFFFFu), acc);
