@@ -266,21 +266,30 @@ def main():
         pm.CSVM = _csvm
 
     cache = {}
-    default_run = (args.config == "dense_rbf_100k" and not (args.kernel or args.dtype or args.points or
-                                                            args.features or sim) and world == 1)
+    default_cfg = args.config == "dense_rbf_100k" and not (args.kernel or args.dtype or args.points or args.features
+                                                          or sim)
+    default_run = default_cfg and world == 1
     rec = run_config(args.config, args, rank, world, dist, uid, args.steps, args.warmup, not args.no_cpu,
                      args.cpu_seconds, args.kp_reps, sim=sim, kernel=args.kernel, dtype=args.dtype,
                      points=args.points, features=args.features, data_cache=cache,
                      solve=(args.solve or default_run) and not args.no_solve and world == 1)
     extra = None
-    if default_run and not args.no_extra:
-        # north_star's sparse target measured under the same clock: configs[2] with RBF (the >= 70 % HBM
-        # row), configs[2] itself (sparse linear, same seeded matrix) and configs[4] (2M x 100k FP22 RBF,
-        # on one GPU: the kernel expansion's memory is O(nnz + multi-feature pairs))
+    if default_cfg and not args.no_extra:
+        # the other BASELINE rows measured under the same clock. One GPU: configs[2] with RBF (the >= 70 % HBM
+        # row), configs[2] itself (sparse linear, same seeded matrix), configs[4] (2M x 100k FP22 RBF, on one
+        # GPU: the kernel expansion's memory is O(nnz + multi-feature pairs)) and configs[3] (dense linear
+        # 500k x 1024 fp32 on the MFMA tiles, ~1.8 s per K·p). N > 1: the two 8-GPU rows of BASELINE
+        # (configs[3], configs[4]) with the same max-over-ranks timing as the headline, so a 1/2/4/8 scaling
+        # run yields their curves too.
         extra = {}
-        for name, steps in (("csr_rbf_1m", 50), ("csr_linear_1m", 200), ("fp22_rbf_2m", 30)):
-            extra[name] = run_config(name, args, rank, world, dist, uid, steps, 2, not args.no_cpu,
-                                     args.cpu_seconds * 0.6, args.kp_reps, data_cache=cache, solve=True)
+        if world == 1:
+            rows = (("csr_rbf_1m", 50, 2), ("csr_linear_1m", 200, 2), ("fp22_rbf_2m", 30, 2), ("dense_linear_500k", 2, 1))
+        else:
+            rows = (("fp22_rbf_2m", 30, 2), ("dense_linear_500k", 3, 1))
+        for name, steps, warm in rows:
+            extra[name] = run_config(name, args, rank, world, dist, uid, steps, warm, not args.no_cpu,
+                                     args.cpu_seconds * 0.6, args.kp_reps if steps >= 10 else 1, data_cache=cache,
+                                     solve=world == 1)
     if rank == 0:
         out = {
             "metric": METRIC,

@@ -23,6 +23,14 @@ struct mi_error : std::runtime_error {
     mi_error(int c, const std::string &msg) : std::runtime_error(msg), code(c) {}
 };
 
+// the PLSSVM_MI_ERR_* code of any exception a setup step may raise (mi_error: its code; host or device
+// allocation: ERR_OOM; anything else, e.g. std::length_error from a host table: ERR_ARG — the C ABI's mapping)
+inline int exception_code(const std::exception &e) {
+    if (const auto *m = dynamic_cast<const mi_error *>(&e)) return m->code;
+    if (dynamic_cast<const std::bad_alloc *>(&e) != nullptr) return -4;
+    return -1;
+}
+
 #define MI_HIP_CHECK(expr)                                                                                        \
     do {                                                                                                          \
         hipError_t e_ = (expr);                                                                                   \

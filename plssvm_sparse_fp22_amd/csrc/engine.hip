@@ -285,6 +285,27 @@ std::vector<double> engine<T>::group_gather(const std::vector<double> &v) {
 }
 
 template <typename T>
+std::vector<double> engine<T>::group_step(int code, const std::string &why, const std::vector<double> &v) {
+    std::vector<double> mine{ (double) code };
+    mine.insert(mine.end(), v.begin(), v.end());
+    const auto g = group_gather(mine);
+    const size_t K1 = mine.size();
+    const int nr = (int) (g.size() / K1);
+    int worst = 0;  // the first rank's failure, a non-OOM one over ERR_OOM (OOM alone: the caller's fallback)
+    for (int r = 0; r < nr; ++r) {
+        const int c = (int) g[(size_t) r * K1];
+        if (c != 0 && (worst == 0 || worst == -4)) worst = c;
+    }
+    if (worst != 0)
+        throw mi_error(worst, code != 0 ? why : std::string("sparse setup failed on another rank of the group"));
+    std::vector<double> out;
+    out.reserve((size_t) nr * v.size());
+    for (int r = 0; r < nr; ++r)
+        out.insert(out.end(), g.begin() + (std::ptrdiff_t) ((size_t) r * K1 + 1), g.begin() + (std::ptrdiff_t) ((size_t) (r + 1) * K1));
+    return out;
+}
+
+template <typename T>
 void engine<T>::setup_dense(const T *X, int64_t n_, int64_t d_) {
     if (X == nullptr || n_ < 1 || d_ < 1) throw mi_error(-1, "Data set is empty!");
     MI_HIP_CHECK(hipSetDevice(device));

@@ -173,7 +173,9 @@ struct engine : engine_base {
     void otf_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);
     bool sparse_stored() const { return sparse && !csr.dense_on; } // K·p through the CSR structures
     bool expansion_eligible();                                    // expand.hip: K, coefficients; true if usable
-    void build_expansion(const int64_t *cpos, int64_t max_inc);   // multi-overlap remainder H, diagonal
+    // multi-overlap remainder H, diagonal; pre: a failure of the caller's preceding step (the SELL plans), which
+    // still joins the group's agreement inside and is rethrown there
+    void build_expansion(const int64_t *cpos, int64_t max_inc, std::exception_ptr pre = nullptr);
     void expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);
     void expansion_dominant(const T *p, const cg_scalars<T> *status);  // the remainder stream
     // column moments (SELL CSC pass); spart: the moment reduce also forms S from w's partials (sG sets)
@@ -204,6 +206,10 @@ struct engine : engine_base {
     void allreduce(T *buf, int64_t count);
     // setup decisions of a real group: every rank's K values, rank-major (world == 1: the local ones)
     std::vector<double> group_gather(const std::vector<double> &v);
+    // one step of a group setup: every rank reports its failure (0 = none, else a PLSSVM_MI_ERR_* code) with
+    // K values; a failure anywhere throws the same error on every rank (no rank is left waiting in a later
+    // exchange), else every rank gets the world x K values, rank-major
+    std::vector<double> group_step(int code, const std::string &why, const std::vector<double> &v);
     bool in_group() const { return world > 1 && sim_world == 0 && (comm != nullptr || xchg != nullptr); }
     void allgather_rows(T *buf);
     int64_t device_bytes() const;

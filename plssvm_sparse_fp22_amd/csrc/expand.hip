@@ -232,6 +232,7 @@ constexpr int RJ_BMW = 32768;  // bitmap words: 1 048 576 partner rows per pass 
 constexpr int RJ_LCAP = 2048;  // repeat sightings held per pass (more: the pass range is halved)
 constexpr int RJ_ECAP = 256;   // entries of row i held in LDS (longer rows: the sort join)
 constexpr int RJ_WPT = RJ_BMW / RJ_NT;
+constexpr int RJ_PMAX = 256;   // passes per row at most (more: the rank takes the sort join; PLSSVM_MI_EXP_RJ_PMAX: tests)
 
 // Rows [r0, r0 + gridDim.x) of the rank, one workgroup per row i: its partners j != i sharing two or more
 // features, ascending, in both triangles. Per pass over a range of partner rows, the column entries of
@@ -240,12 +241,16 @@ constexpr int RJ_WPT = RJ_BMW / RJ_NT;
 // (a block scan of per-thread popcounts). Count mode (sj == nullptr): cnt[r] = #partners. Write mode:
 // partner k of row r at sj[off8[r] + k], pads up to off8[r + 1] marked -1 (exp_rowjoin_h_kernel then
 // forms H). Both modes take the same passes (the halving decisions depend on the data only): deterministic.
+// A halved span grows back (doubles) after every completed range, so one dense cluster of partners does not
+// cut the rest of the row into small passes; a row needing more than RJ_PMAX passes (every pass rescans its
+// incidences) sets *ovf in count mode and the host builds the rank's rows by the sort join instead.
 __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__restrict__ rowptr,
                                                             const int32_t *__restrict__ col,
                                                             const int64_t *__restrict__ colptr,
                                                             const int32_t *__restrict__ crow, int64_t m, int64_t r0,
                                                             int64_t *__restrict__ cnt, const int64_t *__restrict__ off8,
-                                                            int32_t *__restrict__ sj) {
+                                                            int32_t *__restrict__ sj, unsigned int *__restrict__ ovf,
+                                                            int pmax) {
     __shared__ uint32_t bm[RJ_BMW];
     __shared__ int32_t rep[RJ_LCAP];
     __shared__ int32_t zcol[RJ_ECAP];
@@ -275,8 +280,17 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
     const int32_t inc = zoff[ne];
     const bool wr = sj != nullptr;
     int64_t written = 0;
-    int64_t span = (int64_t) RJ_BMW * 32;
+    constexpr int64_t SPAN_MAX = (int64_t) RJ_BMW * 32;
+    int64_t span = SPAN_MAX;
+    int passes = 0;
     for (int64_t R0 = 0; R0 < m;) {
+        if (++passes > pmax) {  // uniform
+            if (!wr && tid == 0) {
+                cnt[r] = 0;
+                atomicOr(ovf, 1u);
+            }
+            return;
+        }
         const int64_t R1 = min(m, R0 + span);
         for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
         if (tid == 0) nrep_s = 0;
@@ -342,6 +356,7 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
         written += U;
         __syncthreads();  // bm / rep are reused by the next pass
         R0 = R1;
+        span = min(span * 2, SPAN_MAX);
     }
     if (!wr) {
         if (tid == 0) cnt[r] = written;
@@ -802,7 +817,15 @@ __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__res
 #define EXP_NH 2  // remainder stream: groups of 64 chunks per lane step (bytes in flight per wave)
 #endif
 #ifndef EXP_DOT2
-#define EXP_DOT2 1  // bfloat16 remainder: a chunk's 4 products as two v_dot2c_f32_bf16 (the stream is VALU-bound)
+// bfloat16 remainder: a chunk's 4 products as two v_dot2_f32_bf16 (the stream is VALU-bound). The instruction
+// pair is inline assembly whose hazard padding (the s_nop in exp_hcell_kernel) was verified on the GPU with the
+// ROCm 7.2 compiler (clang 22, tests/test_gpu_sparse.py::test_expansion_dot2_equals_fma_path); any other
+// compiler builds the FMA chain until the sequence is re-verified there.
+#if HIP_VERSION_MAJOR == 7 && HIP_VERSION_MINOR == 2 && __clang_major__ == 22
+#define EXP_DOT2 1
+#else
+#define EXP_DOT2 0
+#endif
 #endif
 
 // one step of a segmented inclusive lane scan keyed by k (keys non-decreasing in lane order): v += the DPP
@@ -832,7 +855,8 @@ __device__ __forceinline__ void seg_step(double &v, int k) {
 // software-pipelined one step ahead, also across window boundaries), gathers w_j from LDS and adds its
 // rows' partial sums (segmented shuffle reduction) into an LDS row accumulator only it writes.
 // Fixed order, no atomics: bitwise reproducible.
-template <typename T, int RBB, bool HB, bool RF = false>
+// D2 (bfloat16 H only): the dot instructions (EXP_DOT2) or the FMA chain (PLSSVM_MI_EXP_DOT2=0: tests, A/B)
+template <typename T, int RBB, bool HB, bool RF = false, bool D2 = true>
 __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *__restrict__ woff,
                                                                  const uint16_t *__restrict__ hrow,
                                                                  const uint16_t *__restrict__ hjl,
@@ -953,7 +977,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             h2 = (T) __uint_as_float(g.hb.y << 16), h3 = (T) __uint_as_float(g.hb.y & 0xFFFF0000u);
         }
         T acc = T(0);
-        if constexpr (HB && EXP_DOT2 && sizeof(T) == 4) {
+        if constexpr (HB && D2 && EXP_DOT2 && sizeof(T) == 4) {
             // bfloat16 H and w: the pairs' products (exact in fp32) summed by two bf16 dot instructions, H and w
             // packed as they are stored (the window holds w's bfloat16 bits)
             (void) h0, (void) h1, (void) h2, (void) h3;
@@ -1338,10 +1362,24 @@ bool engine<T>::expansion_eligible() {
 // write pass with H from a merge of the two rows), or by the column-join sort (every incidence (i, j < i,
 // a, phi(a)) generated, radix-sorted and reduced by key; PLSSVM_MI_EXP_JOIN=sort); H_ii; the moment buffers.
 template <typename T>
-void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
+void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::exception_ptr pre) {
     auto &ex = csr.ex;
     phase_timer pt;
     const phi_fn phi = make_phi<T>(kernel, degree, gamma, coef0);
+    const int64_t R = r1 - r0;
+    dev_buf<int64_t> off8;
+    dev_buf<int32_t> sj;
+    dev_buf<T> sv;
+    int64_t nslot8 = 0;
+    ex.hratio = -1.0;
+    {
+        const char *e = std::getenv("PLSSVM_MI_EXP_DOT2");
+        ex.dot2 = !(e != nullptr && std::strcmp(e, "0") == 0);
+    }
+    // phase 1 (the symmetric rows) may fail on one rank only (memory, a dense row): in a real group every rank
+    // still reaches the agreement after it, which raises the same error everywhere
+    std::exception_ptr fail1 = pre;
+    if (!fail1) try {
     ex.M.alloc(std::max<int64_t>(d, 1) * ex.KM, stream);
     ex.mom.alloc(std::max<int64_t>(d, 1) * ex.KM, stream);
     csr.ssc.alloc(2, stream);  // device scalar S = sum_j w_j
@@ -1355,11 +1393,6 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
     MI_LAUNCH_CHECK();
 
     // ---- the remainder's symmetric rows [r0, r1), padded to 8 slots: off8[R + 1], (sj, sv)[nslot8] ----
-    const int64_t R = r1 - r0;
-    dev_buf<int64_t> off8;
-    dev_buf<int32_t> sj;
-    dev_buf<T> sv;
-    int64_t nslot8 = 0;
     // the column-join sort (PLSSVM_MI_EXP_JOIN=sort, and rows longer than the row join's LDS copy)
     auto sort_join = [&]() {
         // ---- incidences per row (host) -> row sub-blocks of at most CAP incidences ----
@@ -1618,17 +1651,26 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         for (int64_t r = 0; r < R && row_join; ++r) row_join = rp[(size_t) r + 1] - rp[(size_t) r] <= RJ_ECAP;
         if (row_join && csr.nnz >= (int64_t) INT32_MAX) row_join = false;  // a row's incidences <= nnz
     }
+    dev_buf<int64_t> cnt, cnt8;
+    dev_buf<unsigned long long> lnz;
+    unsigned int ovf_h = 0u;
+    const int rj_pmax = [] {
+        const char *e = std::getenv("PLSSVM_MI_EXP_RJ_PMAX");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 1 ? v : RJ_PMAX;
+    }();
     if (row_join) {
         off8.alloc(R + 1, stream);
-        dev_buf<int64_t> cnt, cnt8;
-        dev_buf<unsigned long long> lnz;
+        {
         cnt.alloc(std::max<int64_t>(R, 1), stream);
         cnt8.alloc(R + 1, stream);
         lnz.alloc(2, stream);  // [0] lower pairs with H != 0, [1] max |H| / kernel value (double bits)
+        dev_buf<unsigned int> ovf;
+        ovf.alloc(1, stream);
         if (R > 0) {
             hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
                                csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(),
-                               (const int64_t *) nullptr, (int32_t *) nullptr);
+                               (const int64_t *) nullptr, (int32_t *) nullptr, ovf.get(), rj_pmax);
             MI_LAUNCH_CHECK();
             hipLaunchKernelGGL(exp_pad8_cnt_kernel, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream, cnt.get(),
                                R, cnt8.get());
@@ -1641,14 +1683,23 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
             t.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
             MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, cnt8.get(), off8.get(), (int) (R + 1), stream));
             MI_HIP_CHECK(hipMemcpyAsync(&nslot8, off8.get() + R, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipMemcpyAsync(&ovf_h, ovf.get(), sizeof(ovf_h), hipMemcpyDeviceToHost, stream));
             MI_HIP_CHECK(hipStreamSynchronize(stream));
         }
         pt.mark("expansion: row join (count)");
+        if (ovf_h != 0u) {  // a row whose partner clusters need more than RJ_PMAX passes: the sort join
+            off8.reset();
+            row_join = false;
+        }
+        }
+    }
+    if (row_join) {
         sj.alloc(std::max<int64_t>(nslot8, 8), stream, false);
         sv.alloc(std::max<int64_t>(nslot8, 8), stream, false);
         if (R > 0) {
             hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
-                               csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(), off8.get(), sj.get());
+                               csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(), off8.get(), sj.get(),
+                               (unsigned int *) nullptr, rj_pmax);
             MI_LAUNCH_CHECK();
             double kbase = 1.0;  // rbf: 1 + E(s); poly: kappa + c(s)
             if (kernel == 1) {
@@ -1672,6 +1723,34 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         sort_join();
     }
     pt.mark("expansion: symmetric rows");
+    } catch (...) {
+        fail1 = std::current_exception();
+    }
+    // H storage (float contexts): bfloat16 when every stored |H_ij| is at most 2^-16 of its pair's kernel value
+    // (the row join's hratio; see "H storage" below). A sharded group gathers bfloat16 w or real w by this flag
+    // (expansion_kp_raw), so a real group takes it once: the AND over the ranks, after every rank's join.
+    const char *hf = std::getenv("PLSSVM_MI_EXP_HFMT");
+    bool hb_ok = !fail1 && sizeof(T) == 4 && ex.hratio >= 0.0 && ex.hratio <= std::ldexp(1.0, -16) &&
+                 !(hf != nullptr && std::strcmp(hf, "full") == 0);
+    if (in_group()) {
+        int code = 0;
+        std::string why;
+        if (fail1) {
+            try {
+                std::rethrow_exception(fail1);
+            } catch (const std::exception &e) {
+                code = exception_code(e);
+                why = e.what();
+            } catch (...) {
+                code = -1;
+                why = "unknown exception in the expansion setup";
+            }
+        }
+        const auto g = group_step(code, why, { hb_ok ? 1.0 : 0.0 });  // throws on every rank if any failed
+        for (double v : g) hb_ok = hb_ok && v != 0.0;
+    } else if (fail1) {
+        std::rethrow_exception(fail1);
+    }
 
     // ---- cells: blocks of RB rows x windows of CW partners, rows padded to 4 slots per cell ----
     // geometry: rows per block RB = the rank's rows spread evenly over the CUs (a multiple of 16: one
@@ -1731,8 +1810,11 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
         // under 5 % of the entries; = 2 regardless). Off by default: 11-20 % fewer bytes (config 3-RBF 7.87 ->
         // 6.99 GB, config 5 8.89 -> 7.10 GB) but 2.5x the VALU per 256-entry step (161 vs 64: row numbering,
         // multi-row lanes, the segmented scan), measured 1.52 vs 1.42 ms (3-RBF) and 1.74 vs 1.67 ms (5)
+        // In a real group only the forced option (= 2, the same on every rank): the run layout keeps real H, so a
+        // per-rank choice would split the group's H storage again.
         const char *re = std::getenv("PLSSVM_MI_EXP_RUNS");
-        const int runs_opt = re != nullptr ? std::atoi(re) : 0;
+        int runs_opt = re != nullptr ? std::atoi(re) : 0;
+        if (in_group() && runs_opt != 2) runs_opt = 0;
         ex.runs = false;
         if (runs_opt != 0 && R > 0) {
             ex.CW = exp_cw_run_host(ex.RBB, (int) sizeof(T));
@@ -1770,9 +1852,8 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/) {
             // relative error <= 2^-9 each, so each pair's term moves by at most ~2^-8 |H_ij w_j| <= 2^-24 of
             // the pair's k_ij w_j — the float rounding of that term itself. PLSSVM_MI_EXP_HFMT=full keeps the
             // real type. The bfloat16 window holds twice the partners (fewer windows, fewer padded cells).
-            const char *hf = std::getenv("PLSSVM_MI_EXP_HFMT");
-            ex.hbf16 = sizeof(T) == 4 && ex.hratio >= 0.0 && ex.hratio <= std::ldexp(1.0, -16) &&
-                       !(hf != nullptr && std::strcmp(hf, "full") == 0);
+            // hb_ok: agreed by the whole group (above).
+            ex.hbf16 = hb_ok;
             ex.CW = ex.hbf16 ? exp_cw16_host(ex.RBB) : exp_cw_host(ex.RBB, (int) sizeof(T));
             ex.nW = ceil_div(std::max<int64_t>(m, 1), (int64_t) ex.CW);
             const int64_t CW = ex.CW, ncnt = ex.nblk * RB * ex.nW;
@@ -1884,21 +1965,24 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
                 default: launch_run(exp_hrun_kernel<T, 16384>);
             }
         } else {
-            auto pick = [&](auto hb, auto rf) {
-                constexpr bool HB = decltype(hb)::value, RF = decltype(rf)::value;
+            auto pick = [&](auto hb, auto rf, auto d2) {
+                constexpr bool HB = decltype(hb)::value, RF = decltype(rf)::value, D2 = decltype(d2)::value;
                 switch (ex.RBB) {
-                    case 4096: launch(exp_hcell_kernel<T, 4096, HB, RF>); break;
-                    case 8192: launch(exp_hcell_kernel<T, 8192, HB, RF>); break;
-                    case 32768: launch(exp_hcell_kernel<T, 32768, HB, RF>); break;
-                    default: launch(exp_hcell_kernel<T, 16384, HB, RF>);
+                    case 4096: launch(exp_hcell_kernel<T, 4096, HB, RF, D2>); break;
+                    case 8192: launch(exp_hcell_kernel<T, 8192, HB, RF, D2>); break;
+                    case 32768: launch(exp_hcell_kernel<T, 32768, HB, RF, D2>); break;
+                    default: launch(exp_hcell_kernel<T, 16384, HB, RF, D2>);
                 }
             };
+            const bool dot2 = ex.dot2;
             if constexpr (sizeof(T) == 4) {
-                if (ex.hbf16 && ex.rflags) pick(std::true_type{}, std::true_type{});
-                else if (ex.hbf16) pick(std::true_type{}, std::false_type{});
-                else pick(std::false_type{}, std::false_type{});
+                if (ex.hbf16 && ex.rflags && dot2) pick(std::true_type{}, std::true_type{}, std::true_type{});
+                else if (ex.hbf16 && ex.rflags) pick(std::true_type{}, std::true_type{}, std::false_type{});
+                else if (ex.hbf16 && dot2) pick(std::true_type{}, std::false_type{}, std::true_type{});
+                else if (ex.hbf16) pick(std::true_type{}, std::false_type{}, std::false_type{});
+                else pick(std::false_type{}, std::false_type{}, std::true_type{});
             } else {
-                pick(std::false_type{}, std::false_type{});
+                pick(std::false_type{}, std::false_type{}, std::true_type{});
             }
         }
         MI_LAUNCH_CHECK();  // G > 1: the row sums stay in hslab, summed in g order by exp_combine_kernel
@@ -2361,7 +2445,7 @@ bool engine<T>::expansion_predict(const T *alpha_dev, T alpha_m, T bias, const i
 
 #define INST(T)                                                                              \
     template bool engine<T>::expansion_eligible();                                           \
-    template void engine<T>::build_expansion(const int64_t *, int64_t);                      \
+    template void engine<T>::build_expansion(const int64_t *, int64_t, std::exception_ptr);                      \
     template void engine<T>::expansion_dominant(const T *, const cg_scalars<T> *);           \
     template void engine<T>::expansion_moments(const T *, const cg_scalars<T> *, const T *, int);            \
     template void engine<T>::expansion_mscale(const cg_scalars<T> *);                        \

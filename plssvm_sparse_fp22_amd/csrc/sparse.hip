@@ -828,25 +828,29 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                     const bool local = (world > 1 && sim_world == 0) || (sim_world > 0 && shard);
                     csr.csc_r0 = local ? r0 : 0;
                     csr.csc_r1 = local ? r1 : m;
-                    build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0],
-                                       f22, csc_gen(csr.csc_r0, csr.csc_r1), blocks, stream, 0, 1, csr.ex.KM);
-                    build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks, stream,
-                                       0, csr.ex.KM, 1);
+                    std::exception_ptr plan_fail;  // joins build_expansion's group agreement, rethrown there
+                    try {
+                        build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0],
+                                           f22, csc_gen(csr.csc_r0, csr.csc_r1), blocks, stream, 0, 1, csr.ex.KM);
+                        build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks,
+                                           stream, 0, csr.ex.KM, 1);
+                    } catch (...) {
+                        plan_fail = std::current_exception();
+                    }
                     pt.mark("setup_csr: SELL plans");
-                    build_expansion(cpos_d.get(), max_inc);
+                    build_expansion(cpos_d.get(), max_inc, plan_fail);
                     pt.mark("setup_csr: expansion");
                 } else {
                     build_gram_blocks(cpos_d.get(), max_inc);
                 }
                 stored = true;
-            } catch (const mi_error &e) {
-                if (!in_group() && (e.code != -4 || forced)) throw;
-                fail = e.code;
-                why = e.what();
-            } catch (const std::bad_alloc &) {
-                if (!in_group() && forced) throw;
-                fail = -4;
-                why = "host allocation failed";
+            } catch (const std::exception &e) {
+                // any failure (also a host table's bad_alloc or length_error, or one rethrown from host_parallel):
+                // in a group every rank must still reach agree() below, with a code
+                const int c = exception_code(e);
+                if (!in_group() && (c != -4 || forced)) throw;
+                fail = c;
+                why = c == -4 && dynamic_cast<const mi_error *>(&e) == nullptr ? "host allocation failed" : e.what();
             }
             fail = agree(fail, why);
             if (fail != 0 && forced) throw mi_error(fail, why.empty() ? "the forced sparse structure did not fit on another rank" : why);
@@ -883,9 +887,10 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                 std::string why;
                 try {
                     setup_otf(fact_ok ? 1 : 0);
-                } catch (const mi_error &e) {  // its tables did not fit either: the densified path decides
-                    if (!in_group() && (e.code != -4 || sparse_algo == 4)) throw;
-                    fail = e.code;
+                } catch (const std::exception &e) {  // its tables did not fit either: the densified path decides
+                    const int c = exception_code(e);
+                    if (!in_group() && (c != -4 || sparse_algo == 4)) throw;
+                    fail = c;
                     why = e.what();
                 }
                 fail = agree(fail, why);
@@ -902,9 +907,9 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                 std::string why;
                 try {
                     setup_sparse_dense();
-                } catch (const mi_error &e) {
+                } catch (const std::exception &e) {
                     if (!in_group()) throw;
-                    fail = e.code;
+                    fail = exception_code(e);
                     why = e.what();
                 }
                 fail = agree(fail, why);

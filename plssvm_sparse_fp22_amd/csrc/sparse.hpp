@@ -86,6 +86,7 @@ struct exp_data {
     dev_buf<uint16_t> hv16;           // [slots] H_ij as bfloat16 (hbf16: see expand.hip, "H storage")
     dev_buf<uint16_t> wv16;           // [m] the stream's partner weights w_j as bfloat16 (hbf16)
     bool hbf16 = false;
+    bool dot2 = true;                 // bfloat16 H: the dot-instruction kernel (PLSSVM_MI_EXP_DOT2=0: the FMA chain)
     bool rflags = false;              // hbf16 chunks without hrow: bit 14 of a chunk's first H marks a row's first chunk
     double hratio = -1.0;             // row join: max |H_ij| / |kernel value of the pair| (< 0: unknown)
     dev_buf<uint16_t> hrow;           // [nchunks] block-local row of each 4-slot chunk

@@ -18,6 +18,7 @@ CASES = {
     "sparse_rbf_onthefly": ("csr", "rbf", "auto", np.float64, 40),
     "sparse_poly_onthefly": ("csr", "polynomial", "auto", np.float64, 40),
     "sparse_rbf_budget_split": ("csr", "rbf", "auto", np.float64, 40),
+    "sparse_f32_rbf_hfmt_split": ("csr", "rbf", "auto", np.float32, 10),
 }
 # sparse poly / rbf K·p algorithm per case (default: auto)
 ALGO = {"sparse_rbf_onthefly": "onthefly", "sparse_poly_onthefly": "onthefly"}
@@ -25,6 +26,11 @@ ALGO = {"sparse_rbf_onthefly": "onthefly", "sparse_poly_onthefly": "onthefly"}
 # budget — rank 0 would store the kernel expansion, rank 1 cannot — so only a group-wide decision keeps
 # both on one path
 BUDGET = {"sparse_rbf_budget_split": {1: "1"}}
+# rows given LONG_ROW entries (beyond the row join's 256-entry LDS copy): the rank holding them builds its
+# remainder by the column-join sort, which measures no bfloat16 bound, while the other rank's rows pass it —
+# only a group-wide H storage keeps the sharded K·p's collectives identical on both ranks
+LONG_ROWS = {"sparse_f32_rbf_hfmt_split": [5000]}
+LONG_ROW = 300
 # cases whose K·p stores no pairs (on the fly / densified)
 UNSTORED = set(ALGO) | set(BUDGET)
 
@@ -35,7 +41,23 @@ def case_data(name):
         X, y = datagen.blobs(3000, 64, seed=3, cluster_std=4.0, dtype=dtype)
         return dict(X=X), y, 64
     csr, y = datagen.sparse_csr(6500, 5000, 20, seed=2, dtype=dtype)
+    for i in LONG_ROWS.get(name, []):
+        csr = _long_row(csr, i, LONG_ROW)
     return dict(csr=csr), y, csr[4]
+
+
+def _long_row(csr, i, k):
+    """csr with row i replaced by k seeded entries (ascending distinct features, values in the set's range)."""
+    rowptr, col, val, n, d = csr
+    rng = np.random.default_rng(1000 + i)
+    c = np.sort(rng.choice(d, size=k, replace=False)).astype(col.dtype)
+    v = rng.uniform(0.1, 1.0, k).astype(val.dtype)
+    a, b = int(rowptr[i]), int(rowptr[i + 1])
+    col2 = np.concatenate([col[:a], c, col[b:]])
+    val2 = np.concatenate([val[:a], v, val[b:]])
+    rp = rowptr.copy()
+    rp[i + 1:] += k - (b - a)
+    return rp, col2, val2, n, d
 
 
 def make_case(name):

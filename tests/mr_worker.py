@@ -47,7 +47,8 @@ def main():
     np.savez(os.path.join(out, f"rank{rank}.npz"), q=q, kp_minus=kp_minus, kp_plus=kp_plus, kpart=kpart,
              alpha=svm.alpha, bias=np.float64(svm.bias), trace=np.asarray(svm.trace), iters=svm.iters,
              QA=np.float64(svm.QA_cost), tiles_local=info["tiles_local"], tiles_total=info["tiles_total"],
-             pairs=info["pairs"], world=info["world_size"], sparse_algo=info["sparse_algo"])
+             pairs=info["pairs"], world=info["world_size"], sparse_algo=info["sparse_algo"],
+             exp_hbytes=info["exp_hbytes"])
     svm.close()
     dist.barrier()
     dist.destroy_process_group()

@@ -1,0 +1,154 @@
+"""Multi-iteration CG residual curves of the sparse K·p paths against the oracle (VERDICT r3 item 1;
+north_star: "CG residual curve matching OpenMP to 1e-6"), across the explicit-residual iteration.
+
+Cases (tests/cg_trace_cases.py): the factored linear SELL path (fp64, fp32), the kernel expansion with real H
+(fp64 rbf, poly; fp32) and with bfloat16 H in the flagged chunk layout (fp32 and FP22 input: the layout of the
+3-RBF / config-5 bench lines, info exp_hbytes == 2, exp_layout == 2), the on-the-fly and densified paths; a
+1200 x 300 CSR set, C = 10, imax = 60, eps at or below every CG's rounding floor, so the runs cross
+run % 50 == 49 (r = b - Q~x explicitly, OpenMP/csvm.cpp:119-132). The oracle references are committed
+fixtures (tests/golden/cg_traces/, tests/golden/make_cg_trace_vectors.py): the oracle's learn() on 1 and
+8 threads (the reference's own run-to-run spread) and the CG in extended precision.
+
+The golden tests' method (test_gpu_golden.py), over the WHOLE trace:
+  * accurate prefix: where the oracle's trace is within R of extended precision (R = 1e-6 fp64, 1e-3 fp32)
+    the HIP trace is within R + 10 x (oracle 1-vs-8-thread spread) of it, and the HIP trace stays accurate
+    at least as long (minus one iteration);
+  * beyond it, every entry within R + 100 x the running 1-vs-8-thread spread (the reference's own
+    sensitivity to a reordered K·p: tight where the recurrence is stable, vacuous where it is not);
+  * the same iteration count (+-2) and the same solution: fp64 the explicit residual of the HIP alphas at most
+    10 x the oracle's; fp32 the alphas against the fp64 oracle within max(2e-2, 2 x the fp32 oracle's distance);
+  * fp32: the trace while the residual is above fp32's rounding floor (delta / delta0 >= 1e-6) against the
+    fp64 oracle within max(1e-3, 2 x the fp32 oracle's own distance).
+And the reset itself, from the HIP path's own iterate: after cg_step(50) (one graph block) the recorded delta_50
+is |b - Q~ x_50|^2 of the HIP x_50, evaluated in extended precision, within the rounding bound
+4 sqrt(m) u || M |x_50| || (M: the magnitudes of Q~'s terms); fp32: also within 30x of the fp32 oracle's
+delta_50 (both sit on fp32's floor after the reset, far above the recursive residual's 1e-32 delta_0).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cg_trace_cases as cc
+import plssvm_sparse_fp22_amd as pm
+
+pytestmark = pytest.mark.gpu
+
+MANIFEST = json.load(open(os.path.join(cc.VECTORS, "manifest.json")))
+
+
+def make_svm(s, name, monkeypatch):
+    kernel, dtype, _, _, fp22, algo, env, _ = cc.CASES[name]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    p = pm.Parameter(kernel, degree=3, gamma=float(s["gamma"]), coef0=float(s["coef0"]), cost=cc.COST,
+                     epsilon=s["eps"], real_type=dtype)
+    rowptr, col, val, n, d = s["csr"]
+    if fp22:
+        p.csr = (rowptr, col, s["fp22"], n, d)
+        p.val_fmt = pm._abi.VAL_FP22
+    else:
+        p.csr = s["csr"]
+    p.labels = s["y"]
+    return pm.CSVM(p, sparse_algo=algo)
+
+
+def stable_prefix(t, ref, R):
+    n = min(len(t), len(ref))
+    bad = np.nonzero(np.abs(t[:n] / ref[:n] - 1) > R)[0]
+    return int(bad[0]) if bad.size else n
+
+
+def check_layout(name, info):
+    algo = cc.CASES[name][5]
+    want = {"expansion": pm._abi.SPARSE_EXPANSION, "onthefly": pm._abi.SPARSE_ONTHEFLY,
+            "dense": pm._abi.SPARSE_DENSE}.get(algo)
+    if want is not None:
+        assert info["sparse_algo"] == want, (name, info["sparse_algo"])
+    for k, v in cc.CASES[name][7].items():
+        assert info[k] == v, (name, k, info[k])
+
+
+@pytest.fixture(scope="module")
+def explicit():
+    cache = {}
+
+    def get(name):
+        if name not in cache:
+            s = cc.build(name)
+            cache[name] = (s, *cc.q_explicit(s, with_abs=True))
+        return cache[name]
+
+    return get
+
+
+@pytest.mark.parametrize("name", sorted(cc.CASES))
+def test_sparse_cg_trace_matches_oracle(name, explicit, monkeypatch):
+    s, Q, _ = explicit(name)
+    meta = MANIFEST[name]
+    assert cc.input_hash(s) == meta["input_sha256"], "input recipe drifted from the committed fixtures"
+    g = np.load(os.path.join(cc.VECTORS, name + ".npz"))
+    f64 = s["dtype"] == np.float64
+    R = 1e-6 if f64 else 1e-3
+    with make_svm(s, name, monkeypatch) as svm:
+        svm.learn(imax=cc.IMAX)
+        check_layout(name, svm.info())
+        t, alpha, iters = np.asarray(svm.trace, np.float64), svm.alpha.astype(np.float64), svm.iters
+    t1, t8, tld = g["trace"], g["trace_t8"], g["trace_ld"]
+    assert abs(iters - int(g["iters"][0])) <= 2, (name, iters, int(g["iters"][0]))
+    assert iters >= 50, (name, iters)  # the run crossed the explicit-residual iteration
+    n = min(len(t), len(t1), len(t8))
+    noise = np.maximum.accumulate(np.abs(t8[:n] / t1[:n] - 1))
+    dev = np.abs(t[:n] / t1[:n] - 1)
+    ns = stable_prefix(t1, tld, R)
+    assert ns >= 1
+    assert np.all(dev[:ns] <= R + 10 * noise[:ns]), (name, ns, dev[:ns], noise[:ns])
+    assert stable_prefix(t, tld, 2 * R) >= ns - 1, (name, t[:ns + 2], tld[:ns + 2])
+    assert np.all(dev <= R + 100 * noise), (name, np.nonzero(dev > R + 100 * noise)[0], dev, noise)
+    m = Q.shape[0]
+    yl = np.asarray(s["y"], np.longdouble)
+    b = yl[:m] - yl[m]
+    if f64:
+        def res(a):
+            r = b - Q @ np.asarray(a[:m], np.longdouble)
+            return float(r @ r)
+
+        assert res(alpha) <= 10 * max(res(g["alpha"].astype(np.float64)), (1e-10) ** 2 * float(t1[0])), name
+    else:
+        t64, a32, a64 = g["trace64"], g["alpha"].astype(np.float64), g["alpha64"]
+        nl = min(int(np.argmax(t64 / t64[0] < 1e-6)), len(t), len(t1))  # the prefix above fp32's rounding floor
+        assert nl >= 1
+        ttol = max(1e-3, 2 * float(np.abs(t1[:nl] / t64[:nl] - 1).max()))
+        np.testing.assert_allclose(t[:nl], t64[:nl], rtol=ttol, err_msg=name)
+        amax = float(np.abs(a64).max())
+        atol = max(2e-2, 2 * float(np.abs(a32[:m] - a64[:m]).max()) / amax)
+        np.testing.assert_allclose(alpha[:m], a64[:m], rtol=0, atol=atol * amax, err_msg=name)
+
+
+@pytest.mark.parametrize("name", sorted(cc.CASES))
+def test_sparse_cg_explicit_residual_at_reset(name, explicit, monkeypatch):
+    s, Q, M = explicit(name)
+    g = np.load(os.path.join(cc.VECTORS, name + ".npz"))
+    dtype = s["dtype"]
+    m = Q.shape[0]
+    b = (s["y"][:m] - s["y"][m]).astype(dtype)
+    with make_svm(s, name, monkeypatch) as svm:
+        svm.setup_data_on_device()
+        check_layout(name, svm.info())
+        svm.generate_q()
+        svm.cg_begin(b, eps=s["eps"])
+        it, _ = svm.cg_step(50, force=True)
+        assert it == 50
+        x, tr, _ = svm.cg_result(51)
+    assert len(tr) == 51
+    xl = np.asarray(x, np.longdouble)
+    r = np.asarray(b, np.longdouble) - Q @ xl
+    u = np.finfo(dtype).eps / 2
+    bound = 4 * np.sqrt(m) * u * float(np.linalg.norm(M @ np.abs(xl)))
+    got, true = float(np.sqrt(tr[50])), float(np.sqrt(r @ r))
+    assert abs(got - true) <= bound, (name, got, true, bound)
+    if dtype == np.float32:  # after the reset both fp32 CGs sit on the explicit residual's rounding floor
+        ref = float(np.sqrt(g["trace"][50]))
+        assert ref / 30 <= got <= 30 * ref, (name, got, ref)
+        assert tr[50] > 1e6 * min(tr[45:50]), (name, tr[45:51])  # the jump from the recursive residual

@@ -23,7 +23,7 @@ import sys
 import numpy as np
 import pytest
 
-from mr_cases import ALGO, BUDGET, CASES, UNSTORED, case_data
+from mr_cases import ALGO, BUDGET, CASES, LONG_ROWS, UNSTORED, case_data
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -102,6 +102,11 @@ def test_world2_group_matches_oracle(oracle, case, tmp_path):
         assert all(int(r["pairs"]) > 0 for r in res)
     # one K·p algorithm for the whole group, also when the ranks' own estimates straddle the budget
     assert len({int(r["sparse_algo"]) for r in res}) == 1, [int(r["sparse_algo"]) for r in res]
+    # one H storage for the whole group (the sharded K·p gathers bfloat16 or real w by it): a rank whose rows
+    # cannot take the bfloat16 bound (LONG_ROWS: the column-join sort) keeps both ranks on real H
+    assert len({int(r["exp_hbytes"]) for r in res}) == 1, [int(r["exp_hbytes"]) for r in res]
+    if case in LONG_ROWS:
+        assert int(res[0]["exp_hbytes"]) == np.dtype(dtype).itemsize
     if case in BUDGET:
         import plssvm_sparse_fp22_amd as pm
 

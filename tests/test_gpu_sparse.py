@@ -449,32 +449,40 @@ def test_expansion_row_join_equals_sort_join(kernel, shape, sim, dtype, monkeypa
     (PLSSVM_MI_EXP_JOIN=sort: every incidence generated, radix-sorted, reduced by key): the same pairs
     (info.pairs) and the same K·p overlap sums — both sum a pair's per-feature products in ascending
     feature order in fp64, so H agrees to the last bit of fp64 before the rounding to the real type.
-    (3000 x 50 @ 40 %: dense-ish rows whose repeats overflow a pass, so passes are split.)"""
+    (3000 x 50 @ 40 %: dense-ish rows whose repeats overflow a pass, so passes are split.) "capped": the
+    row join limited to one pass per row (PLSSVM_MI_EXP_RJ_PMAX=1; default 256) — a rank with a row that needs
+    more passes builds its rows by the sort join instead, with the same result."""
     n, d, k = shape
     csr, _ = datagen.sparse_csr(n, d, k, seed=17, dtype=np.float64)
     m = n - 1
     x = np.random.default_rng(3).uniform(1, 2, m).astype(dtype)
     out = {}
-    for join in ("row", "sort"):
+    for join in ("row", "sort", "capped"):
         if join == "sort":
             monkeypatch.setenv("PLSSVM_MI_EXP_JOIN", "sort")
         else:
             monkeypatch.delenv("PLSSVM_MI_EXP_JOIN", raising=False)
+        if join == "capped":
+            monkeypatch.setenv("PLSSVM_MI_EXP_RJ_PMAX", "1")
+        else:
+            monkeypatch.delenv("PLSSVM_MI_EXP_RJ_PMAX", raising=False)
         with sparse_svm(csr, kernel, dtype, sim=sim, algo="expansion") as svm:
             svm.setup_data_on_device()
             info = svm.info()
             assert info["sparse_algo"] == pm._abi.SPARSE_EXPANSION
             out[join] = (svm.kp_part(x, "overlap"), info["pairs"], info["pair_slots"])
-    assert out["row"][1] == out["sort"][1] and out["row"][2] == out["sort"][2]
-    a, b = out["row"][0].astype(np.float64), out["sort"][0].astype(np.float64)
     tol = 1e-14 if dtype == np.float64 else 1e-6
-    assert np.abs(a - b).max() <= tol * max(np.abs(b).max(), 1e-300), np.abs(a - b).max()
+    b = out["sort"][0].astype(np.float64)
+    for join in ("row", "capped"):
+        assert out[join][1] == out["sort"][1] and out[join][2] == out["sort"][2], join
+        a = out[join][0].astype(np.float64)
+        assert np.abs(a - b).max() <= tol * max(np.abs(b).max(), 1e-300), (join, np.abs(a - b).max())
 
 
 @pytest.mark.parametrize("gamma,want_hbytes", [(None, 2), (0.2, 4)])
 def test_expansion_bf16_remainder_bound(gamma, want_hbytes, monkeypatch):
     """Remainder storage (expand.hip "H storage"): in a float context H is stored as bfloat16
-    when every stored |H_ij| is at most 2^-15 of its pair's kernel value (1 + E(s) for rbf), so rounding H
+    when every stored |H_ij| is at most 2^-16 of its pair's kernel value (1 + E(s) for rbf), so rounding H
     (relative error <= 2^-9) moves each pair's term by at most 2^-24 of that kernel value — below the float
     rounding of the kernel value itself. Checked: the default layout is bfloat16 on the BASELINE-like set and
     the real type when the bound fails (large gamma: H comparable to the kernel value); the kernel sums
@@ -538,3 +546,34 @@ def test_expansion_row_flags_default_and_oracle(oracle):
         svm.setup_data_on_device()
         assert svm.info()["exp_layout"] == 2
     check_sparse_kp(oracle, csr, "rbf", np.float32, algo="expansion")
+
+
+@pytest.mark.parametrize("rows", ["index", "flags"])
+def test_expansion_dot2_equals_fma_path(oracle, rows, monkeypatch):
+    """The bfloat16 remainder's chunk products as two v_dot2_f32_bf16 instructions (inline assembly with a
+    hand-placed hazard wait, expand.hip EXP_DOT2) against the FMA chain of the same kernel
+    (PLSSVM_MI_EXP_DOT2=0), in both chunk layouts (row index / row-start flags): a chunk's four H and the four
+    partners' w differ in every lane here (seeded real data, distinct rows), so a register mix-up between the
+    two halves (the ROCm 7.2 builtin lowering that made the assembly necessary fed the first half's H to both)
+    moves the sums far beyond rounding. Bar: the products are exact in fp32 in both paths, only the summation
+    of a chunk's four products differs — 2^-20 of the row's overlap magnitude. Both also match the oracle."""
+    monkeypatch.setenv("PLSSVM_MI_EXP_ROWS", rows)
+    csr, _ = datagen.sparse_csr(30000, 2000, 24, seed=29, dtype=np.float32)
+    m = csr[3] - 1
+    x = np.random.default_rng(7).uniform(-2, 2, m).astype(np.float32)
+    out = {}
+    for dot2 in ("1", "0"):
+        monkeypatch.setenv("PLSSVM_MI_EXP_DOT2", dot2)
+        with sparse_svm(csr, "rbf", np.float32, algo="expansion") as svm:
+            svm.setup_data_on_device()
+            info = svm.info()
+            assert info["exp_hbytes"] == 2 and info["exp_layout"] == (2 if rows == "flags" else 1), info
+            assert info["pairs"] > 100000
+            out[dot2] = (svm.kp_part(x, "overlap").astype(np.float64), svm.kp_part(np.abs(x), "overlap").astype(np.float64))
+    a, b = out["1"][0], out["0"][0]
+    mag = np.abs(out["0"][1])
+    scale = np.maximum(mag, np.abs(b)) + 2.0 ** -10 * mag.max()
+    err = np.abs(a - b) / scale
+    assert err.max() <= 2.0 ** -20, err.max()
+    info = check_sparse_kp(oracle, csr, "rbf", np.float32, algo="expansion")
+    assert info["exp_hbytes"] == 2

@@ -11,7 +11,7 @@ mkdir -p "$out"
 export TMPDIR=/tmp
 cd /tmp
 timeout -s KILL 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_VALU \
-  --output-format csv -d "$out" -o run -- python3 "$root/bench.py" --steps 1 --warmup 0 --kp-reps 1 --no-cpu "$@" > "$out/bench.json" 2> "$out/bench.log"
+  --output-format csv -d "$out" -o run -- python3 "$root/bench.py" --steps 1 --warmup 0 --kp-reps 1 --no-cpu --no-extra --no-solve "$@" > "$out/bench.json" 2> "$out/bench.log"
 python3 - "$out" "$*" <<'PY'
 import csv, sys, collections, glob, json
 out, args = sys.argv[1], sys.argv[2]
@@ -24,7 +24,7 @@ last = list(d.values())[-1]
 b = open(out + "/bench.json").read()
 b = json.loads(b[b.index('{"metric'):].splitlines()[0])
 res = {"config": b["config"]["workload"], "N": b["config"]["N"], "d": b["config"]["d"],
-       "kernel": b["config"]["kernel"], "n_gpus": b["n_gpus"], "bench_args": args,
+       "kernel": b["config"]["kernel"], "dtype": b["dtype"], "n_gpus": b["n_gpus"], "bench_args": args,
        "counters": {a: int(b) for a, b in last.items()},
        "mfma_util": last["SQ_VALU_MFMA_BUSY_CYCLES"] / max(1.0, 4 * last["SQ_BUSY_CU_CYCLES"]),
        "coexec_cycles": int(last["SQ_VALU_MFMA_COEXEC_CYCLES"])}
