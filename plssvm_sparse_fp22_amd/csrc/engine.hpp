@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 #include <rocblas/rocblas.h>
 
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -162,8 +163,9 @@ struct engine : engine_base {
     void sparse_q();                                              // q, norms, e on CSR data
     void build_gram_blocks(const int64_t *cpos, int64_t max_inc);  // sparse Gram pattern (pairwise kernels)
     int64_t sparse_mem_budget() const;                             // device bytes for stored sparse structures
+    // row_stats (optional): the sampled rows' partners sharing >= 2 features, mean and max
     int64_t estimate_expansion_bytes(const int64_t *rowptr, const int32_t *col, const std::vector<int64_t> &colptr,
-                                     const std::vector<int32_t> &crow, int64_t inc_total) const;
+                                     const std::vector<int32_t> &crow, int64_t inc_total, double *row_stats = nullptr) const;
     void release_sparse_structures();
     void setup_sparse_dense();                                     // densified fallback (PLSSVM_MI_SPARSE_DENSE)
     // on-the-fly path (otf.hip, PLSSVM_MI_SPARSE_ONTHEFLY): estimated seconds per K·p share, setup, K·p
@@ -173,9 +175,10 @@ struct engine : engine_base {
     void otf_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);
     bool sparse_stored() const { return sparse && !csr.dense_on; } // K·p through the CSR structures
     bool expansion_eligible();                                    // expand.hip: K, coefficients; true if usable
-    // multi-overlap remainder H, diagonal; pre: a failure of the caller's preceding step (the SELL plans), which
-    // still joins the group's agreement inside and is rethrown there
-    void build_expansion(const int64_t *cpos, int64_t max_inc, std::exception_ptr pre = nullptr);
+    // multi-overlap remainder H, diagonal; before_agree (optional): waits for a step the caller runs concurrently
+    // (the SELL plans, on a host thread) and returns its failure, which joins the group's agreement and is rethrown
+    void build_expansion(const int64_t *cpos, int64_t max_inc,
+                         const std::function<std::exception_ptr()> &before_agree = {});
     void expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base);
     void expansion_dominant(const T *p, const cg_scalars<T> *status);  // the remainder stream
     // column moments (SELL CSC pass); spart: the moment reduce also forms S from w's partials (sG sets)

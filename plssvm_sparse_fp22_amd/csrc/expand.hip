@@ -454,6 +454,194 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
     if (tid == 0 && lnz_s) atomicAdd(lower_nz, lnz_s);
 }
 
+// One-pass row join (default; PLSSVM_MI_EXP_RJ=twopass keeps count pass + write pass + exp_rowjoin_h_kernel):
+// exp_rowjoin_kernel's passes, and after each pass's enumeration the block forms H of that pass's partners
+// at once — one thread per partner, row j's entries merged into row i's features through an LDS hash of
+// them (one probe per entry instead of a binary search), the matches summed in ascending feature order in
+// fp64 (the arithmetic of exp_rowjoin_h_kernel, so the same H bits) — and writes (j, H) into the row's fixed
+// slot range [r cap, r cap + cap) of the pool. cnt[r] = the row's partner count, also beyond cap (the host
+// checks max over rows <= cap, else it redoes the rows by the two-pass join with exact offsets). No count
+// pass, no padded partner list written and read back.
+constexpr int RJ_HS = 2048;  // hash slots for row i's features (<= RJ_ECAP keys: load <= 1/8)
+__device__ __forceinline__ int rj_hash(int32_t f) { return (int) (((uint32_t) f * 2654435761u) >> (32 - 11)); }
+template <typename T>
+__global__ __launch_bounds__(RJ_NT) void exp_rowjoin_fused_kernel(const int64_t *__restrict__ rowptr,
+                                                                  const int32_t *__restrict__ col,
+                                                                  const T *__restrict__ val,
+                                                                  const int64_t *__restrict__ colptr,
+                                                                  const int32_t *__restrict__ crow, int64_t m, int64_t r0,
+                                                                  int64_t cap, phi_fn phi, double kbase,
+                                                                  int32_t *__restrict__ pj, T *__restrict__ ph,
+                                                                  int64_t *__restrict__ cnt, unsigned int *__restrict__ ovf,
+                                                                  int pmax, unsigned long long *__restrict__ lower_nz,
+                                                                  unsigned long long *__restrict__ ratio_bits,
+                                                                  unsigned long long *__restrict__ cnt_max) {
+    __shared__ uint32_t bm[RJ_BMW];
+    __shared__ int32_t rep[RJ_LCAP];
+    __shared__ int32_t zcol[RJ_ECAP];
+    __shared__ T zval[RJ_ECAP];
+    __shared__ int32_t zoff[RJ_ECAP + 1];
+    __shared__ int64_t cst[RJ_ECAP];
+    __shared__ int32_t hkey[RJ_HS];
+    __shared__ uint8_t hidx[RJ_HS];
+    __shared__ int32_t wtot[RJ_NT / 64];
+    __shared__ int nrep_s;
+    __shared__ unsigned long long lnz_s;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t r = blockIdx.x, i = r0 + r;
+    const int64_t e0 = rowptr[i];
+    const int ne = (int) (rowptr[i + 1] - e0);  // <= RJ_ECAP (host-checked)
+    for (int q = tid; q < RJ_HS; q += RJ_NT) hkey[q] = -1;
+    if (tid == 0) lnz_s = 0ull;
+    for (int e = tid; e < ne; e += RJ_NT) {
+        const int32_t f = col[e0 + e];
+        zcol[e] = f;
+        zval[e] = val[e0 + e];
+        cst[e] = colptr[f];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int32_t a = 0;
+        for (int e = 0; e < ne; ++e) {
+            zoff[e] = a;
+            a += (int32_t) (colptr[zcol[e] + 1] - cst[e]);
+            int h = rj_hash(zcol[e]);
+            while (hkey[h] >= 0) h = (h + 1) & (RJ_HS - 1);  // linear probing, <= 1/8 full
+            hkey[h] = zcol[e];
+            hidx[h] = (uint8_t) e;
+        }
+        zoff[ne] = a;
+    }
+    __syncthreads();
+    const int32_t inc = zoff[ne];
+    const int64_t base = r * cap;
+    int64_t written = 0;
+    unsigned long long lnz = 0ull;
+    double rmax = 0.0;
+    constexpr int64_t SPAN_MAX = (int64_t) RJ_BMW * 32;
+    int64_t span = SPAN_MAX;
+    int passes = 0;
+    for (int64_t R0 = 0; R0 < m;) {
+        if (++passes > pmax) {  // uniform
+            if (tid == 0) {
+                cnt[r] = 0;
+                atomicOr(ovf, 1u);
+            }
+            return;
+        }
+        const int64_t R1 = min(m, R0 + span);
+        for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
+        if (tid == 0) nrep_s = 0;
+        __syncthreads();
+        int e = 0;
+        for (int32_t t = tid; t < inc; t += RJ_NT) {
+            while (zoff[e + 1] <= t) ++e;
+            const int64_t j = crow[cst[e] + (t - zoff[e])];
+            if (j == i || j < R0 || j >= R1) continue;
+            const uint32_t bit = 1u << ((j - R0) & 31);
+            const uint32_t old = atomicOr(&bm[(j - R0) >> 5], bit);
+            if (old & bit) {
+                const int q = atomicAdd(&nrep_s, 1);
+                if (q < RJ_LCAP) rep[q] = (int32_t) j;
+            }
+        }
+        __syncthreads();
+        const int nr = nrep_s;
+        if (nr > RJ_LCAP) {  // uniform: this range again in halves
+            span = (span + 1) / 2;
+            __syncthreads();
+            continue;
+        }
+        for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
+        __syncthreads();
+        for (int q = tid; q < nr; q += RJ_NT) {
+            const int64_t j = rep[q] - R0;
+            atomicOr(&bm[j >> 5], 1u << (j & 31));
+        }
+        __syncthreads();
+        int c = 0;
+#pragma unroll 8
+        for (int w = 0; w < RJ_WPT; ++w) c += __popc(bm[tid * RJ_WPT + w]);
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wtot[wave] = incl;
+        __syncthreads();
+        int before = 0, U = 0;
+        for (int w = 0; w < RJ_NT / 64; ++w) {
+            const int v = wtot[w];
+            if (w < wave) before += v;
+            U += v;
+        }
+        {
+            int pos = before + incl - c;
+            for (int w = 0; w < RJ_WPT; ++w) {
+                uint32_t word = bm[tid * RJ_WPT + w];
+                while (word) {
+                    const int b = __ffs(word) - 1;
+                    word &= word - 1;
+                    rep[pos++] = (int32_t) (R0 + (int64_t) (tid * RJ_WPT + w) * 32 + b);
+                }
+            }
+        }
+        __syncthreads();
+        // H of this pass's partners (ascending in rep): thread q merges row j into row i's features
+        for (int q = tid; q < U; q += RJ_NT) {
+            const int64_t j = rep[q];
+            const int64_t kb = rowptr[j], ke = rowptr[j + 1];
+            double sd = 0.0, sphi = 0.0;
+            int32_t fn = kb < ke ? col[kb] : 0;
+            T vn = kb < ke ? val[kb] : T(0);
+            for (int64_t k = kb; k < ke; ++k) {
+                const int32_t f = fn;
+                const T v = vn;
+                if (k + 1 < ke) fn = col[k + 1], vn = val[k + 1];  // the next entry in flight
+                int h = rj_hash(f);
+                int32_t key;
+                while ((key = hkey[h]) >= 0 && key != f) h = (h + 1) & (RJ_HS - 1);
+                if (key == f) {
+                    const double a = (double) zval[hidx[h]] * (double) v;
+                    sd += a;
+                    sphi += phi(a);
+                }
+            }
+            const double ps = phi(sd);
+            const T hv = (T) (ps - sphi);
+            const double kv = fabs(kbase + ps);
+            const double ratio = hv == T(0) ? 0.0 : (kv > 0.0 ? fabs((double) hv) / kv : 1e300);
+            rmax = fmax(rmax, ratio);
+            if (j < i && hv != T(0)) ++lnz;
+            const int64_t pos = written + q;
+            if (pos < cap) {
+                pj[base + pos] = (int32_t) j;
+                ph[base + pos] = hv;
+            }
+        }
+        written += U;
+        __syncthreads();  // bm / rep are reused by the next pass
+        R0 = R1;
+        span = min(span * 2, SPAN_MAX);
+    }
+    if (lnz) atomicAdd(&lnz_s, lnz);
+    if (rmax > 0.0) atomicMax(ratio_bits, (unsigned long long) __double_as_longlong(rmax));  // >= 0: bit order
+    __syncthreads();
+    if (tid == 0) {
+        cnt[r] = written;
+        if (lnz_s) atomicAdd(lower_nz, lnz_s);
+        atomicMax(cnt_max, (unsigned long long) written);
+    }
+}
+
+// the fused join's row ranges: beg[r] = r cap, end[r] = r cap + cnt[r] (every count <= cap, host-checked)
+__global__ __launch_bounds__(256) void exp_pool_range_kernel(const int64_t *__restrict__ cnt, int64_t R, int64_t cap,
+                                                             int64_t *__restrict__ beg, int64_t *__restrict__ end) {
+    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < R) beg[r] = r * cap, end[r] = r * cap + cnt[r];
+}
+
 __global__ __launch_bounds__(256) void exp_pad8_cnt_kernel(const int64_t *__restrict__ cnt, int64_t R,
                                                            int64_t *__restrict__ cnt8) {
     const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
@@ -537,14 +725,14 @@ __device__ __forceinline__ int64_t exp_cidx(int64_t r, int64_t W, int64_t nW, in
 
 // per row r (rank-local), window W: count of its non-zero entries with j in W, rounded up to 4 slots
 template <typename T>
-__global__ __launch_bounds__(256) void exp_cell_count_kernel(const int64_t *__restrict__ off8,
+__global__ __launch_bounds__(256) void exp_cell_count_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
                                                              const int32_t *__restrict__ sj, const T *__restrict__ sv,
                                                              int64_t R, int64_t nW, int64_t CW, int64_t RB,
                                                              int64_t *__restrict__ cnt) {
     const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
     int64_t Wc = -1, k = 0;
-    for (int64_t s = off8[r]; s < off8[r + 1]; ++s) {  // entries sorted by j
+    for (int64_t s = rbeg[r]; s < rend[r]; ++s) {  // entries sorted by j
         if (sv[s] == T(0)) continue;                    // pads (and no stored H is exactly 0)
         const int64_t W = sj[s] / CW;
         if (W != Wc) {
@@ -621,7 +809,7 @@ __global__ __launch_bounds__(256) void exp_wown_kernel(const T *__restrict__ e, 
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__restrict__ off8,
+__global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
                                                                const int32_t *__restrict__ sj, const T *__restrict__ sv,
                                                                int64_t R, int64_t nW, int64_t CW, int64_t RB,
                                                                const int64_t *__restrict__ coff,
@@ -634,7 +822,7 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__
     auto close = [&]() {
         for (int64_t q = 0; q < ((k + 3) >> 2); ++q) hrow[(base >> 2) + q] = rl;
     };
-    for (int64_t s = off8[r]; s < off8[r + 1]; ++s) {
+    for (int64_t s = rbeg[r]; s < rend[r]; ++s) {
         const T h = sv[s];
         if (h == T(0)) continue;
         const int64_t W = sj[s] / CW;
@@ -662,14 +850,14 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__
 // stats[0] += windows without entries (the dummies the layout would add), stats[1] |= 1 when a stored H's
 // bfloat16 has bit 14 set (|H| >= 2: the bit is not free)
 template <typename T>
-__global__ __launch_bounds__(256) void exp_cell_stats_kernel(const int64_t *__restrict__ off8, const int32_t *__restrict__ sj,
+__global__ __launch_bounds__(256) void exp_cell_stats_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend, const int32_t *__restrict__ sj,
                                                              const T *__restrict__ sv, int64_t R, int64_t nW, int64_t CW,
                                                              unsigned long long *__restrict__ stats) {
     const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long empty = 0, big = 0;
     if (r < R) {
         int64_t Wc = -1, nwin = 0;
-        for (int64_t s = off8[r]; s < off8[r + 1]; ++s) {
+        for (int64_t s = rbeg[r]; s < rend[r]; ++s) {
             if (sv[s] == T(0)) continue;
             const int64_t W = sj[s] / CW;
             if (W != Wc) Wc = W, ++nwin;
@@ -707,15 +895,15 @@ __device__ __forceinline__ int64_t exp_jh_h(int64_t t) { return EXP_JH ? ((t & ~
 // exp_cell_scatter_kernel for the flagged layout (bfloat16 H, buffers zeroed): every window of the row in
 // order, its entries (or a dummy), bit 14 set on the cell's first H
 template <typename T>
-__global__ __launch_bounds__(256) void exp_cell_scatter_flag_kernel(const int64_t *__restrict__ off8,
+__global__ __launch_bounds__(256) void exp_cell_scatter_flag_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
                                                                     const int32_t *__restrict__ sj, const T *__restrict__ sv,
                                                                     int64_t R, int64_t nW, int64_t CW, int64_t RB,
                                                                     const int64_t *__restrict__ coff,
                                                                     uint16_t *__restrict__ hjl, uint16_t *__restrict__ hv16) {
     const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
-    int64_t s = off8[r];
-    const int64_t se = off8[r + 1];
+    int64_t s = rbeg[r];
+    const int64_t se = rend[r];
     for (int64_t W = 0; W < nW; ++W) {
         const int64_t base = coff[exp_cidx(r, W, nW, RB)];
         int64_t k = 0;
@@ -737,7 +925,7 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_flag_kernel(const int64_
 // H = 0). A wave's stream of a window then lists its RPW rows in order and the row of an entry is the
 // number of flags up to it: neither the 4-slot padding nor the chunk rows of the chunk layout are stored.
 template <typename T>
-__global__ __launch_bounds__(256) void exp_run_count_kernel(const int64_t *__restrict__ off8,
+__global__ __launch_bounds__(256) void exp_run_count_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
                                                             const int32_t *__restrict__ sj, const T *__restrict__ sv,
                                                             int64_t R, int64_t nW, int64_t CW, int64_t RB,
                                                             int64_t *__restrict__ cnt,
@@ -746,7 +934,7 @@ __global__ __launch_bounds__(256) void exp_run_count_kernel(const int64_t *__res
     if (r >= R) return;
     for (int64_t W = 0; W < nW; ++W) cnt[exp_cidx(r, W, nW, RB)] = 1;  // the dummy, unless entries follow
     int64_t Wc = -1, k = 0, filled = 0;
-    for (int64_t s = off8[r]; s < off8[r + 1]; ++s) {
+    for (int64_t s = rbeg[r]; s < rend[r]; ++s) {
         if (sv[s] == T(0)) continue;
         const int64_t W = sj[s] / CW;
         if (W != Wc) {
@@ -762,7 +950,7 @@ __global__ __launch_bounds__(256) void exp_run_count_kernel(const int64_t *__res
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void exp_run_scatter_kernel(const int64_t *__restrict__ off8,
+__global__ __launch_bounds__(256) void exp_run_scatter_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
                                                               const int32_t *__restrict__ sj, const T *__restrict__ sv,
                                                               int64_t R, int64_t nW, int64_t CW, int64_t RB,
                                                               const int64_t *__restrict__ coff,
@@ -775,7 +963,7 @@ __global__ __launch_bounds__(256) void exp_run_scatter_kernel(const int64_t *__r
         hv[b] = T(0);
     }
     int64_t Wc = -1, base = 0, k = 0;
-    for (int64_t s = off8[r]; s < off8[r + 1]; ++s) {
+    for (int64_t s = rbeg[r]; s < rend[r]; ++s) {
         const T h = sv[s];
         if (h == T(0)) continue;
         const int64_t W = sj[s] / CW;
@@ -1362,7 +1550,8 @@ bool engine<T>::expansion_eligible() {
 // write pass with H from a merge of the two rows), or by the column-join sort (every incidence (i, j < i,
 // a, phi(a)) generated, radix-sorted and reduced by key; PLSSVM_MI_EXP_JOIN=sort); H_ii; the moment buffers.
 template <typename T>
-void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::exception_ptr pre) {
+void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
+                                const std::function<std::exception_ptr()> &before_agree) {
     auto &ex = csr.ex;
     phase_timer pt;
     const phi_fn phi = make_phi<T>(kernel, degree, gamma, coef0);
@@ -1371,6 +1560,8 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::e
     dev_buf<int32_t> sj;
     dev_buf<T> sv;
     int64_t nslot8 = 0;
+    dev_buf<int64_t> pbeg, pend;
+    const int64_t *rbeg = nullptr, *rend = nullptr;  // row r's symmetric entries: [rbeg[r], rend[r]) of (sj, sv)
     ex.hratio = -1.0;
     {
         const char *e = std::getenv("PLSSVM_MI_EXP_DOT2");
@@ -1378,8 +1569,8 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::e
     }
     // phase 1 (the symmetric rows) may fail on one rank only (memory, a dense row): in a real group every rank
     // still reaches the agreement after it, which raises the same error everywhere
-    std::exception_ptr fail1 = pre;
-    if (!fail1) try {
+    std::exception_ptr fail1;
+    try {
     ex.M.alloc(std::max<int64_t>(d, 1) * ex.KM, stream);
     ex.mom.alloc(std::max<int64_t>(d, 1) * ex.KM, stream);
     csr.ssc.alloc(2, stream);  // device scalar S = sum_j w_j
@@ -1659,19 +1850,81 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::e
         const int v = e ? std::atoi(e) : 0;
         return v >= 1 ? v : RJ_PMAX;
     }();
-    if (row_join) {
+    double kbase = 1.0;  // rbf: 1 + E(s); poly: kappa + c(s)
+    if (kernel == 1)
+        for (int q2 = 0; q2 < degree; ++q2) kbase *= (double) coef0;
+    auto read_lnz = [&]() {
+        unsigned long long np[2] = { 0ull, 0ull };
+        MI_HIP_CHECK(hipMemcpyAsync(np, lnz.get(), sizeof(np), hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        ex.pairs = (int64_t) np[0];
+        double rm = 0.0;
+        std::memcpy(&rm, &np[1], sizeof(rm));
+        ex.hratio = rm;
+    };
+    // one-pass join (exp_rowjoin_fused_kernel) into fixed per-row slot ranges of cap entries, cap from the setup's
+    // sample of the rank's rows (estimate_expansion_bytes); PLSSVM_MI_EXP_RJ=twopass keeps the two-pass join
+    bool have_cnt = false;  // cnt[] holds every row's exact partner count (a fused pass whose cap was too small)
+    if (row_join && R > 0) {
+        const char *rj = std::getenv("PLSSVM_MI_EXP_RJ");
+        const bool want = !(rj != nullptr && std::strcmp(rj, "twopass") == 0);
+        int64_t cap = round_up(std::max<int64_t>({ (int64_t) (2.0 * ex.rj_mean), (int64_t) (1.5 * ex.rj_max), 64 }), 8);
+        if (const char *e = std::getenv("PLSSVM_MI_EXP_RJ_CAP")) {  // tests: force the overflow redo
+            const long long v = std::atoll(e);
+            if (v > 0) cap = v;
+        }
+        size_t free_b = 0, total_b = 0;
+        MI_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+        const double pool_b = (double) R * (double) cap * (double) (4 + sizeof(T));
+        if (want && ex.rj_mean > 0.0 && pool_b <= 0.4 * (double) free_b) {
+            sj.alloc(R * cap, stream, false);
+            sv.alloc(R * cap, stream, false);
+            cnt.alloc(R, stream);
+            lnz.alloc(3, stream);  // [0] lower pairs with H != 0, [1] max |H| / kernel value (double bits), [2] max count
+            dev_buf<unsigned int> ovf;
+            ovf.alloc(1, stream);
+            hipLaunchKernelGGL(exp_rowjoin_fused_kernel<T>, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
+                               csr.col.get(), csr.val.get(), csr.colptr.get(), csr.crow.get(), m, r0, cap, phi, kbase,
+                               sj.get(), sv.get(), cnt.get(), ovf.get(), rj_pmax, lnz.get(), lnz.get() + 1, lnz.get() + 2);
+            MI_LAUNCH_CHECK();
+            unsigned long long cmax = 0ull;
+            MI_HIP_CHECK(hipMemcpyAsync(&ovf_h, ovf.get(), sizeof(ovf_h), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipMemcpyAsync(&cmax, lnz.get() + 2, sizeof(cmax), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            pt.mark("expansion: row join (one pass)");
+            if (ovf_h != 0u) {  // a row whose partner clusters need more than RJ_PMAX passes: the sort join
+                sj.reset(), sv.reset(), cnt.reset();
+                row_join = false;
+            } else if ((int64_t) cmax > cap) {  // a row beyond its slots: the two-pass join with these exact counts
+                sj.reset(), sv.reset();
+                have_cnt = true;
+            } else {
+                read_lnz();
+                pbeg.alloc(R, stream, false);
+                pend.alloc(R, stream, false);
+                hipLaunchKernelGGL(exp_pool_range_kernel, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream, cnt.get(),
+                                   R, cap, pbeg.get(), pend.get());
+                MI_LAUNCH_CHECK();
+                rbeg = pbeg.get();
+                rend = pend.get();
+            }
+        }
+    }
+    if (row_join && rbeg == nullptr) {
+        // two passes: count (unless the fused pass counted), padded offsets, then the write pass and H
         off8.alloc(R + 1, stream);
-        {
-        cnt.alloc(std::max<int64_t>(R, 1), stream);
+        if (!have_cnt) cnt.alloc(std::max<int64_t>(R, 1), stream);
         cnt8.alloc(R + 1, stream);
-        lnz.alloc(2, stream);  // [0] lower pairs with H != 0, [1] max |H| / kernel value (double bits)
+        lnz.alloc(3, stream);
         dev_buf<unsigned int> ovf;
         ovf.alloc(1, stream);
-        if (R > 0) {
+        if (R > 0 && !have_cnt) {
             hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
                                csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(),
                                (const int64_t *) nullptr, (int32_t *) nullptr, ovf.get(), rj_pmax);
             MI_LAUNCH_CHECK();
+        }
+        if (R > 0) {
             hipLaunchKernelGGL(exp_pad8_cnt_kernel, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream, cnt.get(),
                                R, cnt8.get());
             MI_LAUNCH_CHECK();
@@ -1690,41 +1943,37 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::e
         if (ovf_h != 0u) {  // a row whose partner clusters need more than RJ_PMAX passes: the sort join
             off8.reset();
             row_join = false;
-        }
+        } else {
+            sj.alloc(std::max<int64_t>(nslot8, 8), stream, false);
+            sv.alloc(std::max<int64_t>(nslot8, 8), stream, false);
+            if (R > 0) {
+                hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
+                                   csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(), off8.get(), sj.get(),
+                                   (unsigned int *) nullptr, rj_pmax);
+                MI_LAUNCH_CHECK();
+                hipLaunchKernelGGL(exp_rowjoin_h_kernel<T>, dim3((unsigned) R), dim3(RJH_NT), 0, stream, csr.rowptr.get(),
+                                   csr.col.get(), csr.val.get(), r0, phi, kbase, off8.get(), sj.get(), sv.get(), lnz.get(),
+                                   lnz.get() + 1);
+                MI_LAUNCH_CHECK();
+            }
+            read_lnz();
+            rbeg = off8.get();
+            rend = off8.get() + 1;
+            pt.mark("expansion: row join (rows)");
         }
     }
-    if (row_join) {
-        sj.alloc(std::max<int64_t>(nslot8, 8), stream, false);
-        sv.alloc(std::max<int64_t>(nslot8, 8), stream, false);
-        if (R > 0) {
-            hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
-                               csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(), off8.get(), sj.get(),
-                               (unsigned int *) nullptr, rj_pmax);
-            MI_LAUNCH_CHECK();
-            double kbase = 1.0;  // rbf: 1 + E(s); poly: kappa + c(s)
-            if (kernel == 1) {
-                kbase = 1.0;
-                for (int q2 = 0; q2 < degree; ++q2) kbase *= (double) coef0;
-            }
-            hipLaunchKernelGGL(exp_rowjoin_h_kernel<T>, dim3((unsigned) R), dim3(RJH_NT), 0, stream, csr.rowptr.get(),
-                               csr.col.get(), csr.val.get(), r0, phi, kbase, off8.get(), sj.get(), sv.get(), lnz.get(),
-                               lnz.get() + 1);
-            MI_LAUNCH_CHECK();
-        }
-        unsigned long long np[2] = { 0ull, 0ull };
-        MI_HIP_CHECK(hipMemcpyAsync(np, lnz.get(), sizeof(np), hipMemcpyDeviceToHost, stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-        ex.pairs = (int64_t) np[0];
-        double rm = 0.0;
-        std::memcpy(&rm, &np[1], sizeof(rm));
-        ex.hratio = rm;
-        pt.mark("expansion: row join (rows)");
-    } else {
+    if (!row_join) {
         sort_join();
+        rbeg = off8.get();
+        rend = off8.get() + 1;
     }
     pt.mark("expansion: symmetric rows");
     } catch (...) {
         fail1 = std::current_exception();
+    }
+    if (before_agree) {  // the caller's concurrent step (the SELL plans): joined here, its failure counts as ours
+        std::exception_ptr e = before_agree();
+        if (e && !fail1) fail1 = e;
     }
     // H storage (float contexts): bfloat16 when every stored |H_ij| is at most 2^-16 of its pair's kernel value
     // (the row join's hratio; see "H storage" below). A sharded group gathers bfloat16 w or real w by this flag
@@ -1825,7 +2074,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::e
             dev_buf<unsigned long long> dum;
             dum.alloc(1, stream);
             hipLaunchKernelGGL(exp_run_count_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                               off8.get(), sj.get(), sv.get(), R, ex.nW, (int64_t) ex.CW, RB, cnt.get(), dum.get());
+                               rbeg, rend, sj.get(), sv.get(), R, ex.nW, (int64_t) ex.CW, RB, cnt.get(), dum.get());
             MI_LAUNCH_CHECK();
             unsigned long long nd = 0;
             MI_HIP_CHECK(hipMemcpyAsync(&nd, dum.get(), sizeof(nd), hipMemcpyDeviceToHost, stream));
@@ -1837,7 +2086,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::e
                 ex.hv.alloc(ex.slots + 512, stream);
                 ex.hrow.reset();
                 hipLaunchKernelGGL(exp_run_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                                   off8.get(), sj.get(), sv.get(), R, ex.nW, (int64_t) ex.CW, RB, coff.get(),
+                                   rbeg, rend, sj.get(), sv.get(), R, ex.nW, (int64_t) ex.CW, RB, coff.get(),
                                    ex.hjl.get(), ex.hv.get());
                 MI_LAUNCH_CHECK();
                 ex.woff.alloc(std::max<int64_t>(nbv * (ex.nW + 1), 1), stream);
@@ -1861,7 +2110,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::e
             coff.alloc(ncnt + 1, stream, false);
             if (R > 0) {
                 hipLaunchKernelGGL(exp_cell_count_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                                   off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, cnt.get());
+                                   rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, RB, cnt.get());
                 MI_LAUNCH_CHECK();
             }
             // flagged chunks (bfloat16 H only): when every |H| < 2 and the dummies of empty cells (16 B each) cost
@@ -1875,7 +2124,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::e
                     dev_buf<unsigned long long> st;
                     st.alloc(2, stream);
                     hipLaunchKernelGGL(exp_cell_stats_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                                       off8.get(), sj.get(), sv.get(), R, ex.nW, CW, st.get());
+                                       rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, st.get());
                     MI_LAUNCH_CHECK();
                     unsigned long long hs2[2] = { 0ull, 0ull };
                     MI_HIP_CHECK(hipMemcpyAsync(hs2, st.get(), sizeof(hs2), hipMemcpyDeviceToHost, stream));
@@ -1901,14 +2150,14 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/, std::e
             if (ex.rflags) {
                 ex.hrow.reset();
                 hipLaunchKernelGGL(exp_cell_scatter_flag_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                                   off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
+                                   rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
                                    EXP_JH ? ex.hjl.get() : ex.hv16.get());
                 MI_LAUNCH_CHECK();
             } else {
                 ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
                 if (R > 0) {
                     hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                                       off8.get(), sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
+                                       rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
                                        ex.hv.get(), ex.hv16.get(), ex.hrow.get());
                     MI_LAUNCH_CHECK();
                 }
@@ -2445,7 +2694,7 @@ bool engine<T>::expansion_predict(const T *alpha_dev, T alpha_m, T bias, const i
 
 #define INST(T)                                                                              \
     template bool engine<T>::expansion_eligible();                                           \
-    template void engine<T>::build_expansion(const int64_t *, int64_t, std::exception_ptr);                      \
+    template void engine<T>::build_expansion(const int64_t *, int64_t, const std::function<std::exception_ptr()> &);                      \
     template void engine<T>::expansion_dominant(const T *, const cg_scalars<T> *);           \
     template void engine<T>::expansion_moments(const T *, const cg_scalars<T> *, const T *, int);            \
     template void engine<T>::expansion_mscale(const cg_scalars<T> *);                        \

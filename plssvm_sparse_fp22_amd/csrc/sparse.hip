@@ -14,6 +14,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -782,8 +783,10 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         if (!unstored) {
             int64_t inc_total = 0;
             for (int64_t I = csr.rb0; I < csr.rb1; ++I) inc_total += inc_rb[I];
-            csr.est_bytes = use_exp ? estimate_expansion_bytes(rowptr, col, colptr, crow, inc_total)
+            double rs[2] = { 0.0, 0.0 };
+            csr.est_bytes = use_exp ? estimate_expansion_bytes(rowptr, col, colptr, crow, inc_total, rs)
                                     : csr.pair_bound * (int64_t) (2 * (2 + sizeof(T))) + max_inc * 48;
+            csr.ex.rj_mean = rs[0], csr.ex.rj_max = rs[1];  // the one-pass row join's slots per row
         }
         // A real group takes every choice below once, identically on all ranks (the paths run different
         // collectives on different partitions): the largest estimate against the smallest budget, the
@@ -828,17 +831,42 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                     const bool local = (world > 1 && sim_world == 0) || (sim_world > 0 && shard);
                     csr.csc_r0 = local ? r0 : 0;
                     csr.csc_r1 = local ? r1 : m;
-                    std::exception_ptr plan_fail;  // joins build_expansion's group agreement, rethrown there
+                    // the two SELL plans (host work + uploads on a stream of their own) run on a host thread while
+                    // the GPU builds the remainder's rows; build_expansion joins it before the group agreement
+                    std::exception_ptr plan_fail;
+                    hipStream_t ps = nullptr;
+                    std::thread plans([&] {
+                        try {
+                            phase_timer tp;
+                            MI_HIP_CHECK(hipSetDevice(device));
+                            MI_HIP_CHECK(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
+                            build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0,
+                                               rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22, csc_gen(csr.csc_r0, csr.csc_r1),
+                                               blocks, ps, 0, 1, csr.ex.KM);
+                            build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks,
+                                               ps, 0, csr.ex.KM, 1);
+                            MI_HIP_CHECK(hipStreamSynchronize(ps));
+                            tp.mark("setup_csr: SELL plans (host thread, beside the row join)");
+                        } catch (...) {
+                            plan_fail = std::current_exception();
+                        }
+                    });
+                    bool joined = false;
+                    auto join_plans = [&]() -> std::exception_ptr {
+                        if (!joined) {
+                            plans.join();
+                            joined = true;
+                            if (ps != nullptr) (void) hipStreamDestroy(ps);
+                        }
+                        return plan_fail;
+                    };
                     try {
-                        build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0],
-                                           f22, csc_gen(csr.csc_r0, csr.csc_r1), blocks, stream, 0, 1, csr.ex.KM);
-                        build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks,
-                                           stream, 0, csr.ex.KM, 1);
+                        build_expansion(cpos_d.get(), max_inc, join_plans);
                     } catch (...) {
-                        plan_fail = std::current_exception();
+                        join_plans();
+                        throw;
                     }
-                    pt.mark("setup_csr: SELL plans");
-                    build_expansion(cpos_d.get(), max_inc, plan_fail);
+                    join_plans();
                     pt.mark("setup_csr: expansion");
                 } else {
                     build_gram_blocks(cpos_d.get(), max_inc);
@@ -938,13 +966,13 @@ int64_t engine<T>::sparse_mem_budget() const {
 // sort temporaries
 template <typename T>
 int64_t engine<T>::estimate_expansion_bytes(const int64_t *rowptr, const int32_t *col, const std::vector<int64_t> &colptr,
-                                            const std::vector<int32_t> &crow, int64_t inc_total) const {
+                                            const std::vector<int32_t> &crow, int64_t inc_total, double *row_stats) const {
     const int64_t R = r1 - r0;
     if (R <= 0 || m <= 0) return 0;
     std::vector<int32_t> cnt((size_t) m, 0);
     std::vector<int32_t> touched;
     const int64_t S = std::min<int64_t>(R, 64);
-    int64_t sampled = 0, entries = 0, inc = 0;
+    int64_t sampled = 0, entries = 0, inc = 0, row_max = 0;
     for (int64_t s = 0; s < S && inc < (int64_t(1) << 28); ++s) {
         const int64_t i = r0 + (s * R) / S;
         touched.clear();
@@ -956,13 +984,17 @@ int64_t engine<T>::estimate_expansion_bytes(const int64_t *rowptr, const int32_t
             }
             inc += colptr[f + 1] - colptr[f];
         }
+        int64_t row_entries = 0;
         for (const int32_t j : touched) {
-            if (j != i && cnt[j] >= 2) ++entries;
+            if (j != i && cnt[j] >= 2) ++row_entries;
             cnt[j] = 0;
         }
+        entries += row_entries;
+        row_max = std::max(row_max, row_entries);
         ++sampled;
     }
     const double per_row = sampled ? (double) entries / (double) sampled : 0.0;
+    if (row_stats != nullptr) row_stats[0] = per_row, row_stats[1] = (double) row_max;
     const double est_entries = per_row * (double) R;
     const int64_t per_entry = 2 * (4 + 4 + (int64_t) sizeof(T)) + 4 * (4 + (int64_t) sizeof(T)) + 16;
     const int64_t blk = std::min<int64_t>(inc_total, int64_t(1) << 27);

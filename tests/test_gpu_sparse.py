@@ -449,23 +449,25 @@ def test_expansion_row_join_equals_sort_join(kernel, shape, sim, dtype, monkeypa
     (PLSSVM_MI_EXP_JOIN=sort: every incidence generated, radix-sorted, reduced by key): the same pairs
     (info.pairs) and the same K·p overlap sums — both sum a pair's per-feature products in ascending
     feature order in fp64, so H agrees to the last bit of fp64 before the rounding to the real type.
-    (3000 x 50 @ 40 %: dense-ish rows whose repeats overflow a pass, so passes are split.) "capped": the
-    row join limited to one pass per row (PLSSVM_MI_EXP_RJ_PMAX=1; default 256) — a rank with a row that needs
-    more passes builds its rows by the sort join instead, with the same result."""
+    (3000 x 50 @ 40 %: dense-ish rows whose repeats overflow a pass, so passes are split.) "row" is the
+    one-pass join (H formed in the join kernel, fixed slot ranges per row), "twopass" the count pass + write
+    pass + H kernel (PLSSVM_MI_EXP_RJ=twopass) — the same H arithmetic, so bit for bit the same K·p —
+    "smallcap" the one-pass join with 8 slots per row (PLSSVM_MI_EXP_RJ_CAP=8: rows beyond it are redone by
+    the two passes with the counted sizes), "capped" the row join limited to one pass per row
+    (PLSSVM_MI_EXP_RJ_PMAX=1; default 256) — a rank with a row that needs more passes builds its rows by
+    the sort join instead, with the same result."""
     n, d, k = shape
     csr, _ = datagen.sparse_csr(n, d, k, seed=17, dtype=np.float64)
     m = n - 1
     x = np.random.default_rng(3).uniform(1, 2, m).astype(dtype)
     out = {}
-    for join in ("row", "sort", "capped"):
-        if join == "sort":
-            monkeypatch.setenv("PLSSVM_MI_EXP_JOIN", "sort")
-        else:
-            monkeypatch.delenv("PLSSVM_MI_EXP_JOIN", raising=False)
-        if join == "capped":
-            monkeypatch.setenv("PLSSVM_MI_EXP_RJ_PMAX", "1")
-        else:
-            monkeypatch.delenv("PLSSVM_MI_EXP_RJ_PMAX", raising=False)
+    envs = {"sort": ("PLSSVM_MI_EXP_JOIN", "sort"), "capped": ("PLSSVM_MI_EXP_RJ_PMAX", "1"),
+            "twopass": ("PLSSVM_MI_EXP_RJ", "twopass"), "smallcap": ("PLSSVM_MI_EXP_RJ_CAP", "8")}
+    for join in ("row", "sort", "capped", "twopass", "smallcap"):
+        for k, _ in envs.values():
+            monkeypatch.delenv(k, raising=False)
+        if join in envs:
+            monkeypatch.setenv(*envs[join])
         with sparse_svm(csr, kernel, dtype, sim=sim, algo="expansion") as svm:
             svm.setup_data_on_device()
             info = svm.info()
@@ -473,10 +475,12 @@ def test_expansion_row_join_equals_sort_join(kernel, shape, sim, dtype, monkeypa
             out[join] = (svm.kp_part(x, "overlap"), info["pairs"], info["pair_slots"])
     tol = 1e-14 if dtype == np.float64 else 1e-6
     b = out["sort"][0].astype(np.float64)
-    for join in ("row", "capped"):
+    for join in ("row", "capped", "twopass", "smallcap"):
         assert out[join][1] == out["sort"][1] and out[join][2] == out["sort"][2], join
         a = out[join][0].astype(np.float64)
         assert np.abs(a - b).max() <= tol * max(np.abs(b).max(), 1e-300), (join, np.abs(a - b).max())
+    for join in ("twopass", "smallcap"):
+        np.testing.assert_array_equal(out[join][0], out["row"][0], err_msg=join)
 
 
 @pytest.mark.parametrize("gamma,want_hbytes", [(None, 2), (0.2, 4)])
