@@ -244,13 +244,16 @@ constexpr int RJ_PMAX = 256;   // passes per row at most (more: the rank takes t
 // A halved span grows back (doubles) after every completed range, so one dense cluster of partners does not
 // cut the rest of the row into small passes; a row needing more than RJ_PMAX passes (every pass rescans its
 // incidences) sets *ovf in count mode and the host builds the rank's rows by the sort join instead.
+// Slot mode (off8 == nullptr, sj != nullptr; the default one-pass join): partner k of row r at sj[r cap + k]
+// for k < cap, cnt[r] = the row's count (also beyond cap: *cnt_max lets the host redo such rows by the two
+// passes), no pads — the count pass is not needed.
 __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__restrict__ rowptr,
                                                             const int32_t *__restrict__ col,
                                                             const int64_t *__restrict__ colptr,
                                                             const int32_t *__restrict__ crow, int64_t m, int64_t r0,
                                                             int64_t *__restrict__ cnt, const int64_t *__restrict__ off8,
                                                             int32_t *__restrict__ sj, unsigned int *__restrict__ ovf,
-                                                            int pmax) {
+                                                            int pmax, int64_t cap, unsigned long long *__restrict__ cnt_max) {
     __shared__ uint32_t bm[RJ_BMW];
     __shared__ int32_t rep[RJ_LCAP];
     __shared__ int32_t zcol[RJ_ECAP];
@@ -278,14 +281,14 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
     }
     __syncthreads();
     const int32_t inc = zoff[ne];
-    const bool wr = sj != nullptr;
+    const bool wr = sj != nullptr, slots = wr && off8 == nullptr;
     int64_t written = 0;
     constexpr int64_t SPAN_MAX = (int64_t) RJ_BMW * 32;
     int64_t span = SPAN_MAX;
     int passes = 0;
     for (int64_t R0 = 0; R0 < m;) {
         if (++passes > pmax) {  // uniform
-            if (!wr && tid == 0) {
+            if ((!wr || slots) && tid == 0) {
                 cnt[r] = 0;
                 atomicOr(ovf, 1u);
             }
@@ -350,50 +353,71 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
                 }
             }
             __syncthreads();
-            const int64_t base = off8[r] + written;
-            for (int q = tid; q < U; q += RJ_NT) sj[base + q] = rep[q];
+            if (slots) {
+                const int64_t base = r * cap + written;
+                for (int q = tid; q < U && written + q < cap; q += RJ_NT) sj[base + q] = rep[q];
+            } else {
+                const int64_t base = off8[r] + written;
+                for (int q = tid; q < U; q += RJ_NT) sj[base + q] = rep[q];
+            }
         }
         written += U;
         __syncthreads();  // bm / rep are reused by the next pass
         R0 = R1;
         span = min(span * 2, SPAN_MAX);
     }
-    if (!wr) {
-        if (tid == 0) cnt[r] = written;
+    if (!wr || slots) {
+        if (tid == 0) {
+            cnt[r] = written;
+            if (slots) atomicMax(cnt_max, (unsigned long long) written);
+        }
         return;
     }
     const int64_t b0 = off8[r], b1 = off8[r + 1];
     for (int64_t k = b0 + written + tid; k < b1; k += RJ_NT) sj[k] = -1;  // pads (exp_rowjoin_h_kernel)
 }
 
-// H of the row join's partners (sj from exp_rowjoin_kernel's write pass): one 256-thread workgroup per row
-// i (row i in LDS), one partner per wave at a time: the lanes take row j's entries (coalesced, 64 per step),
-// look each up in row i (binary search), and the matches — ascending features — are summed in that order
-// from a ballot: H_ij = phi(s_ij) - sum_f phi(x_if x_jf) in fp64, rounded to T (the sequential sum of the
-// sort join). The next partner's row bounds are loaded one step ahead. Pads (sj < 0): j = i, H = 0.
-// lower_nz += #(j < i, H != 0 in T).
+// H of the row join's partners (sj from exp_rowjoin_kernel's write / slot pass; row r's entries in
+// [rbeg[r], rend[r])): one 256-thread workgroup per row i, row i's features in an LDS hash (open addressing,
+// <= 1/8 full: one probe per lookup instead of a binary search), one partner per wave at a time: the lanes take
+// row j's entries (coalesced, 64 per step), look each up in row i, and the matches — ascending features — are
+// summed in that order from a ballot: H_ij = phi(s_ij) - sum_f phi(x_if x_jf) in fp64, rounded to T (the
+// sequential sum of the sort join). The next partner's row bounds are loaded one step ahead. Pads (sj < 0):
+// j = i, H = 0. lower_nz += #(j < i, H != 0 in T).
 constexpr int RJH_NT = 256;
+constexpr int RJ_HS = 2048;  // hash slots for row i's features (<= RJ_ECAP keys)
+__device__ __forceinline__ int rj_hash(int32_t f) { return (int) (((uint32_t) f * 2654435761u) >> (32 - 11)); }
 template <typename T>
 __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__restrict__ rowptr,
                                                                const int32_t *__restrict__ col,
                                                                const T *__restrict__ val, int64_t r0, phi_fn phi,
-                                                               double kbase, const int64_t *__restrict__ off8,
+                                                               double kbase, const int64_t *__restrict__ rbeg,
+                                                               const int64_t *__restrict__ rend,
                                                                int32_t *__restrict__ sj, T *__restrict__ sv,
                                                                unsigned long long *__restrict__ lower_nz,
                                                                unsigned long long *__restrict__ ratio_bits) {
-    __shared__ int32_t zcol[RJ_ECAP];
+    __shared__ int32_t hkey[RJ_HS];
+    __shared__ uint8_t hidx[RJ_HS];
     __shared__ T zval[RJ_ECAP];
     __shared__ unsigned long long lnz_s;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t r = blockIdx.x, i = r0 + r;
     const int64_t e0 = rowptr[i];
-    const int ne = (int) (rowptr[i + 1] - e0);
-    for (int e = tid; e < ne; e += RJH_NT) zcol[e] = col[e0 + e], zval[e] = val[e0 + e];
+    const int ne = (int) (rowptr[i + 1] - e0);  // <= RJ_ECAP (host-checked)
+    for (int q = tid; q < RJ_HS; q += RJH_NT) hkey[q] = -1;
     if (tid == 0) lnz_s = 0ull;
+    __syncthreads();
+    for (int e = tid; e < ne; e += RJH_NT) {
+        const int32_t f = col[e0 + e];
+        zval[e] = val[e0 + e];
+        int h = rj_hash(f);
+        while (atomicCAS(&hkey[h], -1, f) != -1) h = (h + 1) & (RJ_HS - 1);  // distinct features: no duplicates
+        hidx[h] = (uint8_t) e;
+    }
     __syncthreads();
     unsigned long long lnz = 0ull;
     double rmax = 0.0;
-    const int64_t q0 = off8[r], q1 = off8[r + 1];
+    const int64_t q0 = rbeg[r], q1 = rend[r];
     constexpr int NW = RJH_NT / 64;
     int64_t q = q0 + wave;
     int64_t jn = q < q1 ? sj[q] : -1, kbn = 0, ken = 0;
@@ -415,16 +439,13 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
             const int64_t k = k0 + lane;
             double a = 0.0, pa = 0.0;
             bool hit = false;
-            if (k < ke && ne > 0) {
+            if (k < ke) {
                 const int32_t f = col[k];
-                int lo = 0, hi = ne - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (zcol[mid] < f) lo = mid + 1;
-                    else hi = mid;
-                }
-                if (zcol[lo] == f) {
-                    a = (double) zval[lo] * (double) val[k];
+                int h = rj_hash(f);
+                int32_t key;
+                while ((key = hkey[h]) >= 0 && key != f) h = (h + 1) & (RJ_HS - 1);
+                if (key == f) {
+                    a = (double) zval[hidx[h]] * (double) val[k];
                     pa = phi(a);
                     hit = true;
                 }
@@ -454,188 +475,7 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
     if (tid == 0 && lnz_s) atomicAdd(lower_nz, lnz_s);
 }
 
-// One-pass row join (default; PLSSVM_MI_EXP_RJ=twopass keeps count pass + write pass + exp_rowjoin_h_kernel):
-// exp_rowjoin_kernel's passes, and after each pass's enumeration the block forms H of that pass's partners
-// at once — one thread per partner, row j's entries merged into row i's features through an LDS hash of
-// them (one probe per entry instead of a binary search), the matches summed in ascending feature order in
-// fp64 (the arithmetic of exp_rowjoin_h_kernel, so the same H bits) — and writes (j, H) into the row's fixed
-// slot range [r cap, r cap + cap) of the pool. cnt[r] = the row's partner count, also beyond cap (the host
-// checks max over rows <= cap, else it redoes the rows by the two-pass join with exact offsets). No count
-// pass, no padded partner list written and read back.
-constexpr int RJ_HS = 2048;  // hash slots for row i's features (<= RJ_ECAP keys: load <= 1/8)
-__device__ __forceinline__ int rj_hash(int32_t f) { return (int) (((uint32_t) f * 2654435761u) >> (32 - 11)); }
-template <typename T>
-__global__ __launch_bounds__(RJ_NT) void exp_rowjoin_fused_kernel(const int64_t *__restrict__ rowptr,
-                                                                  const int32_t *__restrict__ col,
-                                                                  const T *__restrict__ val,
-                                                                  const int64_t *__restrict__ colptr,
-                                                                  const int32_t *__restrict__ crow, int64_t m, int64_t r0,
-                                                                  int64_t cap, phi_fn phi, double kbase,
-                                                                  int32_t *__restrict__ pj, T *__restrict__ ph,
-                                                                  int64_t *__restrict__ cnt, unsigned int *__restrict__ ovf,
-                                                                  int pmax, unsigned long long *__restrict__ lower_nz,
-                                                                  unsigned long long *__restrict__ ratio_bits,
-                                                                  unsigned long long *__restrict__ cnt_max) {
-    __shared__ uint32_t bm[RJ_BMW];
-    __shared__ int32_t rep[RJ_LCAP];
-    __shared__ int32_t zcol[RJ_ECAP];
-    __shared__ T zval[RJ_ECAP];
-    __shared__ int32_t zoff[RJ_ECAP + 1];
-    __shared__ int64_t cst[RJ_ECAP];
-    __shared__ int32_t hkey[RJ_HS];
-    __shared__ uint8_t hidx[RJ_HS];
-    __shared__ int32_t wtot[RJ_NT / 64];
-    __shared__ int nrep_s;
-    __shared__ unsigned long long lnz_s;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t r = blockIdx.x, i = r0 + r;
-    const int64_t e0 = rowptr[i];
-    const int ne = (int) (rowptr[i + 1] - e0);  // <= RJ_ECAP (host-checked)
-    for (int q = tid; q < RJ_HS; q += RJ_NT) hkey[q] = -1;
-    if (tid == 0) lnz_s = 0ull;
-    for (int e = tid; e < ne; e += RJ_NT) {
-        const int32_t f = col[e0 + e];
-        zcol[e] = f;
-        zval[e] = val[e0 + e];
-        cst[e] = colptr[f];
-    }
-    __syncthreads();
-    if (tid == 0) {
-        int32_t a = 0;
-        for (int e = 0; e < ne; ++e) {
-            zoff[e] = a;
-            a += (int32_t) (colptr[zcol[e] + 1] - cst[e]);
-            int h = rj_hash(zcol[e]);
-            while (hkey[h] >= 0) h = (h + 1) & (RJ_HS - 1);  // linear probing, <= 1/8 full
-            hkey[h] = zcol[e];
-            hidx[h] = (uint8_t) e;
-        }
-        zoff[ne] = a;
-    }
-    __syncthreads();
-    const int32_t inc = zoff[ne];
-    const int64_t base = r * cap;
-    int64_t written = 0;
-    unsigned long long lnz = 0ull;
-    double rmax = 0.0;
-    constexpr int64_t SPAN_MAX = (int64_t) RJ_BMW * 32;
-    int64_t span = SPAN_MAX;
-    int passes = 0;
-    for (int64_t R0 = 0; R0 < m;) {
-        if (++passes > pmax) {  // uniform
-            if (tid == 0) {
-                cnt[r] = 0;
-                atomicOr(ovf, 1u);
-            }
-            return;
-        }
-        const int64_t R1 = min(m, R0 + span);
-        for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
-        if (tid == 0) nrep_s = 0;
-        __syncthreads();
-        int e = 0;
-        for (int32_t t = tid; t < inc; t += RJ_NT) {
-            while (zoff[e + 1] <= t) ++e;
-            const int64_t j = crow[cst[e] + (t - zoff[e])];
-            if (j == i || j < R0 || j >= R1) continue;
-            const uint32_t bit = 1u << ((j - R0) & 31);
-            const uint32_t old = atomicOr(&bm[(j - R0) >> 5], bit);
-            if (old & bit) {
-                const int q = atomicAdd(&nrep_s, 1);
-                if (q < RJ_LCAP) rep[q] = (int32_t) j;
-            }
-        }
-        __syncthreads();
-        const int nr = nrep_s;
-        if (nr > RJ_LCAP) {  // uniform: this range again in halves
-            span = (span + 1) / 2;
-            __syncthreads();
-            continue;
-        }
-        for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
-        __syncthreads();
-        for (int q = tid; q < nr; q += RJ_NT) {
-            const int64_t j = rep[q] - R0;
-            atomicOr(&bm[j >> 5], 1u << (j & 31));
-        }
-        __syncthreads();
-        int c = 0;
-#pragma unroll 8
-        for (int w = 0; w < RJ_WPT; ++w) c += __popc(bm[tid * RJ_WPT + w]);
-        int incl = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int v = __shfl_up(incl, o);
-            if (lane >= o) incl += v;
-        }
-        if (lane == 63) wtot[wave] = incl;
-        __syncthreads();
-        int before = 0, U = 0;
-        for (int w = 0; w < RJ_NT / 64; ++w) {
-            const int v = wtot[w];
-            if (w < wave) before += v;
-            U += v;
-        }
-        {
-            int pos = before + incl - c;
-            for (int w = 0; w < RJ_WPT; ++w) {
-                uint32_t word = bm[tid * RJ_WPT + w];
-                while (word) {
-                    const int b = __ffs(word) - 1;
-                    word &= word - 1;
-                    rep[pos++] = (int32_t) (R0 + (int64_t) (tid * RJ_WPT + w) * 32 + b);
-                }
-            }
-        }
-        __syncthreads();
-        // H of this pass's partners (ascending in rep): thread q merges row j into row i's features
-        for (int q = tid; q < U; q += RJ_NT) {
-            const int64_t j = rep[q];
-            const int64_t kb = rowptr[j], ke = rowptr[j + 1];
-            double sd = 0.0, sphi = 0.0;
-            int32_t fn = kb < ke ? col[kb] : 0;
-            T vn = kb < ke ? val[kb] : T(0);
-            for (int64_t k = kb; k < ke; ++k) {
-                const int32_t f = fn;
-                const T v = vn;
-                if (k + 1 < ke) fn = col[k + 1], vn = val[k + 1];  // the next entry in flight
-                int h = rj_hash(f);
-                int32_t key;
-                while ((key = hkey[h]) >= 0 && key != f) h = (h + 1) & (RJ_HS - 1);
-                if (key == f) {
-                    const double a = (double) zval[hidx[h]] * (double) v;
-                    sd += a;
-                    sphi += phi(a);
-                }
-            }
-            const double ps = phi(sd);
-            const T hv = (T) (ps - sphi);
-            const double kv = fabs(kbase + ps);
-            const double ratio = hv == T(0) ? 0.0 : (kv > 0.0 ? fabs((double) hv) / kv : 1e300);
-            rmax = fmax(rmax, ratio);
-            if (j < i && hv != T(0)) ++lnz;
-            const int64_t pos = written + q;
-            if (pos < cap) {
-                pj[base + pos] = (int32_t) j;
-                ph[base + pos] = hv;
-            }
-        }
-        written += U;
-        __syncthreads();  // bm / rep are reused by the next pass
-        R0 = R1;
-        span = min(span * 2, SPAN_MAX);
-    }
-    if (lnz) atomicAdd(&lnz_s, lnz);
-    if (rmax > 0.0) atomicMax(ratio_bits, (unsigned long long) __double_as_longlong(rmax));  // >= 0: bit order
-    __syncthreads();
-    if (tid == 0) {
-        cnt[r] = written;
-        if (lnz_s) atomicAdd(lower_nz, lnz_s);
-        atomicMax(cnt_max, (unsigned long long) written);
-    }
-}
-
-// the fused join's row ranges: beg[r] = r cap, end[r] = r cap + cnt[r] (every count <= cap, host-checked)
+// the one-pass join's row ranges: beg[r] = r cap, end[r] = r cap + cnt[r] (every count <= cap, host-checked)
 __global__ __launch_bounds__(256) void exp_pool_range_kernel(const int64_t *__restrict__ cnt, int64_t R, int64_t cap,
                                                              int64_t *__restrict__ beg, int64_t *__restrict__ end) {
     const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
@@ -1862,9 +1702,19 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
         std::memcpy(&rm, &np[1], sizeof(rm));
         ex.hratio = rm;
     };
-    // one-pass join (exp_rowjoin_fused_kernel) into fixed per-row slot ranges of cap entries, cap from the setup's
-    // sample of the rank's rows (estimate_expansion_bytes); PLSSVM_MI_EXP_RJ=twopass keeps the two-pass join
-    bool have_cnt = false;  // cnt[] holds every row's exact partner count (a fused pass whose cap was too small)
+    // one pass of the join into fixed per-row slot ranges of cap partners (exp_rowjoin_kernel's slot mode, no
+    // count pass), cap from the setup's sample of the rank's rows (estimate_expansion_bytes); a row beyond its
+    // slots: the two passes with the counts this pass took. PLSSVM_MI_EXP_RJ=twopass: count pass + write pass.
+    bool have_cnt = false;  // cnt[] holds every row's exact partner count (a slot pass whose cap was too small)
+    auto h_pass = [&]() {  // H of every listed partner, then the pairs count and the H bound
+        if (R > 0) {
+            hipLaunchKernelGGL(exp_rowjoin_h_kernel<T>, dim3((unsigned) R), dim3(RJH_NT), 0, stream, csr.rowptr.get(),
+                               csr.col.get(), csr.val.get(), r0, phi, kbase, rbeg, rend, sj.get(), sv.get(), lnz.get(),
+                               lnz.get() + 1);
+            MI_LAUNCH_CHECK();
+        }
+        read_lnz();
+    };
     if (row_join && R > 0) {
         const char *rj = std::getenv("PLSSVM_MI_EXP_RJ");
         const bool want = !(rj != nullptr && std::strcmp(rj, "twopass") == 0);
@@ -1878,14 +1728,13 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
         const double pool_b = (double) R * (double) cap * (double) (4 + sizeof(T));
         if (want && ex.rj_mean > 0.0 && pool_b <= 0.4 * (double) free_b) {
             sj.alloc(R * cap, stream, false);
-            sv.alloc(R * cap, stream, false);
             cnt.alloc(R, stream);
             lnz.alloc(3, stream);  // [0] lower pairs with H != 0, [1] max |H| / kernel value (double bits), [2] max count
             dev_buf<unsigned int> ovf;
             ovf.alloc(1, stream);
-            hipLaunchKernelGGL(exp_rowjoin_fused_kernel<T>, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
-                               csr.col.get(), csr.val.get(), csr.colptr.get(), csr.crow.get(), m, r0, cap, phi, kbase,
-                               sj.get(), sv.get(), cnt.get(), ovf.get(), rj_pmax, lnz.get(), lnz.get() + 1, lnz.get() + 2);
+            hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
+                               csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(), (const int64_t *) nullptr,
+                               sj.get(), ovf.get(), rj_pmax, cap, lnz.get() + 2);
             MI_LAUNCH_CHECK();
             unsigned long long cmax = 0ull;
             MI_HIP_CHECK(hipMemcpyAsync(&ovf_h, ovf.get(), sizeof(ovf_h), hipMemcpyDeviceToHost, stream));
@@ -1893,13 +1742,13 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             MI_HIP_CHECK(hipStreamSynchronize(stream));
             pt.mark("expansion: row join (one pass)");
             if (ovf_h != 0u) {  // a row whose partner clusters need more than RJ_PMAX passes: the sort join
-                sj.reset(), sv.reset(), cnt.reset();
+                sj.reset(), cnt.reset();
                 row_join = false;
             } else if ((int64_t) cmax > cap) {  // a row beyond its slots: the two-pass join with these exact counts
-                sj.reset(), sv.reset();
+                sj.reset();
                 have_cnt = true;
             } else {
-                read_lnz();
+                sv.alloc(R * cap, stream, false);
                 pbeg.alloc(R, stream, false);
                 pend.alloc(R, stream, false);
                 hipLaunchKernelGGL(exp_pool_range_kernel, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream, cnt.get(),
@@ -1907,11 +1756,13 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
                 MI_LAUNCH_CHECK();
                 rbeg = pbeg.get();
                 rend = pend.get();
+                h_pass();
+                pt.mark("expansion: row join (H)");
             }
         }
     }
     if (row_join && rbeg == nullptr) {
-        // two passes: count (unless the fused pass counted), padded offsets, then the write pass and H
+        // two passes: count (unless the slot pass counted), padded offsets, then the write pass and H
         off8.alloc(R + 1, stream);
         if (!have_cnt) cnt.alloc(std::max<int64_t>(R, 1), stream);
         cnt8.alloc(R + 1, stream);
@@ -1921,7 +1772,8 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
         if (R > 0 && !have_cnt) {
             hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
                                csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(),
-                               (const int64_t *) nullptr, (int32_t *) nullptr, ovf.get(), rj_pmax);
+                               (const int64_t *) nullptr, (int32_t *) nullptr, ovf.get(), rj_pmax, (int64_t) 0,
+                               (unsigned long long *) nullptr);
             MI_LAUNCH_CHECK();
         }
         if (R > 0) {
@@ -1949,16 +1801,12 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             if (R > 0) {
                 hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
                                    csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(), off8.get(), sj.get(),
-                                   (unsigned int *) nullptr, rj_pmax);
-                MI_LAUNCH_CHECK();
-                hipLaunchKernelGGL(exp_rowjoin_h_kernel<T>, dim3((unsigned) R), dim3(RJH_NT), 0, stream, csr.rowptr.get(),
-                                   csr.col.get(), csr.val.get(), r0, phi, kbase, off8.get(), sj.get(), sv.get(), lnz.get(),
-                                   lnz.get() + 1);
+                                   (unsigned int *) nullptr, rj_pmax, (int64_t) 0, (unsigned long long *) nullptr);
                 MI_LAUNCH_CHECK();
             }
-            read_lnz();
             rbeg = off8.get();
             rend = off8.get() + 1;
+            h_pass();
             pt.mark("expansion: row join (rows)");
         }
     }

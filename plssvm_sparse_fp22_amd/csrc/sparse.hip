@@ -556,13 +556,23 @@ template <typename T>
 void host_check_csr(const int64_t *rowptr, const int32_t *col, int64_t n, int64_t d) {
     if (!rowptr || !col || n < 1 || d < 1) throw mi_error(-1, "Data set is empty!");
     if (rowptr[0] != 0) throw mi_error(-1, "CSR rowptr[0] must be 0");
-    for (int64_t i = 0; i < n; ++i) {
-        if (rowptr[i + 1] < rowptr[i]) throw mi_error(-1, "CSR rowptr must be non-decreasing");
-        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-            if (col[k] < 0 || col[k] >= d) throw mi_error(-1, "CSR column index out of range");
-            if (k > rowptr[i] && col[k] <= col[k - 1]) throw mi_error(-1, "CSR columns must be strictly ascending");
+    // the first failure in row order, as a sequential scan would find it: the rows before the first decreasing
+    // rowptr are checked on the host threads (each thread's first error is its lowest row's, and host_parallel
+    // rethrows the lowest thread's), then the rowptr error itself
+    int64_t ibad = n;
+    for (int64_t i = 0; i < n; ++i)
+        if (rowptr[i + 1] < rowptr[i]) {
+            ibad = i;
+            break;
         }
-    }
+    host_parallel(ibad, [&](int, int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i)
+            for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+                if (col[k] < 0 || col[k] >= d) throw mi_error(-1, "CSR column index out of range");
+                if (k > rowptr[i] && col[k] <= col[k - 1]) throw mi_error(-1, "CSR columns must be strictly ascending");
+            }
+    });
+    if (ibad < n) throw mi_error(-1, "CSR rowptr must be non-decreasing");
 }
 
 }  // namespace

@@ -450,8 +450,9 @@ def test_expansion_row_join_equals_sort_join(kernel, shape, sim, dtype, monkeypa
     (info.pairs) and the same K·p overlap sums — both sum a pair's per-feature products in ascending
     feature order in fp64, so H agrees to the last bit of fp64 before the rounding to the real type.
     (3000 x 50 @ 40 %: dense-ish rows whose repeats overflow a pass, so passes are split.) "row" is the
-    one-pass join (H formed in the join kernel, fixed slot ranges per row), "twopass" the count pass + write
-    pass + H kernel (PLSSVM_MI_EXP_RJ=twopass) — the same H arithmetic, so bit for bit the same K·p —
+    one-pass join (partners written into fixed slot ranges per row, no count pass), "twopass" the count pass
+    + write pass (PLSSVM_MI_EXP_RJ=twopass) — the same H kernel over the same partners, so bit for bit the same
+    K·p —
     "smallcap" the one-pass join with 8 slots per row (PLSSVM_MI_EXP_RJ_CAP=8: rows beyond it are redone by
     the two passes with the counted sizes), "capped" the row join limited to one pass per row
     (PLSSVM_MI_EXP_RJ_PMAX=1; default 256) — a rank with a row that needs more passes builds its rows by
