@@ -259,6 +259,8 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
     __shared__ int32_t zcol[RJ_ECAP];
     __shared__ int32_t zoff[RJ_ECAP + 1];
     __shared__ int64_t cst[RJ_ECAP];
+    __shared__ int64_t pst[RJ_ECAP];    // a partial pass: each column's first entry with a row in [R0, R1)
+    __shared__ int32_t pzoff[RJ_ECAP + 1];
     __shared__ int32_t wtot[RJ_NT / 64];
     __shared__ int nrep_s;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -280,7 +282,6 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
         zoff[ne] = a;
     }
     __syncthreads();
-    const int32_t inc = zoff[ne];
     const bool wr = sj != nullptr, slots = wr && off8 == nullptr;
     int64_t written = 0;
     constexpr int64_t SPAN_MAX = (int64_t) RJ_BMW * 32;
@@ -297,11 +298,41 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
         const int64_t R1 = min(m, R0 + span);
         for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
         if (tid == 0) nrep_s = 0;
+        // a pass over part of the partner rows reads only that part of each column (rows ascend within a
+        // column: two binary searches per feature), not every incidence of the row once per pass
+        const bool whole = R0 == 0 && R1 >= m;
+        if (!whole) {
+            for (int e = tid; e < ne; e += RJ_NT) {
+                const int64_t a = cst[e], b = a + (zoff[e + 1] - zoff[e]);
+                int64_t lo = a, hi = b;
+                while (lo < hi) {  // first row >= R0
+                    const int64_t mid = (lo + hi) >> 1;
+                    if (crow[mid] < R0) lo = mid + 1;
+                    else hi = mid;
+                }
+                int64_t lo2 = lo, hi2 = b;
+                while (lo2 < hi2) {  // first row >= R1
+                    const int64_t mid = (lo2 + hi2) >> 1;
+                    if (crow[mid] < R1) lo2 = mid + 1;
+                    else hi2 = mid;
+                }
+                pst[e] = lo;
+                pzoff[e + 1] = (int32_t) (lo2 - lo);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                pzoff[0] = 0;
+                for (int e = 0; e < ne; ++e) pzoff[e + 1] += pzoff[e];
+            }
+        }
         __syncthreads();
+        const int64_t *S = whole ? cst : pst;
+        const int32_t *Z = whole ? zoff : pzoff;
+        const int32_t pinc = Z[ne];
         int e = 0;
-        for (int32_t t = tid; t < inc; t += RJ_NT) {
-            while (zoff[e + 1] <= t) ++e;
-            const int64_t j = crow[cst[e] + (t - zoff[e])];
+        for (int32_t t = tid; t < pinc; t += RJ_NT) {
+            while (Z[e + 1] <= t) ++e;
+            const int64_t j = crow[S[e] + (t - Z[e])];
             if (j == i || j < R0 || j >= R1) continue;
             const uint32_t bit = 1u << ((j - R0) & 31);
             const uint32_t old = atomicOr(&bm[(j - R0) >> 5], bit);

@@ -32,14 +32,14 @@ CASES = {
     "rbf_f64_expansion": ("rbf", np.float64, 0.05, 0.0, False, "expansion", {}, {"exp_hbytes": 8}),
     "poly_f64_expansion": ("polynomial", np.float64, 0.05, 1.0, False, "expansion", {}, {"exp_hbytes": 8}),
     # kernel expansion in fp32 with bfloat16 H + flagged chunks (the layout of the 3-RBF / config-5 bench lines;
-    # gamma small enough for the 2^-16 bound — |x| <= 1: |H| <= (2 gamma)^2 = 4e-6; the flags forced: few windows
-    # leave many empty cells here)
-    "rbf_f32_bf16_flags": ("rbf", np.float32, 0.001, 0.0, False, "expansion", {"PLSSVM_MI_EXP_ROWS": "flags"},
+    # gamma small enough for the 2^-16 bound — up to ~6 shared features of |x| <= 1: max |H| / k = 6.6e-6 here;
+    # the flags forced: few windows leave many empty cells here)
+    "rbf_f32_bf16_flags": ("rbf", np.float32, 0.0005, 0.0, False, "expansion", {"PLSSVM_MI_EXP_ROWS": "flags"},
                            {"exp_hbytes": 2, "exp_layout": 2}),
-    "rbf_fp22_bf16_flags": ("rbf", np.float32, 0.001, 0.0, True, "expansion", {"PLSSVM_MI_EXP_ROWS": "flags"},
+    "rbf_fp22_bf16_flags": ("rbf", np.float32, 0.0005, 0.0, True, "expansion", {"PLSSVM_MI_EXP_ROWS": "flags"},
                             {"exp_hbytes": 2, "exp_layout": 2}),
     # the real-H fp32 layout (bound forced off)
-    "rbf_f32_realh": ("rbf", np.float32, 0.001, 0.0, False, "expansion", {"PLSSVM_MI_EXP_HFMT": "full"},
+    "rbf_f32_realh": ("rbf", np.float32, 0.0005, 0.0, False, "expansion", {"PLSSVM_MI_EXP_HFMT": "full"},
                       {"exp_hbytes": 4}),
     # the unstored paths
     "rbf_f64_onthefly": ("rbf", np.float64, 0.05, 0.0, False, "onthefly", {}, {}),
