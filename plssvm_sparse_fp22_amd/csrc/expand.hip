@@ -227,8 +227,14 @@ __global__ __launch_bounds__(256) void exp_iota_kernel(uint32_t *__restrict__ v,
 
 // ---- row join: the remainder's symmetric rows built per row (default; PLSSVM_MI_EXP_JOIN=sort keeps the
 // column-join sort below) ------------------------------------------------------------------------------
-constexpr int RJ_NT = 1024;
-constexpr int RJ_BMW = 32768;  // bitmap words: 1 048 576 partner rows per pass (128 KiB of LDS)
+#ifndef RJ_NT_OPT
+#define RJ_NT_OPT 1024
+#endif
+#ifndef RJ_BMW_OPT
+#define RJ_BMW_OPT 32768
+#endif
+constexpr int RJ_NT = RJ_NT_OPT;
+constexpr int RJ_BMW = RJ_BMW_OPT;  // bitmap words: 1 048 576 partner rows per pass (128 KiB of LDS)
 constexpr int RJ_LCAP = 2048;  // repeat sightings held per pass (more: the pass range is halved)
 constexpr int RJ_ECAP = 256;   // entries of row i held in LDS (longer rows: the sort join)
 constexpr int RJ_WPT = RJ_BMW / RJ_NT;
@@ -594,26 +600,63 @@ __device__ __forceinline__ int64_t exp_cidx(int64_t r, int64_t W, int64_t nW, in
     return ((I * EXP_NWV + v) * nW + W) * RPW + rr;
 }
 
+// The cell kernels below walk one row per wave: a row's entries (sorted by j; H == 0 entries — pads, or a
+// remainder that rounded to 0 — skipped) are read 64 at a time, coalesced (one row per thread read a row's
+// range serially: uncoalesced, 3-4x slower at setup). The valid entries of a step form runs of equal windows
+// (j ascending); per run: on_open(prev window, window) when a window starts (wave-uniform), on_entry for each
+// of its entries with its rank k among the row's valid entries of that window (lane-parallel), and
+// on_close(window, count) when the window's last entry has been seen (wave-uniform). Same order, same values
+// as the sequential walk.
+template <typename T, typename FO, typename FE, typename FC>
+__device__ __forceinline__ void exp_row_windows(const int32_t *__restrict__ sj, const T *__restrict__ sv, int64_t b,
+                                                int64_t e, int64_t CW, FO on_open, FE on_entry, FC on_close) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    int curW = -1;
+    int64_t kcur = 0;
+    for (int64_t s0 = b; s0 < e; s0 += 64) {
+        const int64_t s = s0 + lane;
+        bool valid = false;
+        int W = 0;
+        int32_t jj = 0;
+        T h = T(0);
+        if (s < e) {
+            h = sv[s];
+            jj = sj[s];
+            valid = h != T(0);
+            W = valid ? (int) (jj / CW) : 0;
+        }
+        uint64_t rem = __ballot(valid);
+        while (rem) {  // wave-uniform: one run of equal windows at a time
+            const int W0 = __shfl(W, __ffsll((long long) rem) - 1);
+            const uint64_t m0 = __ballot(valid && W == W0) & rem;
+            if (W0 != curW) {
+                if (curW >= 0) on_close(curW, kcur);
+                on_open(curW, W0);
+                curW = W0;
+                kcur = 0;
+            }
+            if ((m0 >> lane) & 1ull) on_entry(jj, h, W0, kcur + __popcll(m0 & below));
+            kcur += __popcll(m0);
+            rem &= ~m0;
+        }
+    }
+    if (curW >= 0) on_close(curW, kcur);
+}
+
 // per row r (rank-local), window W: count of its non-zero entries with j in W, rounded up to 4 slots
 template <typename T>
 __global__ __launch_bounds__(256) void exp_cell_count_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
                                                              const int32_t *__restrict__ sj, const T *__restrict__ sv,
                                                              int64_t R, int64_t nW, int64_t CW, int64_t RB,
                                                              int64_t *__restrict__ cnt) {
-    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= R) return;
-    int64_t Wc = -1, k = 0;
-    for (int64_t s = rbeg[r]; s < rend[r]; ++s) {  // entries sorted by j
-        if (sv[s] == T(0)) continue;                    // pads (and no stored H is exactly 0)
-        const int64_t W = sj[s] / CW;
-        if (W != Wc) {
-            if (Wc >= 0) cnt[exp_cidx(r, Wc, nW, RB)] = (k + 3) & ~int64_t(3);
-            Wc = W;
-            k = 0;
-        }
-        ++k;
-    }
-    if (Wc >= 0) cnt[exp_cidx(r, Wc, nW, RB)] = (k + 3) & ~int64_t(3);
+    const int lane = threadIdx.x & 63;
+    exp_row_windows<T>(sj, sv, rbeg[r], rend[r], CW, [](int, int) {}, [](int32_t, T, int, int64_t) {},
+                       [&](int W, int64_t k) {
+                           if (lane == 0) cnt[exp_cidx(r, W, nW, RB)] = (k + 3) & ~int64_t(3);
+                       });
 }
 
 // bfloat16 of a float, round to nearest even (finite values)
@@ -686,29 +729,20 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__
                                                                const int64_t *__restrict__ coff,
                                                                uint16_t *__restrict__ hjl, T *__restrict__ hv,
                                                                uint16_t *__restrict__ hv16, uint16_t *__restrict__ hrow) {
-    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= R) return;
+    const int lane = threadIdx.x & 63;
     const uint16_t rl = (uint16_t) (r % RB);
-    int64_t Wc = -1, base = 0, k = 0;
-    auto close = [&]() {
-        for (int64_t q = 0; q < ((k + 3) >> 2); ++q) hrow[(base >> 2) + q] = rl;
-    };
-    for (int64_t s = rbeg[r]; s < rend[r]; ++s) {
-        const T h = sv[s];
-        if (h == T(0)) continue;
-        const int64_t W = sj[s] / CW;
-        if (W != Wc) {
-            if (Wc >= 0) close();
-            Wc = W;
-            base = coff[exp_cidx(r, W, nW, RB)];
-            k = 0;
-        }
-        hjl[base + k] = (uint16_t) (sj[s] - W * CW);
-        if (hv16 != nullptr) hv16[base + k] = bf16_rne((float) h);
-        else hv[base + k] = h;
-        ++k;
-    }
-    if (Wc >= 0) close();
+    int64_t base = 0;
+    exp_row_windows<T>(sj, sv, rbeg[r], rend[r], CW, [&](int, int W) { base = coff[exp_cidx(r, W, nW, RB)]; },
+                       [&](int32_t j, T h, int W, int64_t k) {
+                           hjl[base + k] = (uint16_t) (j - (int64_t) W * CW);
+                           if (hv16 != nullptr) hv16[base + k] = bf16_rne((float) h);
+                           else hv[base + k] = h;
+                       },
+                       [&](int, int64_t k) {
+                           for (int64_t q = lane; q < ((k + 3) >> 2); q += 64) hrow[(base >> 2) + q] = rl;
+                       });
 }
 
 // ---- flagged chunks (hbf16 layouts): no per-chunk row index ------------------------------------------------
@@ -721,28 +755,22 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_kernel(const int64_t *__
 // stats[0] += windows without entries (the dummies the layout would add), stats[1] |= 1 when a stored H's
 // bfloat16 has bit 14 set (|H| >= 2: the bit is not free)
 template <typename T>
-__global__ __launch_bounds__(256) void exp_cell_stats_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend, const int32_t *__restrict__ sj,
-                                                             const T *__restrict__ sv, int64_t R, int64_t nW, int64_t CW,
+__global__ __launch_bounds__(256) void exp_cell_stats_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
+                                                             const int32_t *__restrict__ sj, const T *__restrict__ sv,
+                                                             int64_t R, int64_t nW, int64_t CW,
                                                              unsigned long long *__restrict__ stats) {
-    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned long long empty = 0, big = 0;
-    if (r < R) {
-        int64_t Wc = -1, nwin = 0;
-        for (int64_t s = rbeg[r]; s < rend[r]; ++s) {
-            if (sv[s] == T(0)) continue;
-            const int64_t W = sj[s] / CW;
-            if (W != Wc) Wc = W, ++nwin;
-            if (bf16_rne((float) sv[s]) & 0x4000u) big = 1;
-        }
-        empty = (unsigned long long) (nW - nwin);
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        empty += __shfl_xor(empty, o);
-        big |= __shfl_xor(big, o);
-    }
+    const int64_t r = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    int64_t nwin = 0;
+    unsigned long long big = 0;
+    exp_row_windows<T>(sj, sv, rbeg[r], rend[r], CW, [&](int, int) { ++nwin; },
+                       [&](int32_t, T h, int, int64_t) {
+                           if (bf16_rne((float) h) & 0x4000u) big = 1;
+                       },
+                       [](int, int64_t) {});
+    big = __ballot(big != 0) ? 1ull : 0ull;
     if ((threadIdx.x & 63) == 0) {
-        if (empty) atomicAdd(stats, empty);
+        if (nW - nwin) atomicAdd(stats, (unsigned long long) (nW - nwin));
         if (big) atomicOr(stats + 1, big);
     }
 }
@@ -764,30 +792,33 @@ __device__ __forceinline__ int64_t exp_jh_j(int64_t t) { return EXP_JH ? ((t & ~
 __device__ __forceinline__ int64_t exp_jh_h(int64_t t) { return EXP_JH ? ((t & ~int64_t(3)) << 1) + 4 + (t & 3) : t; }
 
 // exp_cell_scatter_kernel for the flagged layout (bfloat16 H, buffers zeroed): every window of the row in
-// order, its entries (or a dummy), bit 14 set on the cell's first H
+// order, its entries with bit 14 set on the cell's first H, or a dummy (j = 0, H = 0 with the bit) for a window
+// without entries
 template <typename T>
 __global__ __launch_bounds__(256) void exp_cell_scatter_flag_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
                                                                     const int32_t *__restrict__ sj, const T *__restrict__ sv,
                                                                     int64_t R, int64_t nW, int64_t CW, int64_t RB,
                                                                     const int64_t *__restrict__ coff,
                                                                     uint16_t *__restrict__ hjl, uint16_t *__restrict__ hv16) {
-    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= R) return;
-    int64_t s = rbeg[r];
-    const int64_t se = rend[r];
-    for (int64_t W = 0; W < nW; ++W) {
-        const int64_t base = coff[exp_cidx(r, W, nW, RB)];
-        int64_t k = 0;
-        for (; s < se; ++s) {  // entries sorted by j: this window's, then stop at the next window's first
-            const T h = sv[s];
-            if (h == T(0)) continue;  // pads
-            if (sj[s] / CW != W) break;
-            hjl[exp_jh_j(base + k)] = (uint16_t) (sj[s] - W * CW);
-            hv16[exp_jh_h(base + k)] = bf16_rne((float) h);
-            ++k;
-        }
-        hv16[exp_jh_h(base)] |= (uint16_t) 0x4000u;  // k == 0: the dummy (j = 0, H = 0)
-    }
+    const int lane = threadIdx.x & 63;
+    auto dummies = [&](int64_t w0, int64_t w1) {  // windows [w0, w1) without entries
+        for (int64_t w = w0 + lane; w < w1; w += 64) hv16[exp_jh_h(coff[exp_cidx(r, w, nW, RB)])] = (uint16_t) 0x4000u;
+    };
+    int64_t base = 0, last = -1;
+    exp_row_windows<T>(sj, sv, rbeg[r], rend[r], CW,
+                       [&](int prev, int W) {
+                           dummies(prev + 1, W);
+                           base = coff[exp_cidx(r, W, nW, RB)];
+                           last = W;
+                       },
+                       [&](int32_t j, T h, int W, int64_t k) {
+                           hjl[exp_jh_j(base + k)] = (uint16_t) (j - (int64_t) W * CW);
+                           hv16[exp_jh_h(base + k)] = (uint16_t) (bf16_rne((float) h) | (k == 0 ? 0x4000u : 0u));
+                       },
+                       [](int, int64_t) {});
+    dummies(last + 1, nW);
 }
 
 // ---- run layout (option, PLSSVM_MI_EXP_RUNS): no padding, no per-chunk row index --------------------
@@ -1988,7 +2019,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             cnt.alloc(ncnt + 1, stream);
             coff.alloc(ncnt + 1, stream, false);
             if (R > 0) {
-                hipLaunchKernelGGL(exp_cell_count_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                hipLaunchKernelGGL(exp_cell_count_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream,
                                    rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, RB, cnt.get());
                 MI_LAUNCH_CHECK();
             }
@@ -2002,7 +2033,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
                 if (ropt >= 0) {
                     dev_buf<unsigned long long> st;
                     st.alloc(2, stream);
-                    hipLaunchKernelGGL(exp_cell_stats_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                    hipLaunchKernelGGL(exp_cell_stats_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream,
                                        rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, st.get());
                     MI_LAUNCH_CHECK();
                     unsigned long long hs2[2] = { 0ull, 0ull };
@@ -2028,14 +2059,14 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             else ex.hv.alloc(std::max<int64_t>(ex.slots, 4), stream);
             if (ex.rflags) {
                 ex.hrow.reset();
-                hipLaunchKernelGGL(exp_cell_scatter_flag_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                hipLaunchKernelGGL(exp_cell_scatter_flag_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream,
                                    rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
                                    EXP_JH ? ex.hjl.get() : ex.hv16.get());
                 MI_LAUNCH_CHECK();
             } else {
                 ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
                 if (R > 0) {
-                    hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
+                    hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream,
                                        rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
                                        ex.hv.get(), ex.hv16.get(), ex.hrow.get());
                     MI_LAUNCH_CHECK();

@@ -2,7 +2,8 @@
 against the oracle, across the explicit-residual iteration (run % 50 == 49, OpenMP/csvm.cpp:119-132).
 
 One seeded CSR set (1200 points x 300 features, 20 per row: most pairs share a feature, many share
-several, so the kernel expansion's stored remainder H carries real weight), C = 10, imax = 60 and
+several, so the kernel expansion's stored remainder H carries real weight), C = 10 (1000 for the fp32 rbf
+cases, COST_CASE), imax = 60 and
 eps = 1e-12 — below every fp32/fp64 CG's rounding floor, so every run (the reference's, the oracle's,
 the HIP path's) takes exactly imax iterations and crosses the reset. Test infrastructure only (shared by
 tests/golden/make_cg_trace_vectors.py and tests/test_gpu_cg_trace.py).
@@ -19,9 +20,12 @@ VECTORS = os.path.join(ROOT, "tests", "golden", "cg_traces")
 
 N, D, K, SEED = 1200, 300, 20, 8
 COST, IMAX, EPS = 10.0, 60, 1e-12
-# the fp32 rbf runs' recursive residual reaches eps^2 delta_0 = 1e-24 delta_0 after ~34 iterations: eps = 1e-30
-# (eps^2 underflows to 0 in fp32: no stop) makes them cross the reset too
+# the fp32 rbf cases (gamma 5e-4 for the bfloat16 bound: a nearly constant kernel) are too well conditioned at
+# C = 10 — their recursive residual reaches 0 in fp32 after ~35-48 iterations. At C = 1000 their CG still moves
+# after 60 iterations (delta / delta0 ~ 1e-12 at the reset), and eps = 1e-30 (eps^2 underflows to 0 in fp32:
+# no stop) makes every run take exactly imax iterations across the reset.
 EPS_CASE = {"rbf_f32_bf16_flags": 1e-30, "rbf_fp22_bf16_flags": 1e-30, "rbf_f32_realh": 1e-30}
+COST_CASE = {"rbf_f32_bf16_flags": 1000.0, "rbf_fp22_bf16_flags": 1000.0, "rbf_f32_realh": 1000.0}
 
 # name: kernel, real type, gamma, coef0, FP22 input, sparse algorithm, environment of the HIP run, layout checks
 CASES = {
@@ -62,7 +66,7 @@ def build(name):
     dt = np.dtype(dtype).type
     g = dt(1.0) / dt(d) if gamma is None else dt(gamma)
     return dict(csr=(rowptr, col, val.astype(dtype), n, d), fp22=words, y=y.astype(dtype), gamma=g, coef0=dt(coef0),
-                kernel=kernel, dtype=dtype, eps=EPS_CASE.get(name, EPS))
+                kernel=kernel, dtype=dtype, eps=EPS_CASE.get(name, EPS), cost=COST_CASE.get(name, COST))
 
 
 def input_hash(s):
@@ -91,8 +95,8 @@ def q_explicit(s, with_abs=False):
         nrm = np.diag(G)
         Kf = np.exp(-g * (nrm[:, None] + nrm[None, :] - 2 * G))
     m = n - 1
-    eye = np.eye(m, dtype=np.longdouble) / np.longdouble(COST)
-    qa = Kf[m, m] + np.longdouble(1.0 / COST)
+    eye = np.eye(m, dtype=np.longdouble) / np.longdouble(s["cost"])
+    qa = Kf[m, m] + np.longdouble(1.0 / s["cost"])
     Q = Kf[:m, :m] + qa - Kf[:m, m][:, None] - Kf[:m, m][None, :] + eye
     if not with_abs:
         return Q

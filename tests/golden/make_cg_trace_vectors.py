@@ -28,7 +28,7 @@ def oracle_learn(s, dtype, nthreads):
     rowptr, col, val, n, d = s["csr"]
     data = pyoracle.Data(rowptr=rowptr, col=col, val=val.astype(dtype), n=n, d=d, dtype=dtype)
     dt = np.dtype(dtype).type
-    return pyoracle.learn(s["kernel"], data, s["y"].astype(dtype), cost=cc.COST, eps=s["eps"], imax=cc.IMAX, degree=3,
+    return pyoracle.learn(s["kernel"], data, s["y"].astype(dtype), cost=s["cost"], eps=s["eps"], imax=cc.IMAX, degree=3,
                           gamma=dt(s["gamma"]), coef0=dt(s["coef0"]), nthreads=nthreads)
 
 
@@ -43,7 +43,7 @@ def vectors(name):
     if dtype == np.float32:
         r64 = oracle_learn(s, np.float64, 1)
         arrays.update(trace64=r64["trace"], alpha64=r64["alpha"], bias64=np.array([r64["bias"]], np.float64))
-    meta = dict(kernel=s["kernel"], dtype=np.dtype(dtype).name, n=cc.N, d=cc.D, cost=cc.COST, eps=s["eps"],
+    meta = dict(kernel=s["kernel"], dtype=np.dtype(dtype).name, n=cc.N, d=cc.D, cost=s["cost"], eps=s["eps"],
                 imax=cc.IMAX, gamma=float(s["gamma"]), coef0=float(s["coef0"]), fp22=s["fp22"] is not None,
                 input_sha256=cc.input_hash(s), iters=int(r1["iters"]))
     return arrays, meta

@@ -42,7 +42,7 @@ def make_svm(s, name, monkeypatch):
     kernel, dtype, _, _, fp22, algo, env, _ = cc.CASES[name]
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    p = pm.Parameter(kernel, degree=3, gamma=float(s["gamma"]), coef0=float(s["coef0"]), cost=cc.COST,
+    p = pm.Parameter(kernel, degree=3, gamma=float(s["gamma"]), coef0=float(s["coef0"]), cost=s["cost"],
                      epsilon=s["eps"], real_type=dtype)
     rowptr, col, val, n, d = s["csr"]
     if fp22:
