@@ -238,6 +238,9 @@ constexpr int RJ_BMW = RJ_BMW_OPT;  // bitmap words: 1 048 576 partner rows per 
 constexpr int RJ_LCAP = 2048;  // repeat sightings held per pass (more: the pass range is halved)
 constexpr int RJ_ECAP = 256;   // entries of row i held in LDS (longer rows: the sort join)
 constexpr int RJ_WPT = RJ_BMW / RJ_NT;
+#ifndef RJ_U
+#define RJ_U 4  // incidence reads in flight per thread in the join's walk
+#endif
 constexpr int RJ_PMAX = 256;   // passes per row at most (more: the rank takes the sort join; PLSSVM_MI_EXP_RJ_PMAX: tests)
 
 // Rows [r0, r0 + gridDim.x) of the rank, one workgroup per row i: its partners j != i sharing two or more
@@ -335,16 +338,29 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
         const int64_t *S = whole ? cst : pst;
         const int32_t *Z = whole ? zoff : pzoff;
         const int32_t pinc = Z[ne];
+        // RJ_U incidences per thread in flight (the walk is bound by the latency of these scattered reads)
         int e = 0;
-        for (int32_t t = tid; t < pinc; t += RJ_NT) {
-            while (Z[e + 1] <= t) ++e;
-            const int64_t j = crow[S[e] + (t - Z[e])];
-            if (j == i || j < R0 || j >= R1) continue;
-            const uint32_t bit = 1u << ((j - R0) & 31);
-            const uint32_t old = atomicOr(&bm[(j - R0) >> 5], bit);
-            if (old & bit) {
-                const int q = atomicAdd(&nrep_s, 1);
-                if (q < RJ_LCAP) rep[q] = (int32_t) j;
+        for (int32_t t0 = tid; t0 < pinc; t0 += RJ_U * RJ_NT) {
+            int64_t jv[RJ_U];
+#pragma unroll
+            for (int u = 0; u < RJ_U; ++u) {
+                const int32_t t = t0 + u * RJ_NT;
+                jv[u] = -1;
+                if (t < pinc) {
+                    while (Z[e + 1] <= t) ++e;
+                    jv[u] = crow[S[e] + (t - Z[e])];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < RJ_U; ++u) {
+                const int64_t j = jv[u];
+                if (j < 0 || j == i || j < R0 || j >= R1) continue;
+                const uint32_t bit = 1u << ((j - R0) & 31);
+                const uint32_t old = atomicOr(&bm[(j - R0) >> 5], bit);
+                if (old & bit) {
+                    const int q = atomicAdd(&nrep_s, 1);
+                    if (q < RJ_LCAP) rep[q] = (int32_t) j;
+                }
             }
         }
         __syncthreads();
@@ -422,9 +438,6 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
 // sequential sum of the sort join). The next partner's row bounds are loaded one step ahead. Pads (sj < 0):
 // j = i, H = 0. lower_nz += #(j < i, H != 0 in T).
 constexpr int RJH_NT = 256;
-#ifndef RJH_PF
-#define RJH_PF 1  // exp_rowjoin_h_kernel: partners software-pipelined (0: bounds one step ahead only)
-#endif
 constexpr int RJ_HS = 2048;  // hash slots for row i's features (<= RJ_ECAP keys)
 __device__ __forceinline__ int rj_hash(int32_t f) { return (int) (((uint32_t) f * 2654435761u) >> (32 - 11)); }
 template <typename T>
@@ -459,70 +472,6 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
     double rmax = 0.0;
     const int64_t q0 = rbeg[r], q1 = rend[r];
     constexpr int NW = RJH_NT / 64;
-#if RJH_PF
-    // software pipeline over this wave's partners (stride NW): the partner index three steps ahead, its row
-    // bounds two steps ahead, the first 64 entries (column, value) of the next partner one step ahead — the
-    // step's own work then waits only for loads issued a step earlier (in-order vmcnt)
-    auto idx = [&](int64_t qq) -> int64_t { return qq < q1 ? (int64_t) sj[qq] : -1; };
-    int64_t q = q0 + wave;
-    int64_t j = idx(q), j1 = idx(q + NW), j2 = idx(q + 2 * NW);
-    int64_t kb = 0, ke = 0, kb1 = 0, ke1 = 0;
-    if (j >= 0) kb = rowptr[j], ke = rowptr[j + 1];
-    if (j1 >= 0) kb1 = rowptr[j1], ke1 = rowptr[j1 + 1];
-    int32_t f0 = kb + lane < ke ? col[kb + lane] : -1;
-    T v0 = kb + lane < ke ? val[kb + lane] : T(0);
-    for (; q < q1; q += NW) {
-        const int32_t fn = kb1 + lane < ke1 ? col[kb1 + lane] : -1;  // next partner's first entries
-        const T vn = kb1 + lane < ke1 ? val[kb1 + lane] : T(0);
-        int64_t kb2 = 0, ke2 = 0;
-        if (j2 >= 0) kb2 = rowptr[j2], ke2 = rowptr[j2 + 1];
-        const int64_t j3 = idx(q + 3 * NW);
-        if (j < 0) {  // pad
-            if (lane == 0) {
-                sj[q] = (int32_t) i;
-                sv[q] = T(0);
-            }
-        } else {
-            double sd = 0.0, sphi = 0.0;
-            for (int64_t k0 = kb; k0 < ke; k0 += 64) {
-                const int64_t k = k0 + lane;
-                double a = 0.0, pa = 0.0;
-                bool hit = false;
-                if (k < ke) {
-                    const int32_t f = k0 == kb ? f0 : col[k];
-                    int h = rj_hash(f);
-                    int32_t key;
-                    while ((key = hkey[h]) >= 0 && key != f) h = (h + 1) & (RJ_HS - 1);
-                    if (key == f) {
-                        a = (double) zval[hidx[h]] * (double) (k0 == kb ? v0 : val[k]);
-                        pa = phi(a);
-                        hit = true;
-                    }
-                }
-                uint64_t mask = __ballot(hit);
-                while (mask) {  // wave-uniform: the shared features in ascending order
-                    const int b = __ffsll((long long) mask) - 1;
-                    mask &= mask - 1;
-                    sd += __shfl(a, b);
-                    sphi += __shfl(pa, b);
-                }
-            }
-            const double ps = phi(sd);
-            const T h = (T) (ps - sphi);
-            // |H| relative to the pair's kernel value without the e_i e_j factor (rbf 1 + E(s), poly kappa + c(s))
-            const double kv = fabs(kbase + ps);
-            const double ratio = h == T(0) ? 0.0 : (kv > 0.0 ? fabs((double) h) / kv : 1e300);
-            if (lane == 0) {
-                sv[q] = h;
-                if (j < i && h != T(0)) ++lnz;
-                rmax = fmax(rmax, ratio);
-            }
-        }
-        j = j1, kb = kb1, ke = ke1, f0 = fn, v0 = vn;
-        j1 = j2, kb1 = kb2, ke1 = ke2;
-        j2 = j3;
-    }
-#else
     int64_t q = q0 + wave;
     int64_t jn = q < q1 ? sj[q] : -1, kbn = 0, ken = 0;
     if (jn >= 0) kbn = rowptr[jn], ken = rowptr[jn + 1];
@@ -573,7 +522,6 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
             rmax = fmax(rmax, ratio);
         }
     }
-#endif
     if (lane == 0 && lnz) atomicAdd(&lnz_s, lnz);
     if (lane == 0 && rmax > 0.0) atomicMax(ratio_bits, (unsigned long long) __double_as_longlong(rmax));  // >= 0: bit order
     __syncthreads();
