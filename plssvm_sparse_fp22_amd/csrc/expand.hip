@@ -276,19 +276,17 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
     const int64_t r = blockIdx.x, i = r0 + r;
     const int64_t e0 = rowptr[i];
     const int ne = (int) (rowptr[i + 1] - e0);  // <= RJ_ECAP (host-checked)
-    for (int e = tid; e < ne; e += RJ_NT) {
+    for (int e = tid; e < ne; e += RJ_NT) {  // column starts and lengths in parallel (one global read each)
         const int32_t f = col[e0 + e];
         zcol[e] = f;
-        cst[e] = colptr[f];
+        const int64_t c0 = colptr[f];
+        cst[e] = c0;
+        zoff[e + 1] = (int32_t) (colptr[f + 1] - c0);
     }
     __syncthreads();
-    if (tid == 0) {
-        int32_t a = 0;
-        for (int e = 0; e < ne; ++e) {
-            zoff[e] = a;
-            a += (int32_t) (colptr[zcol[e] + 1] - cst[e]);
-        }
-        zoff[ne] = a;
+    if (tid == 0) {  // prefix over LDS only
+        zoff[0] = 0;
+        for (int e = 0; e < ne; ++e) zoff[e + 1] += zoff[e];
     }
     __syncthreads();
     const bool wr = sj != nullptr, slots = wr && off8 == nullptr;
@@ -2428,24 +2426,31 @@ __global__ __launch_bounds__(PRED_NT) void exp_pred_point_kernel(
     const int64_t p = blockIdx.x;
     const int64_t e0 = zr[p];
     const int nz = (int) (zr[p + 1] - e0);
-    for (int e = tid; e < nz; e += PRED_NT) zcol_s[e] = zc[e0 + e], zval_s[e] = zv[e0 + e];
+    // the point's entries, x_m at its columns and its columns' CSC lengths: one parallel read each (a serial
+    // loop of dependent global reads in one thread cost ~1 us per entry); x_m's values borrow the bitmap's LDS,
+    // which every pass below clears before use
+    static_assert(PRED_ZCAP * sizeof(T) <= PRED_BMW * sizeof(uint32_t), "x_m staging must fit the bitmap");
+    T *xl_s = reinterpret_cast<T *>(bm);
+    for (int e = tid; e < nz; e += PRED_NT) {
+        const int32_t f = zc[e0 + e];
+        zcol_s[e] = f;
+        zval_s[e] = zv[e0 + e];
+        xl_s[e] = xlast[f];
+        zoff[e + 1] = colptr[f + 1] - colptr[f];
+    }
     __syncthreads();
-    // |z|^2 (column order) and x_m . z (entry order), thread 0
+    // |z|^2 (column order) and x_m . z (entry order), thread 0, from LDS
     if (tid == 0) {
         T nzz = 0, dl = 0;
         for (int e = 0; e < nz; ++e) {
             nzz = fma(zval_s[e], zval_s[e], nzz);
-            dl = fma(xlast[zcol_s[e]], zval_s[e], dl);
+            dl = fma(xl_s[e], zval_s[e], dl);
         }
         red[0] = (double) nzz;
         red[1] = (double) dl;
         // CSC offsets of z's columns (flattened incidences)
-        int64_t acc = 0;
-        for (int e = 0; e < nz; ++e) {
-            zoff[e] = acc;
-            acc += colptr[zcol_s[e] + 1] - colptr[zcol_s[e]];
-        }
-        zoff[nz] = acc;
+        zoff[0] = 0;
+        for (int e = 0; e < nz; ++e) zoff[e + 1] += zoff[e];
     }
     __syncthreads();
     const T nzz = (T) red[0], dl = (T) red[1];
