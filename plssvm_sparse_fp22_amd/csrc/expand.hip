@@ -920,6 +920,9 @@ __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__res
 #ifndef EXP_NH
 #define EXP_NH 2  // remainder stream: groups of 64 chunks per lane step (bytes in flight per wave)
 #endif
+#ifndef EXP_PSCAN
+#define EXP_PSCAN 1  // bfloat16 remainder: row sums as differences of one unsegmented lane prefix (0: segmented scan)
+#endif
 #ifndef EXP_DOT2
 // bfloat16 remainder: a chunk's 4 products as two v_dot2_f32_bf16 (the stream is VALU-bound). The instruction
 // pair is inline assembly whose hazard padding (the s_nop in exp_hcell_kernel) was verified on the GPU with the
@@ -1037,7 +1040,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
         if (empty) return;  // empty stream (wave-uniform)
 #pragma unroll
         for (int hh = 0; hh < EXP_NH; ++hh) {
-            const int64_t cc = c + 64 * hh, cl = cc < s_end ? cc : s_end - 1;
+            const int64_t cl = c + 64 * hh;  // past s_end: the stream's zeroed padding (masked by have)
             group_regs &g = nx[hh];
             if constexpr (!RF) g.rl = (int) __builtin_nontemporal_load(hrow + cl);
             if constexpr (RF && EXP_JH) {  // indices and H of the chunk in one 16-byte load
@@ -1067,7 +1070,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
         uint32_t hx = g.hb.x;
         if constexpr (RF) {
             const uint32_t fb = (hx >> 14) & 1u;  // the row-start flag as 0 / 1
-            const unsigned long long bal = __ballot(have && fb != 0u);
+            const unsigned long long bal = __ballot((hx & 0x4000u) != 0u) & __ballot(have);
             const int below = (int) __builtin_amdgcn_mbcnt_hi((uint32_t) (bal >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t) bal, 0u));
             rl = have ? carry + below + (int) fb - 1 : -1;
@@ -1102,6 +1105,25 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             acc = fma(h3, wat(jj.y >> 16), acc);
         }
 #if EXP_DPP
+        if constexpr (HB && EXP_PSCAN && sizeof(T) == 4) {
+            // bfloat16 H (|H w| <= 2^-16 |k w| per pair): an unsegmented inclusive prefix P of the 64 chunk sums (six
+            // DPP adds, no keys); a row ending at lane e adds P_e to its accumulator and the row that starts at
+            // e + 1 subtracts it — the row's sum as a difference of prefixes. The cancellation costs at most
+            // 2^-24 of the group's |H w| (<= 256 pair terms of <= 2^-16 |k w| each), far below the float rounding
+            // of the row's K·p; fixed order, bitwise reproducible.
+            float P = acc;
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x111, 0xF, 0xF, true));  // row_shr:1
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x112, 0xF, 0xF, true));  // row_shr:2
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x114, 0xF, 0xF, true));  // row_shr:4
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x118, 0xF, 0xF, true));  // row_shr:8
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x142, 0xA, 0xF, true));  // row_bcast:15
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x143, 0xC, 0xF, true));  // row_bcast:31
+            const int rnext = __builtin_amdgcn_update_dpp(-1, rl, 0x130, 0xF, 0xF, false);  // wave_shl:1 (lane 63: -1)
+            const bool end = rl >= 0 && (lane == 63 || rnext != rl);
+            if (end) racc[rl] += (T) P;  // rows of this wave only
+            if (end && lane != 63 && rnext >= 0) racc[rnext] -= (T) P;
+            return;
+        }
         // segmented inclusive prefix sums over the lanes by DPP (rows are non-decreasing in lane order):
         // row_shr 1/2/4/8 inside each 16-lane row, then row_bcast 15 / 31 across rows; the total of a
         // row's run lands on its last lane, which adds it to the row accumulator
@@ -2064,13 +2086,16 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             }
             scan(ncnt);
             ex.nchunks = ex.slots / 4;
-            ex.hjl.alloc(std::max<int64_t>(ex.slots, 4) * (ex.rflags && EXP_JH ? 2 : 1), stream);
+            // EXP_NH x 64 chunks of zeroed padding past the stream's end: the remainder stream's loads of a step
+            // past the end read padding (masked) instead of clamping each lane's 64-bit address
+            const int64_t spad = std::max<int64_t>(ex.slots, 4) + (int64_t) EXP_NH * 64 * 4;
+            ex.hjl.alloc(spad * (ex.rflags && EXP_JH ? 2 : 1), stream);
             if (ex.hbf16) {
                 if (ex.rflags && EXP_JH) ex.hv16.reset();
-                else ex.hv16.alloc(std::max<int64_t>(ex.slots, 4), stream);
+                else ex.hv16.alloc(spad, stream);
                 ex.wv16.alloc(round_up(std::max<int64_t>({ m, chunk * G, 8 }), (int64_t) 8), stream);
             }
-            else ex.hv.alloc(std::max<int64_t>(ex.slots, 4), stream);
+            else ex.hv.alloc(spad, stream);
             if (ex.rflags) {
                 ex.hrow.reset();
                 hipLaunchKernelGGL(exp_cell_scatter_flag_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream,
@@ -2078,7 +2103,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
                                    EXP_JH ? ex.hjl.get() : ex.hv16.get());
                 MI_LAUNCH_CHECK();
             } else {
-                ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1), stream);
+                ex.hrow.alloc(std::max<int64_t>(ex.nchunks, 1) + (int64_t) EXP_NH * 64, stream);
                 if (R > 0) {
                     hipLaunchKernelGGL(exp_cell_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream,
                                        rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, RB, coff.get(), ex.hjl.get(),
