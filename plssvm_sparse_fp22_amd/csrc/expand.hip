@@ -238,6 +238,14 @@ constexpr int RJ_BMW = RJ_BMW_OPT;  // bitmap words: 1 048 576 partner rows per 
 constexpr int RJ_LCAP = 2048;  // repeat sightings held per pass (more: the pass range is halved)
 constexpr int RJ_ECAP = 256;   // entries of row i held in LDS (longer rows: the sort join)
 constexpr int RJ_WPT = RJ_BMW / RJ_NT;
+// bitmap word L of the join (partner rows 32 L .. 32 L + 31 of the pass) lives at LDS word (L % WPT) NT + L / WPT:
+// thread t owns the contiguous words t WPT .. t WPT + WPT - 1 (its count and its ascending enumeration), and at
+// each step of those loops the 64 lanes read consecutive LDS words — one bank each (word t WPT + w of a plain
+// layout put every lane of a wave on the same bank: 64-way conflicts)
+template <int WPT, int NT>
+__device__ __forceinline__ int bm_addr(int64_t L) {
+    return (int) (L % WPT) * NT + (int) (L / WPT);
+}
 #ifndef RJ_U
 #define RJ_U 4  // incidence reads in flight per thread in the join's walk
 #endif
@@ -354,7 +362,7 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
                 const int64_t j = jv[u];
                 if (j < 0 || j == i || j < R0 || j >= R1) continue;
                 const uint32_t bit = 1u << ((j - R0) & 31);
-                const uint32_t old = atomicOr(&bm[(j - R0) >> 5], bit);
+                const uint32_t old = atomicOr(&bm[bm_addr<RJ_WPT, RJ_NT>((j - R0) >> 5)], bit);
                 if (old & bit) {
                     const int q = atomicAdd(&nrep_s, 1);
                     if (q < RJ_LCAP) rep[q] = (int32_t) j;
@@ -372,12 +380,12 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
         __syncthreads();
         for (int q = tid; q < nr; q += RJ_NT) {
             const int64_t j = rep[q] - R0;
-            atomicOr(&bm[j >> 5], 1u << (j & 31));
+            atomicOr(&bm[bm_addr<RJ_WPT, RJ_NT>(j >> 5)], 1u << (j & 31));
         }
         __syncthreads();
         int c = 0;
 #pragma unroll 8
-        for (int w = 0; w < RJ_WPT; ++w) c += __popc(bm[tid * RJ_WPT + w]);
+        for (int w = 0; w < RJ_WPT; ++w) c += __popc(bm[w * RJ_NT + tid]);
         // exclusive block scan of c (wave scans + wave totals)
         int incl = c;
 #pragma unroll
@@ -396,7 +404,7 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
         if (wr) {
             int pos = before + incl - c;
             for (int w = 0; w < RJ_WPT; ++w) {
-                uint32_t word = bm[tid * RJ_WPT + w];
+                uint32_t word = bm[w * RJ_NT + tid];
                 while (word) {
                     const int b = __ffs(word) - 1;
                     word &= word - 1;
@@ -2508,7 +2516,7 @@ __global__ __launch_bounds__(PRED_NT) void exp_pred_point_kernel(
             const int64_t i = crow[colptr[zcol_s[lo]] + (t - zoff[lo])];
             if (i < R0 || i >= R1) continue;
             const uint32_t bit = 1u << ((i - R0) & 31);
-            const uint32_t old = atomicOr(&bm[(i - R0) >> 5], bit);
+            const uint32_t old = atomicOr(&bm[bm_addr<PRED_BMW / PRED_NT, PRED_NT>((i - R0) >> 5)], bit);
             if (old & bit) {
                 const int q = atomicAdd(&nmulti, 1);
                 if (q < PRED_MCAP) multi[q] = (int32_t) i;
@@ -2525,28 +2533,33 @@ __global__ __launch_bounds__(PRED_NT) void exp_pred_point_kernel(
         __syncthreads();
         for (int q = tid; q < nm; q += PRED_NT) {
             const int64_t i = multi[q] - R0;
-            atomicOr(&bm[i >> 5], 1u << (i & 31));
+            atomicOr(&bm[bm_addr<PRED_BMW / PRED_NT, PRED_NT>(i >> 5)], 1u << (i & 31));
         }
         __syncthreads();
         constexpr int WPT = PRED_BMW / PRED_NT;
         int c = 0;
-        for (int q = 0; q < WPT; ++q) c += __popc(bm[tid * WPT + q]);
-        wcnt[tid] = c;
-        __syncthreads();
-        if (tid == 0) {  // exclusive scan of the 1024 counts
-            int a = 0;
-            for (int q = 0; q < PRED_NT; ++q) {
-                const int v = wcnt[q];
-                wcnt[q] = a;
-                a += v;
-            }
-            nmulti = a;
+        for (int q = 0; q < WPT; ++q) c += __popc(bm[q * PRED_NT + tid]);
+        // exclusive block scan of the counts (wave scans, then the wave totals), not a serial loop over 1024
+        const int lane = tid & 63, wave = tid >> 6;
+        int incl = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
         }
+        if (lane == 63) wcnt[wave] = incl;
         __syncthreads();
+        int before = 0, tot = 0;
+        for (int w2 = 0; w2 < PRED_NT / 64; ++w2) {
+            const int v = wcnt[w2];
+            if (w2 < wave) before += v;
+            tot += v;
+        }
+        if (tid == 0) nmulti = tot;
         {
-            int pos = wcnt[tid];
+            int pos = before + incl - c;
             for (int q = 0; q < WPT; ++q) {
-                uint32_t word = bm[tid * WPT + q];
+                uint32_t word = bm[q * PRED_NT + tid];
                 while (word) {
                     const int b = __ffs(word) - 1;
                     word &= word - 1;

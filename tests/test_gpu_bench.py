@@ -44,3 +44,18 @@ def test_sparse_extra_line_contract():
     assert (cfg["N"], cfg["d"], cfg["layout"]) == (1_000_000, 50_000, "csr")
     roof = r["roofline"]
     assert roof["bound"] == "hbm" and 0.3 < roof["frac"] < 1.0
+
+
+@pytest.mark.gpu
+def test_dense_linear_500k_line_contract():
+    """BASELINE configs[3] (dense linear 500k x 1024 fp32, the MFMA row) at its full size on one GPU: the record the
+    default line carries as extra.dense_linear_500k"""
+    r = run_bench("--config", "dense_linear_500k", "--no-cpu", "--steps", "1", "--warmup", "0", "--kp-reps", "1")
+    cfg = r["config"]
+    assert (cfg["N"], cfg["d"], cfg["kernel"], cfg["layout"], cfg["kp_mode"]) == (500_000, 1024, "linear", "dense",
+                                                                                 "pairwise")
+    assert r["dtype"] == "f32"
+    roof = r["roofline"]
+    assert roof["bound"] == "mfma" and roof["kernel"] == "kp_tile_kernel"
+    assert roof["alg_flop_per_launch"] == pytest.approx(2 * 1024 * 499_999 * 500_000 / 2)
+    assert 0.5 < roof["frac"] < 1.0
