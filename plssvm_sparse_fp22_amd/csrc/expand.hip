@@ -444,13 +444,6 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
 // sequential sum of the sort join). The next partner's row bounds are loaded one step ahead. Pads (sj < 0):
 // j = i, H = 0. lower_nz += #(j < i, H != 0 in T).
 constexpr int RJH_NT = 256;
-// a double of lane b (wave-uniform b), via two scalar lane reads instead of an LDS permute
-__device__ __forceinline__ double readlane_f64(double v, int b) {
-    const long long u = __double_as_longlong(v);
-    const uint32_t lo = (uint32_t) __builtin_amdgcn_readlane((int) (uint32_t) u, b);
-    const uint32_t hi = (uint32_t) __builtin_amdgcn_readlane((int) (u >> 32), b);
-    return __longlong_as_double((long long) (((uint64_t) hi << 32) | lo));
-}
 constexpr int RJ_HS = 2048;  // hash slots for row i's features (<= RJ_ECAP keys)
 __device__ __forceinline__ int rj_hash(int32_t f) { return (int) (((uint32_t) f * 2654435761u) >> (32 - 11)); }
 template <typename T>
@@ -517,11 +510,11 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
                 }
             }
             uint64_t mask = __ballot(hit);
-            while (mask) {  // wave-uniform: the shared features in ascending order, read by lane index (no LDS)
+            while (mask) {  // wave-uniform: the shared features in ascending order
                 const int b = __ffsll((long long) mask) - 1;
                 mask &= mask - 1;
-                sd += readlane_f64(a, b);
-                sphi += readlane_f64(pa, b);
+                sd += __shfl(a, b);
+                sphi += __shfl(pa, b);
             }
         }
         const double ps = phi(sd);
