@@ -441,8 +441,8 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
 // <= 1/8 full: one probe per lookup instead of a binary search), one partner per wave at a time: the lanes take
 // row j's entries (coalesced, 64 per step), look each up in row i, and the matches — ascending features — are
 // summed in that order from a ballot: H_ij = phi(s_ij) - sum_f phi(x_if x_jf) in fp64, rounded to T (the
-// sequential sum of the sort join). The next partner's row bounds are loaded one step ahead. Pads (sj < 0):
-// j = i, H = 0. lower_nz += #(j < i, H != 0 in T).
+// sequential sum of the sort join; rbf: a product recurrence without the expm1 of s_ij, in the body). The next
+// partner's row bounds are loaded one step ahead. Pads (sj < 0): j = i, H = 0. lower_nz += #(j < i, H != 0 in T).
 constexpr int RJH_NT = 256;
 constexpr int RJ_HS = 2048;  // hash slots for row i's features (<= RJ_ECAP keys)
 __device__ __forceinline__ int rj_hash(int32_t f) { return (int) (((uint32_t) f * 2654435761u) >> (32 - 11)); }
@@ -493,7 +493,11 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
             }
             continue;
         }
-        double sd = 0.0, sphi = 0.0;
+        // rbf: with E_f = expm1(2 g x_if x_jf), 1 + E(s_ij) = prod_f (1 + E_f), so H = prod (1 + E_f) - 1 - sum E_f
+        // accumulates over the shared features (ascending) as Q += P E_f, P += E_f + P E_f (P = prod - 1): no
+        // expm1 of s_ij and no cancellation (two shared features: H = E_a E_b exactly). poly: H = c(s) - sum c(a_f).
+        const bool rbf = phi.rbf != 0;
+        double sd = 0.0, sphi = 0.0, P = 0.0;
         for (int64_t k0 = kb; k0 < ke; k0 += 64) {
             const int64_t k = k0 + lane;
             double a = 0.0, pa = 0.0;
@@ -513,19 +517,26 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
             while (mask) {  // wave-uniform: the shared features in ascending order
                 const int b = __ffsll((long long) mask) - 1;
                 mask &= mask - 1;
-                sd += __shfl(a, b);
-                sphi += __shfl(pa, b);
+                const double pb = __shfl(pa, b);
+                if (rbf) {
+                    const double t = P * pb;
+                    sphi += t;  // Q
+                    P += pb + t;
+                } else {
+                    sd += __shfl(a, b);
+                    sphi += pb;
+                }
             }
         }
-        const double ps = phi(sd);
-        const T h = (T) (ps - sphi);
-        // |H| relative to the pair's kernel value without the e_i e_j factor (rbf 1 + E(s), poly kappa + c(s))
-        const double kv = fabs(kbase + ps);
-        const double ratio = h == T(0) ? 0.0 : (kv > 0.0 ? fabs((double) h) / kv : 1e300);
+        const double ps = rbf ? P : phi(sd);  // E(s) or c(s)
+        const T h = (T) (rbf ? sphi : ps - sphi);
+        // |H| relative to the pair's kernel value without the e_i e_j factor (rbf 1 + E(s), poly kappa + c(s));
+        // the division only when it can raise the maximum (wave-uniform values)
+        const double kv = fabs(kbase + ps), ah = fabs((double) h);
+        if (h != T(0) && ah > rmax * kv) rmax = kv > 0.0 ? ah / kv : 1e300;
         if (lane == 0) {
             sv[q] = h;
             if (j < i && h != T(0)) ++lnz;
-            rmax = fmax(rmax, ratio);
         }
     }
     if (lane == 0 && lnz) atomicAdd(&lnz_s, lnz);
