@@ -167,6 +167,7 @@ struct engine : engine_base {
     int64_t estimate_expansion_bytes(const int64_t *rowptr, const int32_t *col, const std::vector<int64_t> &colptr,
                                      const std::vector<int32_t> &crow, int64_t inc_total, double *row_stats = nullptr) const;
     void release_sparse_structures();
+    void csc_device(int64_t nnz, dev_buf<int64_t> &cpos_d);  // csr.colptr / crow / cval and cpos on the device
     void setup_sparse_dense();                                     // densified fallback (PLSSVM_MI_SPARSE_DENSE)
     // on-the-fly path (otf.hip, PLSSVM_MI_SPARSE_ONTHEFLY): estimated seconds per K·p share, setup, K·p
     double otf_estimate_s(const int64_t *rowptr, const int32_t *col, const std::vector<int64_t> &colptr) const;

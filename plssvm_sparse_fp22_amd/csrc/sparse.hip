@@ -76,6 +76,59 @@ __global__ __launch_bounds__(256) void csr_q_kernel(kfun<T> kf, const int64_t *_
     }
 }
 
+// ---- CSC on the device (rows 0..m-1): a stable radix sort of the entries by column keeps the rows ascending
+// inside every column — the host counting sort's CSC (csc_host below), bit for bit ------------------------
+// entry k's row, and k itself (the sort's payload); one wave per row
+__global__ __launch_bounds__(256) void csc_rowid_kernel(const int64_t *__restrict__ rowptr, int64_t m,
+                                                        int32_t *__restrict__ rowid, int32_t *__restrict__ kid) {
+    const int64_t i = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= m) return;
+    for (int64_t k = rowptr[i] + (threadIdx.x & 63); k < rowptr[i + 1]; k += 64) {
+        rowid[k] = (int32_t) i;
+        kid[k] = (int32_t) k;
+    }
+}
+
+// colptr[f] = #entries of a column < f, from the sorted columns: the first entry q of a column >= f writes
+// it (each f exactly once: q = nnz takes the empty columns after the last entry's)
+__global__ __launch_bounds__(256) void csc_colptr_kernel(const uint32_t *__restrict__ skey, int64_t nnz, int64_t d,
+                                                         int64_t *__restrict__ colptr) {
+    const int64_t q = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (q > nnz) return;
+    const int64_t lo = q == 0 ? 0 : (int64_t) skey[q - 1] + 1, hi = q == nnz ? d : (int64_t) skey[q];
+    for (int64_t f = lo; f <= hi; ++f) colptr[f] = q;
+}
+
+// CSC slot q holds entry k = sk[q]: its row, its (decoded) value; cpos[k] = q
+template <typename T>
+__global__ __launch_bounds__(256) void csc_gather_kernel(const int32_t *__restrict__ sk, const int32_t *__restrict__ rowid,
+                                                         const T *__restrict__ val, int64_t nnz, int32_t *__restrict__ crow,
+                                                         T *__restrict__ cval, int64_t *__restrict__ cpos) {
+    const int64_t q = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nnz) return;
+    const int32_t k = sk[q];
+    crow[q] = rowid[k];
+    cval[q] = val[k];
+    cpos[k] = q;
+}
+
+// incidences of each block of rb rows: sum over its entries of #{ earlier rows in the entry's column }
+// (integers: exact in any order)
+__global__ __launch_bounds__(256) void csc_inc_rb_kernel(const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+                                                         const int64_t *__restrict__ cpos, const int64_t *__restrict__ colptr,
+                                                         int64_t m, int64_t rb, int64_t *__restrict__ inc_rb) {
+    __shared__ long long part[4];
+    const int64_t I = blockIdx.x;
+    const int64_t k0 = rowptr[I * rb], k1 = rowptr[min(m, (I + 1) * rb)];
+    long long a = 0;
+    for (int64_t k = k0 + threadIdx.x; k < k1; k += 256) a += (long long) (cpos[k] - colptr[col[k]]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) inc_rb[I] = (int64_t) (part[0] + part[1] + part[2] + part[3]);
+}
+
 // ---- Gram pattern build ---------------------------------------------------------------------------------
 // incidences of row i: sum over its entries e of #{ j < i in column col[e] } = cpos[e] - colptr[col[e]]
 __global__ __launch_bounds__(256) void gram_count_kernel(const int64_t *__restrict__ rowptr,
@@ -577,7 +630,55 @@ void host_check_csr(const int64_t *rowptr, const int32_t *col, int64_t n, int64_
 
 }  // namespace
 
+// FP22 input: the SELL streams hold the packed values (PLSSVM_MI_SELL_F22=1) or their exact fp32 decoding
+inline bool sell_fp22_stream() {
+    static const bool on = [] {
+        const char *e = std::getenv("PLSSVM_MI_SELL_F22");
+        return e == nullptr || std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 // ---- engine members ----------------------------------------------------------------------------------
+// the CSC of rows 0..m-1 from the device CSR (0 < nnz < 2^31): entries sorted by column with a stable radix sort
+// (rows stay ascending inside a column), colptr from the sorted columns, crow / cval / cpos by a gather
+template <typename T>
+void engine<T>::csc_device(int64_t nnz, dev_buf<int64_t> &cpos_d) {
+    const int n32 = (int) nnz;
+    int end_bit = 1;
+    while (end_bit < 32 && (int64_t(1) << end_bit) < d) ++end_bit;
+    dev_buf<int32_t> rowid, kid, kid_s;
+    dev_buf<uint32_t> key_s;
+    rowid.alloc(nnz, stream, false);
+    kid.alloc(nnz, stream, false);
+    kid_s.alloc(nnz, stream, false);
+    key_s.alloc(nnz, stream, false);
+    hipLaunchKernelGGL(csc_rowid_kernel, dim3((unsigned) ceil_div(m, 4)), dim3(256), 0, stream, csr.rowptr.get(), m,
+                       rowid.get(), kid.get());
+    MI_LAUNCH_CHECK();
+    const uint32_t *keys = reinterpret_cast<const uint32_t *>(csr.col.get());  // columns >= 0: the same order unsigned
+    size_t tb = 0;
+    MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, key_s.get(), kid.get(), kid_s.get(), n32, 0, end_bit,
+                                                    stream));
+    {
+        dev_buf<unsigned char> tmp;
+        tmp.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
+        MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp.get(), tb, keys, key_s.get(), kid.get(), kid_s.get(), n32, 0,
+                                                        end_bit, stream));
+        csr.colptr.alloc(d + 1, stream, false);
+        hipLaunchKernelGGL(csc_colptr_kernel, dim3((unsigned) ceil_div(nnz + 1, 256)), dim3(256), 0, stream, key_s.get(),
+                           nnz, d, csr.colptr.get());
+        MI_LAUNCH_CHECK();
+        csr.crow.alloc(nnz, stream, false);
+        csr.cval.alloc(nnz, stream, false);
+        cpos_d.alloc(nnz, stream, false);
+        hipLaunchKernelGGL(csc_gather_kernel<T>, dim3((unsigned) ceil_div(nnz, 256)), dim3(256), 0, stream, kid_s.get(),
+                           rowid.get(), csr.val.get(), nnz, csr.crow.get(), csr.cval.get(), cpos_d.get());
+        MI_LAUNCH_CHECK();
+        MI_HIP_CHECK(hipStreamSynchronize(stream));  // the temporaries are freed on return
+    }
+}
+
 template <typename T>
 void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void *val, int val_fmt, int64_t n_,
                           int64_t d_) {
@@ -637,64 +738,108 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     finish_setup();  // row split r0, r1
     pt.mark("setup_csr: check + upload + norms");
 
-    // CSC of rows 0..m-1 for the Gram pattern (counting sort: rows ascending inside each column) and,
-    // per CSR entry, its CSC position (the column join needs "rows < i in this column" = cpos - colptr)
-    // (a counting sort on the host threads: thread t owns a contiguous row range, so its entries of a column
-    // follow thread t - 1's — the same CSC as the sequential sort)
-    std::vector<int64_t> colptr(d + 1, 0), cpos(std::max<int64_t>(nnz, 1));
-    std::vector<int32_t> crow(std::max<int64_t>(nnz, 1));
+    // CSC of rows 0..m-1 (rows ascending inside each column) and, per CSR entry, its CSC position cpos (the
+    // Gram pattern's column join needs "rows < i in this column" = cpos - colptr). On the device by default
+    // (csc_device: a radix sort, the host keeps colptr and crow for its estimates and fetches the values only
+    // for the SELL plans); on the host threads (csc_host: a counting sort) when nnz reaches 2^31 or with
+    // PLSSVM_MI_CSC=host. Both give the same arrays.
+    std::vector<int64_t> colptr(d + 1, 0), cpos;
+    std::vector<int32_t> crow;
     // values in CSC order, decoded (FP22 input included: the Gram build multiplies them once at setup,
     // the K·p stream holds the products s_ij, so FP22 changes only the input format)
-    std::vector<T> cval_real(std::max<int64_t>(nnz, 1));
+    std::vector<T> cval_real;
+    dev_buf<int64_t> cpos_d;
     double amax = 0.0, nmax = 0.0;  // max x^2 and max |x_i|^2 (kernel expansion eligibility)
-    {
-        const int NT = (int) std::max<int64_t>(1, std::min<int64_t>(host_threads(), nnz / 65536 + 1));
-        std::vector<int64_t> rb(NT + 1, 0);  // row ranges balanced by entries
-        for (int t = 1; t < NT; ++t)
-            rb[t] = std::upper_bound(rowptr, rowptr + m + 1, (nnz * t) / NT) - rowptr - 1;
-        rb[NT] = m;
-        for (int t = 1; t <= NT; ++t) rb[t] = std::max(rb[t], rb[t - 1]);
-        std::vector<std::vector<int64_t>> cnt((size_t) NT);
+    const bool dev_csc = [&] {
+        const char *e = std::getenv("PLSSVM_MI_CSC");
+        return nnz > 0 && nnz < (int64_t) INT32_MAX && !(e != nullptr && std::strcmp(e, "host") == 0);
+    }();
+    if (dev_csc) {
+        csc_device(nnz, cpos_d);
+        crow.resize((size_t) nnz);
+        MI_HIP_CHECK(hipMemcpyAsync(colptr.data(), csr.colptr.get(), sizeof(int64_t) * (size_t) (d + 1),
+                                    hipMemcpyDeviceToHost, stream));
+        MI_HIP_CHECK(hipMemcpyAsync(crow.data(), csr.crow.get(), sizeof(int32_t) * (size_t) nnz, hipMemcpyDeviceToHost,
+                                    stream));
+        // amax / nmax from the host CSR, in the host sort's order (rows ascending, each row's entries in order)
+        const int NT = (int) std::max<int64_t>(1, std::min<int64_t>(host_threads(), m / 4096 + 1));
         std::vector<double> amax_t(NT, 0.0), nmax_t(NT, 0.0);
-        host_parallel(NT, [&](int, int64_t t0, int64_t t1) {
-            for (int64_t t = t0; t < t1; ++t) {
-                auto &c = cnt[(size_t) t];
-                c.assign((size_t) d, 0);
-                for (int64_t k = rowptr[rb[t]]; k < rowptr[rb[t + 1]]; ++k) ++c[(size_t) col[k]];
-            }
-        }, NT);
-        for (int64_t f = 0; f < d; ++f) {  // colptr and each thread's first slot per column
-            int64_t a = colptr[f];
-            for (int t = 0; t < NT; ++t) {
-                const int64_t v = cnt[(size_t) t][(size_t) f];
-                cnt[(size_t) t][(size_t) f] = a;
-                a += v;
-            }
-            colptr[f + 1] = a;
-        }
-        host_parallel(NT, [&](int, int64_t t0, int64_t t1) {
-            for (int64_t t = t0; t < t1; ++t) {
-                auto &fill = cnt[(size_t) t];
-                double am = 0.0, nm = 0.0;
-                for (int64_t i = rb[t]; i < rb[t + 1]; ++i) {
-                    double nrm = 0.0;
-                    for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-                        const int64_t q = fill[(size_t) col[k]]++;
-                        crow[q] = (int32_t) i;
-                        cpos[k] = q;
-                        cval_real[q] = hval(k);
-                        const double x = (double) cval_real[q];
-                        am = std::max(am, x * x);
-                        nrm += x * x;
-                    }
-                    nm = std::max(nm, nrm);
+        host_parallel(m, [&](int t, int64_t i0, int64_t i1) {
+            double am = 0.0, nm = 0.0;
+            for (int64_t i = i0; i < i1; ++i) {
+                double nrm = 0.0;
+                for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+                    const double x = (double) hval(k);
+                    am = std::max(am, x * x);
+                    nrm += x * x;
                 }
-                amax_t[(size_t) t] = am;
-                nmax_t[(size_t) t] = nm;
+                nm = std::max(nm, nrm);
             }
+            amax_t[(size_t) t] = std::max(amax_t[(size_t) t], am);
+            nmax_t[(size_t) t] = std::max(nmax_t[(size_t) t], nm);
         }, NT);
         for (int t = 0; t < NT; ++t) amax = std::max(amax, amax_t[(size_t) t]), nmax = std::max(nmax, nmax_t[(size_t) t]);
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+    } else {
+        cpos.assign((size_t) std::max<int64_t>(nnz, 1), 0);
+        crow.assign((size_t) std::max<int64_t>(nnz, 1), 0);
+        cval_real.assign((size_t) std::max<int64_t>(nnz, 1), T(0));
+        {
+            const int NT = (int) std::max<int64_t>(1, std::min<int64_t>(host_threads(), nnz / 65536 + 1));
+            std::vector<int64_t> rb(NT + 1, 0);  // row ranges balanced by entries
+            for (int t = 1; t < NT; ++t)
+                rb[t] = std::upper_bound(rowptr, rowptr + m + 1, (nnz * t) / NT) - rowptr - 1;
+            rb[NT] = m;
+            for (int t = 1; t <= NT; ++t) rb[t] = std::max(rb[t], rb[t - 1]);
+            std::vector<std::vector<int64_t>> cnt((size_t) NT);
+            std::vector<double> amax_t(NT, 0.0), nmax_t(NT, 0.0);
+            host_parallel(NT, [&](int, int64_t t0, int64_t t1) {
+                for (int64_t t = t0; t < t1; ++t) {
+                    auto &c = cnt[(size_t) t];
+                    c.assign((size_t) d, 0);
+                    for (int64_t k = rowptr[rb[t]]; k < rowptr[rb[t + 1]]; ++k) ++c[(size_t) col[k]];
+                }
+            }, NT);
+            for (int64_t f = 0; f < d; ++f) {  // colptr and each thread's first slot per column
+                int64_t a = colptr[f];
+                for (int t = 0; t < NT; ++t) {
+                    const int64_t v = cnt[(size_t) t][(size_t) f];
+                    cnt[(size_t) t][(size_t) f] = a;
+                    a += v;
+                }
+                colptr[f + 1] = a;
+            }
+            host_parallel(NT, [&](int, int64_t t0, int64_t t1) {
+                for (int64_t t = t0; t < t1; ++t) {
+                    auto &fill = cnt[(size_t) t];
+                    double am = 0.0, nm = 0.0;
+                    for (int64_t i = rb[t]; i < rb[t + 1]; ++i) {
+                        double nrm = 0.0;
+                        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+                            const int64_t q = fill[(size_t) col[k]]++;
+                            crow[q] = (int32_t) i;
+                            cpos[k] = q;
+                            cval_real[q] = hval(k);
+                            const double x = (double) cval_real[q];
+                            am = std::max(am, x * x);
+                            nrm += x * x;
+                        }
+                        nm = std::max(nm, nrm);
+                    }
+                    amax_t[(size_t) t] = am;
+                    nmax_t[(size_t) t] = nm;
+                }
+            }, NT);
+            for (int t = 0; t < NT; ++t) amax = std::max(amax, amax_t[(size_t) t]), nmax = std::max(nmax, nmax_t[(size_t) t]);
+        }
     }
+    // the CSC values on the host (the SELL plans' CSC generator): fetched on first use after a device sort
+    auto need_cval_h = [&](hipStream_t s) {
+        if (!dev_csc || !cval_real.empty()) return;
+        cval_real.resize((size_t) nnz);
+        MI_HIP_CHECK(hipMemcpyAsync(cval_real.data(), csr.cval.get(), sizeof(T) * (size_t) nnz, hipMemcpyDeviceToHost, s));
+        MI_HIP_CHECK(hipStreamSynchronize(s));
+    };
     // CSC segments of rows [c0, c1) (rows ascending in each column: a contiguous part of the column)
     auto csc_gen = [&](int64_t c0, int64_t c1) {
         return [&, c0, c1](auto emit, int64_t f0, int64_t f1) {
@@ -720,8 +865,11 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         const bool local = (world > 1 && sim_world == 0) || (sim_world > 0 && shard);
         csr.csc_r0 = local ? r0 : 0;
         csr.csc_r1 = local ? r1 : m;
-        const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
+        const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22 && sell_fp22_stream();
         const int64_t blocks = sell_target_blocks();
+        need_cval_h(stream);
+        // the K·p reads only the SELL streams: no device CSC
+        cpos_d.reset(), csr.colptr.reset(), csr.crow.reset(), csr.cval.reset();
         build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22,
                            csc_gen(csr.csc_r0, csr.csc_r1), blocks, stream);
         build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks, stream);
@@ -732,32 +880,51 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     }
     csr.csc_r0 = 0;
     csr.csc_r1 = m;
-    csr.colptr.alloc(d + 1, stream);
-    MI_HIP_CHECK(hipMemcpyAsync(csr.colptr.get(), colptr.data(), sizeof(int64_t) * (size_t) (d + 1),
-                                hipMemcpyHostToDevice, stream));
-    csr.crow.alloc(std::max<int64_t>(nnz, 1), stream);
-    if (nnz)
-        MI_HIP_CHECK(hipMemcpyAsync(csr.crow.get(), crow.data(), sizeof(int32_t) * (size_t) nnz, hipMemcpyHostToDevice,
-                                    stream));
-    csr.cval.alloc(std::max<int64_t>(nnz, 1), stream);
-    if (nnz)
-        MI_HIP_CHECK(hipMemcpyAsync(csr.cval.get(), cval_real.data(), sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice,
-                                    stream));
-    MI_HIP_CHECK(hipStreamSynchronize(stream));
-    pt.mark("setup_csr: host CSC");
+    if (!dev_csc) {  // the host sort's CSC to the device
+        csr.colptr.alloc(d + 1, stream);
+        MI_HIP_CHECK(hipMemcpyAsync(csr.colptr.get(), colptr.data(), sizeof(int64_t) * (size_t) (d + 1),
+                                    hipMemcpyHostToDevice, stream));
+        csr.crow.alloc(std::max<int64_t>(nnz, 1), stream);
+        if (nnz)
+            MI_HIP_CHECK(hipMemcpyAsync(csr.crow.get(), crow.data(), sizeof(int32_t) * (size_t) nnz, hipMemcpyHostToDevice,
+                                        stream));
+        csr.cval.alloc(std::max<int64_t>(nnz, 1), stream);
+        if (nnz)
+            MI_HIP_CHECK(hipMemcpyAsync(csr.cval.get(), cval_real.data(), sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice,
+                                        stream));
+        cpos_d.alloc(std::max<int64_t>(nnz, 1), stream);
+        if (nnz)
+            MI_HIP_CHECK(hipMemcpyAsync(cpos_d.get(), cpos.data(), sizeof(int64_t) * (size_t) nnz, hipMemcpyHostToDevice,
+                                        stream));
+        MI_HIP_CHECK(hipStreamSynchronize(stream));
+    }
+    pt.mark(dev_csc ? "setup_csr: device CSC" : "setup_csr: host CSC");
 
     {
         // Gram pattern: row blocks owned by this rank, balanced by column-join incidences
         const int64_t nRB = ceil_div(std::max<int64_t>(m, 1), GRAM_RB);
         std::vector<int64_t> inc_rb(nRB, 0);
-        host_parallel(nRB, [&](int, int64_t I0, int64_t I1) {
-            for (int64_t I = I0; I < I1; ++I) {
-                int64_t a = 0;
-                for (int64_t k = rowptr[I * GRAM_RB]; k < rowptr[std::min<int64_t>(m, (I + 1) * GRAM_RB)]; ++k)
-                    a += cpos[k] - colptr[col[k]];
-                inc_rb[(size_t) I] = a;
+        if (dev_csc) {
+            dev_buf<int64_t> irb;
+            irb.alloc(nRB, stream);
+            if (m > 0) {
+                hipLaunchKernelGGL(csc_inc_rb_kernel, dim3((unsigned) nRB), dim3(256), 0, stream, csr.rowptr.get(),
+                                   csr.col.get(), cpos_d.get(), csr.colptr.get(), m, (int64_t) GRAM_RB, irb.get());
+                MI_LAUNCH_CHECK();
             }
-        });
+            MI_HIP_CHECK(hipMemcpyAsync(inc_rb.data(), irb.get(), sizeof(int64_t) * (size_t) nRB, hipMemcpyDeviceToHost,
+                                        stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+        } else {
+            host_parallel(nRB, [&](int, int64_t I0, int64_t I1) {
+                for (int64_t I = I0; I < I1; ++I) {
+                    int64_t a = 0;
+                    for (int64_t k = rowptr[I * GRAM_RB]; k < rowptr[std::min<int64_t>(m, (I + 1) * GRAM_RB)]; ++k)
+                        a += cpos[k] - colptr[col[k]];
+                    inc_rb[(size_t) I] = a;
+                }
+            });
+        }
         const int eff_world = sim_world > 0 ? sim_world : world, eff_rank = sim_world > 0 ? sim_rank : rank;
         std::vector<int64_t> cum(nRB + 1, 0);
         for (int64_t I = 0; I < nRB; ++I) cum[I + 1] = cum[I] + inc_rb[I];
@@ -771,12 +938,6 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         csr.rb0 = std::min(split(eff_rank), nRB);
         csr.rb1 = std::max(csr.rb0, std::min(split(eff_rank + 1), nRB));
         csr.pair_bound = cum[csr.rb1] - cum[csr.rb0];
-        // device copy of cpos for the generator
-        dev_buf<int64_t> cpos_d;
-        cpos_d.alloc(std::max<int64_t>(nnz, 1), stream);
-        if (nnz)
-            MI_HIP_CHECK(hipMemcpyAsync(cpos_d.get(), cpos.data(), sizeof(int64_t) * (size_t) nnz, hipMemcpyHostToDevice,
-                                        stream));
         int64_t max_inc = 0;
         for (int64_t I = csr.rb0; I < csr.rb1; ++I) max_inc = std::max(max_inc, inc_rb[I]);
         // kernel expansion (expand.hip) when it represents the kernel to rounding, else the Gram pattern;
@@ -836,7 +997,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                     // the two SELL passes of the kernel expansion (the factored linear path's plans, with K channels):
                     // column moments over the CSC of this rank's rows in a real group (all-reduced, d x K values)
                     // or of all rows, the Horner pass over this rank's CSR rows
-                    const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22;
+                    const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22 && sell_fp22_stream();
                     const int64_t blocks = sell_target_blocks();
                     const bool local = (world > 1 && sim_world == 0) || (sim_world > 0 && shard);
                     csr.csc_r0 = local ? r0 : 0;
@@ -850,6 +1011,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                             phase_timer tp;
                             MI_HIP_CHECK(hipSetDevice(device));
                             MI_HIP_CHECK(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
+                            need_cval_h(ps);
                             build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0,
                                                rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22, csc_gen(csr.csc_r0, csr.csc_r1),
                                                blocks, ps, 0, 1, csr.ex.KM);
