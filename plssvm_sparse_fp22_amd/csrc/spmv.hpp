@@ -73,7 +73,7 @@ constexpr bool SELL_VAL2 = SELL_IDX2 && PLSSVM_MI_SELL_VAL2 != 0;
 // stream as well, so one 12-byte load per lane (3 words at 4-byte alignment) decodes two values instead of two
 // overlapping 8-byte loads
 #ifndef PLSSVM_MI_SELL_F22PAIR
-#define PLSSVM_MI_SELL_F22PAIR 0
+#define PLSSVM_MI_SELL_F22PAIR 1
 #endif
 constexpr bool SELL_F22PAIR = SELL_IDX2 && PLSSVM_MI_SELL_F22PAIR != 0;
 // storage position of the entry at value position t = off + 64 j + l (off % 128 == 0 when paired)
