@@ -38,13 +38,32 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
-// phi in double: the exact per-pair function (rbf: expm1(2 g a); poly: sum_k bin_k a^k, no cancellation)
+// phi in double: the exact per-pair function (rbf: expm1(2 g a); poly: sum_k bin_k a^k, no cancellation).
+// rbf with |u| = |2 g a| < 2^-7 (every pair of the BASELINE sets: u <= 2 g max x^2 ~ 1e-4): the Taylor
+// polynomial of degree 7, whose remainder u^8 / 8! is below 2^-54 |u| there — fp64 accuracy in 8 fma instead of
+// the library expm1's range reduction (the setup's remainder kernels evaluate phi once per wave step)
+#ifndef PLSSVM_MI_PHI_POLY
+#define PLSSVM_MI_PHI_POLY 1
+#endif
 struct phi_fn {
     int rbf = 0, deg = 0;
     double g2 = 0.0;                   // rbf: 2 g
     double bin[EXP_KMAX + 1] = {};     // poly: C(deg, k) c0^(deg - k) g^k
     __host__ __device__ double operator()(double a) const {
-        if (rbf) return expm1(g2 * a);
+        if (rbf) {
+            const double u = g2 * a;
+            if (PLSSVM_MI_PHI_POLY && fabs(u) < 0x1p-7) {
+                double p = 1.0 / 5040.0;
+                p = fma(p, u, 1.0 / 720.0);
+                p = fma(p, u, 1.0 / 120.0);
+                p = fma(p, u, 1.0 / 24.0);
+                p = fma(p, u, 1.0 / 6.0);
+                p = fma(p, u, 0.5);
+                p = fma(p, u, 1.0);
+                return p * u;
+            }
+            return expm1(u);
+        }
         double h = 0.0;
         for (int k = deg; k >= 1; --k) h = (h + bin[k]) * a;
         return h;
