@@ -582,3 +582,46 @@ def test_expansion_dot2_equals_fma_path(oracle, rows, monkeypatch):
     assert err.max() <= 2.0 ** -20, err.max()
     info = check_sparse_kp(oracle, csr, "rbf", np.float32, algo="expansion")
     assert info["exp_hbytes"] == 2
+
+
+@pytest.mark.parametrize("kernel,dtype,algo,fp22", [("rbf", np.float32, "expansion", False), ("rbf", np.float32, "expansion", True),
+                                                    ("rbf", np.float64, "expansion", False),
+                                                    ("polynomial", np.float64, "pattern", False),
+                                                    ("rbf", np.float32, "onthefly", False), ("rbf", np.float64, "dense", False),
+                                                    ("linear", np.float64, "auto", False), ("linear", np.float32, "auto", True)])
+def test_csc_device_equals_host(kernel, dtype, algo, fp22, monkeypatch):
+    """The setup's CSC (colptr, rows ascending per column, values, each CSR entry's CSC position) sorted on the device
+    (the default: a stable radix sort by column) and by the host counting sort (PLSSVM_MI_CSC=host, the path for
+    nnz >= 2^31): the same arrays, so every structure built from them and every K·p is bit for bit the same —
+    on a ragged set with empty rows, empty columns and one long row, for every sparse path (kernel expansion with
+    its row join, the Gram pattern's column join and its incidence split, on the fly, densified, factored linear
+    SELL plans) and FP22 input."""
+    n, d = 4000, 1500
+    rng = np.random.default_rng(29)
+    rows = []
+    for i in range(n):
+        k = 0 if i % 97 == 5 else (200 if i == 1234 else int(rng.integers(1, 30)))
+        cols = np.sort(rng.choice(d - 100, size=k, replace=False)) if k else np.zeros(0, np.int64)  # columns >= 1400 empty
+        rows.append(cols)
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    rowptr[1:] = np.cumsum([len(c) for c in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    val = rng.uniform(0.05, 1.0, col.size)
+    csr = (rowptr, col, val, n, d)
+    m = n - 1
+    x = np.random.default_rng(7).uniform(1, 2, m).astype(dtype)
+    out = {}
+    for where in ("device", "host"):
+        if where == "host":
+            monkeypatch.setenv("PLSSVM_MI_CSC", "host")
+        else:
+            monkeypatch.delenv("PLSSVM_MI_CSC", raising=False)
+        with sparse_svm(csr, kernel, dtype, fp22=fp22, algo=algo) as svm:
+            svm.setup_data_on_device()
+            svm.generate_q()
+            info = svm.info()
+            ret = np.zeros(m, dtype=dtype)
+            svm.run_device_kernel(None, ret, x, 1.0)
+            out[where] = (ret, info["sparse_algo"], info["pairs"], info["pair_slots"])
+    np.testing.assert_array_equal(out["device"][0], out["host"][0])
+    assert out["device"][1:] == out["host"][1:]
