@@ -522,12 +522,14 @@ __global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__
             double a = 0.0, pa = 0.0;
             bool hit = false;
             if (k < ke) {
+                // the value is loaded with the feature (one latency per partner, not a second one after the probe)
                 const int32_t f = col[k];
+                const T vk = val[k];
                 int h = rj_hash(f);
                 int32_t key;
                 while ((key = hkey[h]) >= 0 && key != f) h = (h + 1) & (RJ_HS - 1);
                 if (key == f) {
-                    a = (double) zval[hidx[h]] * (double) val[k];
+                    a = (double) zval[hidx[h]] * (double) vk;
                     pa = phi(a);
                     hit = true;
                 }
