@@ -112,6 +112,43 @@ __global__ __launch_bounds__(256) void csc_gather_kernel(const int32_t *__restri
     cpos[k] = q;
 }
 
+// packed FP22 words -> the context's real type (fp22_get: the host decoding, bit for bit)
+template <typename T>
+__global__ __launch_bounds__(256) void fp22_unpack_kernel(const uint32_t *__restrict__ words, int64_t n, T *__restrict__ out) {
+    const int64_t k = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) out[k] = (T) fp22_get(words, k);
+}
+
+// max_k x_k^2 and max_i sum_{k in row i} x_k^2 (double; each row's sum in entry order, separate multiply and add as
+// on the host), as the bits of non-negative doubles (ordered like the values): mx[0], mx[1]
+template <typename T>
+__global__ __launch_bounds__(256) void csr_maxsq_kernel(const int64_t *__restrict__ rowptr, const T *__restrict__ val,
+                                                        int64_t m, unsigned long long *__restrict__ mx) {
+#pragma clang fp contract(off)
+    __shared__ double red[2][4];
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    double am = 0.0, nrm = 0.0;
+    if (i < m)
+        for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+            const double x = (double) val[k];
+            const double x2 = x * x;
+            am = fmax(am, x2);
+            nrm = nrm + x2;
+        }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        am = fmax(am, __shfl_xor(am, o));
+        nrm = fmax(nrm, __shfl_xor(nrm, o));
+    }
+    if ((threadIdx.x & 63) == 0) red[0][threadIdx.x >> 6] = am, red[1][threadIdx.x >> 6] = nrm;
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        double v = red[threadIdx.x][0];
+        for (int w = 1; w < 4; ++w) v = fmax(v, red[threadIdx.x][w]);
+        if (v > 0.0) atomicMax(mx + threadIdx.x, (unsigned long long) __double_as_longlong(v));
+    }
+}
+
 // incidences of each block of rb rows: sum over its entries of #{ earlier rows in the entry's column }
 // (integers: exact in any order)
 __global__ __launch_bounds__(256) void csc_inc_rb_kernel(const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
@@ -720,11 +757,14 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     // stays packed only where the K·p streams feature values (the factored-linear SELL stream)
     csr.val.alloc(std::max<int64_t>(nnz, 1), stream);
     if (nnz && val_fmt == PLSSVM_MI_VAL_FP22) {
-        std::vector<T> dec((size_t) nnz);
-        host_parallel(nnz, [&](int, int64_t k0, int64_t k1) {
-            for (int64_t k = k0; k < k1; ++k) dec[(size_t) k] = hval(k);
-        });
-        MI_HIP_CHECK(hipMemcpyAsync(csr.val.get(), dec.data(), sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice, stream));
+        // the packed words cross PCIe (2.75 B per value) and are decoded on the device (fp22_get, as on the host)
+        const int64_t nw = fp22_words(nnz);
+        dev_buf<uint32_t> w22;
+        w22.alloc(nw, stream, false);
+        MI_HIP_CHECK(hipMemcpyAsync(w22.get(), val, sizeof(uint32_t) * (size_t) nw, hipMemcpyHostToDevice, stream));
+        hipLaunchKernelGGL(fp22_unpack_kernel<T>, dim3((unsigned) ceil_div(nnz, 256)), dim3(256), 0, stream, w22.get(), nnz,
+                           csr.val.get());
+        MI_LAUNCH_CHECK();
         MI_HIP_CHECK(hipStreamSynchronize(stream));
     } else if (nnz) {
         MI_HIP_CHECK(hipMemcpyAsync(csr.val.get(), val, sizeof(T) * (size_t) nnz, hipMemcpyHostToDevice, stream));
@@ -761,25 +801,19 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                                     hipMemcpyDeviceToHost, stream));
         MI_HIP_CHECK(hipMemcpyAsync(crow.data(), csr.crow.get(), sizeof(int32_t) * (size_t) nnz, hipMemcpyDeviceToHost,
                                     stream));
-        // amax / nmax from the host CSR, in the host sort's order (rows ascending, each row's entries in order)
-        const int NT = (int) std::max<int64_t>(1, std::min<int64_t>(host_threads(), m / 4096 + 1));
-        std::vector<double> amax_t(NT, 0.0), nmax_t(NT, 0.0);
-        host_parallel(m, [&](int t, int64_t i0, int64_t i1) {
-            double am = 0.0, nm = 0.0;
-            for (int64_t i = i0; i < i1; ++i) {
-                double nrm = 0.0;
-                for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
-                    const double x = (double) hval(k);
-                    am = std::max(am, x * x);
-                    nrm += x * x;
-                }
-                nm = std::max(nm, nrm);
-            }
-            amax_t[(size_t) t] = std::max(amax_t[(size_t) t], am);
-            nmax_t[(size_t) t] = std::max(nmax_t[(size_t) t], nm);
-        }, NT);
-        for (int t = 0; t < NT; ++t) amax = std::max(amax, amax_t[(size_t) t]), nmax = std::max(nmax, nmax_t[(size_t) t]);
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
+        // amax / nmax on the device, each row's sum of squares in the host sort's order (entries in order, no fma)
+        {
+            dev_buf<unsigned long long> mx;
+            mx.alloc(2, stream);
+            hipLaunchKernelGGL(csr_maxsq_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream, csr.rowptr.get(),
+                               csr.val.get(), m, mx.get());
+            MI_LAUNCH_CHECK();
+            unsigned long long h[2] = { 0ull, 0ull };
+            MI_HIP_CHECK(hipMemcpyAsync(h, mx.get(), sizeof(h), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            std::memcpy(&amax, &h[0], sizeof(double));
+            std::memcpy(&nmax, &h[1], sizeof(double));
+        }
     } else {
         cpos.assign((size_t) std::max<int64_t>(nnz, 1), 0);
         crow.assign((size_t) std::max<int64_t>(nnz, 1), 0);
