@@ -289,7 +289,8 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
                                                             const int32_t *__restrict__ crow, int64_t m, int64_t r0,
                                                             int64_t *__restrict__ cnt, const int64_t *__restrict__ off8,
                                                             int32_t *__restrict__ sj, unsigned int *__restrict__ ovf,
-                                                            int pmax, int64_t cap, unsigned long long *__restrict__ cnt_max) {
+                                                            int pmax, int64_t cap, unsigned long long *__restrict__ cnt_max,
+                                                            const int64_t *__restrict__ csplit, int nsplit) {
     __shared__ uint32_t bm[RJ_BMW];
     __shared__ int32_t rep[RJ_LCAP];
     __shared__ int32_t zcol[RJ_ECAP];
@@ -336,19 +337,30 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
         // column: two binary searches per feature), not every incidence of the row once per pass
         const bool whole = R0 == 0 && R1 >= m;
         if (!whole) {
+            // a pass of the full span starts and ends where every row's passes do: the column positions come from the
+            // setup's table (one load per feature) instead of two binary searches (a chain of dependent loads)
+            const bool tab = csplit != nullptr && R0 % SPAN_MAX == 0 && (R1 >= m || R1 % SPAN_MAX == 0);
             for (int e = tid; e < ne; e += RJ_NT) {
                 const int64_t a = cst[e], b = a + (zoff[e + 1] - zoff[e]);
-                int64_t lo = a, hi = b;
-                while (lo < hi) {  // first row >= R0
-                    const int64_t mid = (lo + hi) >> 1;
-                    if (crow[mid] < R0) lo = mid + 1;
-                    else hi = mid;
-                }
-                int64_t lo2 = lo, hi2 = b;
-                while (lo2 < hi2) {  // first row >= R1
-                    const int64_t mid = (lo2 + hi2) >> 1;
-                    if (crow[mid] < R1) lo2 = mid + 1;
-                    else hi2 = mid;
+                int64_t lo = a, lo2 = b;
+                if (tab) {
+                    const int64_t *cs = csplit + (int64_t) zcol[e] * nsplit;
+                    lo = cs[R0 / SPAN_MAX];
+                    lo2 = R1 >= m ? b : cs[R1 / SPAN_MAX];
+                } else {
+                    int64_t hi = b;
+                    while (lo < hi) {  // first row >= R0
+                        const int64_t mid = (lo + hi) >> 1;
+                        if (crow[mid] < R0) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    lo2 = lo;
+                    int64_t hi2 = b;
+                    while (lo2 < hi2) {  // first row >= R1
+                        const int64_t mid = (lo2 + hi2) >> 1;
+                        if (crow[mid] < R1) lo2 = mid + 1;
+                        else hi2 = mid;
+                    }
                 }
                 pst[e] = lo;
                 pzoff[e + 1] = (int32_t) (lo2 - lo);
@@ -453,6 +465,21 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
     }
     const int64_t b0 = off8[r], b1 = off8[r + 1];
     for (int64_t k = b0 + written + tid; k < b1; k += RJ_NT) sj[k] = -1;  // pads (exp_rowjoin_h_kernel)
+}
+
+// csplit[f][p] = the first position of column f whose row is >= p x (the join's full pass span), p < nsplit
+__global__ __launch_bounds__(256) void exp_colsplit_kernel(const int64_t *__restrict__ colptr, const int32_t *__restrict__ crow,
+                                                           int64_t d, int nsplit, int64_t span, int64_t *__restrict__ csplit) {
+    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= d * nsplit) return;
+    const int64_t f = t / nsplit, R = (t % nsplit) * span;
+    int64_t lo = colptr[f], hi = colptr[f + 1];
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (crow[mid] < R) lo = mid + 1;
+        else hi = mid;
+    }
+    csplit[t] = lo;
 }
 
 // H of the row join's partners (sj from exp_rowjoin_kernel's write / slot pass; row r's entries in
@@ -1820,6 +1847,18 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
         for (int64_t r = 0; r < R && row_join; ++r) row_join = rp[(size_t) r + 1] - rp[(size_t) r] <= RJ_ECAP;
         if (row_join && csr.nnz >= (int64_t) INT32_MAX) row_join = false;  // a row's incidences <= nnz
     }
+    // the join's pass boundaries in every column (more rows than one bitmap pass: each row's full passes start at the
+    // same partner rows, p x RJ_BMW x 32, so each column's positions there are found once here)
+    dev_buf<int64_t> csplit;
+    int nsplit = 0;
+    const char *cse = std::getenv("PLSSVM_MI_EXP_COLSPLIT");  // "0": binary searches only (tests)
+    if (row_join && R > 0 && d > 0 && m > (int64_t) RJ_BMW * 32 && !(cse != nullptr && std::strcmp(cse, "0") == 0)) {
+        nsplit = (int) ceil_div(m, (int64_t) RJ_BMW * 32);
+        csplit.alloc(d * nsplit, stream, false);
+        hipLaunchKernelGGL(exp_colsplit_kernel, dim3((unsigned) ceil_div(d * nsplit, 256)), dim3(256), 0, stream,
+                           csr.colptr.get(), csr.crow.get(), d, nsplit, (int64_t) RJ_BMW * 32, csplit.get());
+        MI_LAUNCH_CHECK();
+    }
     dev_buf<int64_t> cnt, cnt8;
     dev_buf<unsigned long long> lnz;
     unsigned int ovf_h = 0u;
@@ -1872,7 +1911,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             ovf.alloc(1, stream);
             hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
                                csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(), (const int64_t *) nullptr,
-                               sj.get(), ovf.get(), rj_pmax, cap, lnz.get() + 2);
+                               sj.get(), ovf.get(), rj_pmax, cap, lnz.get() + 2, csplit.get(), nsplit);
             MI_LAUNCH_CHECK();
             unsigned long long cmax = 0ull;
             MI_HIP_CHECK(hipMemcpyAsync(&ovf_h, ovf.get(), sizeof(ovf_h), hipMemcpyDeviceToHost, stream));
@@ -1911,7 +1950,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
                                csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(),
                                (const int64_t *) nullptr, (int32_t *) nullptr, ovf.get(), rj_pmax, (int64_t) 0,
-                               (unsigned long long *) nullptr);
+                               (unsigned long long *) nullptr, csplit.get(), nsplit);
             MI_LAUNCH_CHECK();
         }
         if (R > 0) {
@@ -1939,7 +1978,8 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             if (R > 0) {
                 hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
                                    csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, cnt.get(), off8.get(), sj.get(),
-                                   (unsigned int *) nullptr, rj_pmax, (int64_t) 0, (unsigned long long *) nullptr);
+                                   (unsigned int *) nullptr, rj_pmax, (int64_t) 0, (unsigned long long *) nullptr,
+                                   csplit.get(), nsplit);
                 MI_LAUNCH_CHECK();
             }
             rbeg = off8.get();

@@ -625,3 +625,25 @@ def test_csc_device_equals_host(kernel, dtype, algo, fp22, monkeypatch):
             out[where] = (ret, info["sparse_algo"], info["pairs"], info["pair_slots"])
     np.testing.assert_array_equal(out["device"][0], out["host"][0])
     assert out["device"][1:] == out["host"][1:]
+
+
+def test_expansion_row_join_column_split_table(monkeypatch):
+    """More rows than one bitmap pass of the row join (2^20 partner rows): every row takes two passes over its
+    columns, which start at the same partner rows for every row, so the setup finds those positions in each column
+    once (exp_colsplit_kernel) instead of two binary searches per feature and pass. PLSSVM_MI_EXP_COLSPLIT=0 keeps
+    the searches: the same pairs and bit for bit the same K·p (1.1M rows x 20k features, 4 per row)."""
+    csr, _ = datagen.sparse_csr(1_100_001, 20000, 4, seed=41, dtype=np.float32)
+    m = csr[3] - 1
+    x = np.random.default_rng(9).uniform(1, 2, m).astype(np.float32)
+    out = {}
+    for mode in ("table", "search"):
+        if mode == "search":
+            monkeypatch.setenv("PLSSVM_MI_EXP_COLSPLIT", "0")
+        else:
+            monkeypatch.delenv("PLSSVM_MI_EXP_COLSPLIT", raising=False)
+        with sparse_svm(csr, "rbf", np.float32, algo="expansion") as svm:
+            svm.setup_data_on_device()
+            info = svm.info()
+            out[mode] = (svm.kp_part(x, "overlap"), info["pairs"], info["pair_slots"])
+    assert out["table"][1:] == out["search"][1:] and out["table"][1] > 0
+    np.testing.assert_array_equal(out["table"][0], out["search"][0])
