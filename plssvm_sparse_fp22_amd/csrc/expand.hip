@@ -492,8 +492,11 @@ __global__ __launch_bounds__(256) void exp_colsplit_kernel(const int64_t *__rest
 constexpr int RJH_NT = 256;
 constexpr int RJ_HS = 2048;  // hash slots for row i's features (<= RJ_ECAP keys)
 __device__ __forceinline__ int rj_hash(int32_t f) { return (int) (((uint32_t) f * 2654435761u) >> (32 - 11)); }
+#ifndef RJH_WPE
+#define RJH_WPE 8  // waves per SIMD the H kernel is compiled for (<= 64 VGPRs: 8 resident 256-thread workgroups per CU)
+#endif
 template <typename T>
-__global__ __launch_bounds__(RJH_NT) void exp_rowjoin_h_kernel(const int64_t *__restrict__ rowptr,
+__global__ __launch_bounds__(RJH_NT) __attribute__((amdgpu_waves_per_eu(RJH_WPE, RJH_WPE))) void exp_rowjoin_h_kernel(const int64_t *__restrict__ rowptr,
                                                                const int32_t *__restrict__ col,
                                                                const T *__restrict__ val, int64_t r0, phi_fn phi,
                                                                double kbase, const int64_t *__restrict__ rbeg,

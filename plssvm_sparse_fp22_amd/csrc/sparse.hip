@@ -1046,6 +1046,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                             MI_HIP_CHECK(hipSetDevice(device));
                             MI_HIP_CHECK(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
                             need_cval_h(ps);
+                            tp.mark("setup_csr: (plans thread) CSC values to the host");
                             build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0,
                                                rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22, csc_gen(csr.csc_r0, csr.csc_r1),
                                                blocks, ps, 0, 1, csr.ex.KM);

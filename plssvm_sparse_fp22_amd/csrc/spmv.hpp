@@ -432,6 +432,7 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
     pl.nseg = nseg;
     pl.nnz = nnz;
     if (nseg <= 0) return;
+    phase_timer pt;
     const int64_t Wmax = sell_width<T>() / xch;
     const int64_t P_lds = std::max<int64_t>(1, ceil_div(std::max<int64_t>(xn, 1), Wmax));
     bool ldsx = P_lds * (nseg + 1) * 2 <= std::max<int64_t>(nnz, 1);
@@ -446,6 +447,7 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
     host_parallel(nseg, [&](int, int64_t s0, int64_t s1) {
         gen([&](int64_t s, int64_t g, double) { ++len[(size_t) ((g / W) * nseg + s)]; }, s0, s1);
     });
+    pt.mark("  SELL plan: segment lengths");
     // per panel: sort windows by length (descending, stable), deal 64 slots per chunk
     const int64_t slots_per_panel = round_up(nseg, 64);
     const int64_t nch_per_panel = slots_per_panel / 64;
@@ -484,6 +486,7 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
             off += (int64_t) width * 64;
         }
     }
+    pt.mark("  SELL plan: order + chunks");
     pl.entries = off;
     pl.nchunks = (int64_t) chunks.size();
     pl.nchp = nch_per_panel;
@@ -514,7 +517,9 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
             else vr[tv] = (T) v;
         }, s0, s1);
     });
+    pt.mark("  SELL plan: fill");
     const std::vector<uint32_t> v22 = fp22 ? fp22_pack_host(vf) : std::vector<uint32_t>{};
+    pt.mark("  SELL plan: FP22 pack");
     // blocks: target_blocks contiguous chunk ranges of equal cost (entries + a per-chunk charge for its
     // descriptor, slot map and output) over the panel-major chunk sequence; a range may cross panels
     constexpr int64_t CHUNK_COST = 8 * 64;
@@ -550,6 +555,7 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
     up(pl.bchunk, bchunk);
     if (P > 1) pl.partial.alloc(P * nseg * och, stream, false);
     MI_HIP_CHECK(hipStreamSynchronize(stream));
+    pt.mark("  SELL plan: blocks + upload");
 }
 
 // ---- row-block CSR pass with the CG finalize fused (factored sparse linear, one GPU) ------------------
