@@ -2056,9 +2056,14 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             ex.RB = (int) std::min<int64_t>(want, ex.RBB / es);
         } else {
             ex.RBB = 32768;
-            const int64_t nI = ceil_div(Rr, cap_max);
-            ex.RB = (int) round_up(ceil_div(Rr, nI), (int64_t) EXP_NWV);
+            int64_t nI = ceil_div(Rr, cap_max);
             ex.G = (int) std::max<int64_t>(1, cus / nI);
+#ifndef PLSSVM_MI_EXP_FILLCU
+#define PLSSVM_MI_EXP_FILLCU 1
+#endif
+            // as many row blocks as the G window groups leave CUs (3-RBF: 128 x 2 = 256 workgroups, not 123 x 2)
+            if (PLSSVM_MI_EXP_FILLCU) nI = std::max<int64_t>(nI, cus / ex.G);
+            ex.RB = (int) round_up(ceil_div(Rr, nI), (int64_t) EXP_NWV);
         }
         if (const char *e = std::getenv("PLSSVM_MI_EXP_RBB")) {
             const int v = std::atoi(e);
