@@ -202,8 +202,7 @@ __global__ __launch_bounds__(CG_NT) void cg_upd_rr_kernel(T *__restrict__ x, T *
         const int64_t i = i0 + e * st;
         if (i < m) xv[e] = x[i], dv[e] = d[i], av[e] = reset ? b[i] : Ad[i], rv[e] = reset ? T(0) : r[i];
     }
-    T dAd, unused;
-    partials_total(pdad, G, red, bc, dAd, unused);
+    const T dAd = partials_total1(pdad, G, red, bc);
     const T delta = sc->delta;
     const T alpha = delta / dAd;
     if (blockIdx.x == 0 && threadIdx.x == 0) sc->dAd = dAd, sc->alpha = alpha, sc->delta_prev = delta;
@@ -226,7 +225,7 @@ __global__ __launch_bounds__(CG_NT) void cg_upd_rr_kernel(T *__restrict__ x, T *
         if (i < m) one(i, xv[e], dv[e], av[e], rv[e]);
     }
     for (int64_t i = i0 + CG_PRE * st; i < m; i += st) one(i, x[i], d[i], reset ? b[i] : Ad[i], reset ? T(0) : r[i]);
-    if (!reset) store_partials(s1, T(0), red, prr);
+    if (!reset) store_partial1(s1, red, prr);
 }
 
 template <typename T>
@@ -245,8 +244,7 @@ __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, c
     }
     T beta = 0;
     if (!init) {
-        T rr, unused;
-        partials_total(prr, G, red, bc, rr, unused);
+        const T rr = partials_total1(prr, G, red, bc);
         const bool conv = rr <= sc->eps2delta0;
         beta = rr / sc->delta_prev;
         if (blockIdx.x == 0 && threadIdx.x == 0) {  // FIN_DELTA of dot_final_kernel

@@ -54,6 +54,29 @@ __device__ __forceinline__ void partials_total(const T *__restrict__ partials, i
     r2 = block_sum_all(s2, red, bc);
 }
 
+// partials_total's first sum only (producers whose second partial is zero: d.Ad, r.r) — the same bits for r1,
+// one block reduction fewer
+template <typename T>
+__device__ __forceinline__ T partials_total1(const T *__restrict__ partials, int G, T *red, T *bc) {
+    T s1 = 0;
+    for (int i = threadIdx.x; i < RED_BLOCKS; i += blockDim.x) {
+        T a = partials[i];
+        for (int g = 1; g < G; ++g) a += partials[g * 2 * RED_BLOCKS + i];
+        s1 += a;
+    }
+    return block_sum_all(s1, red, bc);
+}
+
+// store_partials(v1, 0): the second partial of the pair is zero
+template <typename T>
+__device__ __forceinline__ void store_partial1(T v1, T *red, T *__restrict__ partials) {
+    const T r1 = block_sum(v1, red);
+    if (threadIdx.x == 0) {
+        partials[blockIdx.x] = r1;
+        partials[RED_BLOCKS + blockIdx.x] = T(0);
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ void store_partials(T v1, T v2, T *red, T *__restrict__ partials) {
     const T r1 = block_sum(v1, red);
