@@ -785,15 +785,28 @@ __global__ __launch_bounds__(256) void exp_wown_kernel(const T *__restrict__ e, 
     if (status != nullptr && status->converged) return;
     __shared__ T red[4];
     T s1 = 0;
-    for (int64_t i = ib + (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < ie; i += (int64_t) gridDim.x * blockDim.x) {
-        T v = p[i];
+    const int64_t st = (int64_t) gridDim.x * blockDim.x;
+    auto one = [&](int64_t i, T v, T ev) {
         if (e != nullptr) {
-            v = e[i] * v;
+            v = ev * v;
             w[i] = v;
         }
         s1 += v;
         w16[i] = bf16_rne((float) v);
+    };
+    int64_t i = ib + (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    // four elements' loads in flight per thread, then summed in the thread's element order (the one-at-a-time bits)
+    for (; i + 3 * st < ie; i += 4 * st) {
+        T pv[4], ev[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            pv[u] = p[i + u * st];
+            ev[u] = e != nullptr ? e[i + u * st] : T(1);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) one(i + u * st, pv[u], ev[u]);
     }
+    for (; i < ie; i += st) one(i, p[i], e != nullptr ? e[i] : T(1));
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) s1 += __shfl_xor(s1, o);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s1;
