@@ -185,7 +185,7 @@ __global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__
         if (i < m) one(i, rw[e], qv[e], dv[e]);
     }
     for (int64_t i = i0 + CG_PRE * st; i < m; i += st) one(i, load_raw(i), q[i], d[i]);
-    store_partials(s1, T(0), red, pdad);
+    store_partial1(s1, red, pdad);
 }
 
 template <typename T>

@@ -1508,7 +1508,7 @@ __global__ __launch_bounds__(cgk::CG_NT) void exp_combine_fin_kernel(
         Ad[i] = v;
         s1 = cgk::cg_acc(s1, di, v);
     }
-    cgk::store_partials(s1, T(0), red, pdad);
+    cgk::store_partial1(s1, red, pdad);
 }
 
 template <typename T>
