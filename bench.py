@@ -171,7 +171,7 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
         log(f"[rank {rank}] {name}: learn at eps 1e-3: setup {t_setup:.2f}s + q {t_q:.3f}s + CG {it} iterations "
             f"{t_cg:.3f}s (converged: {conv})")
     svm.close()
-    roof = roofline(cfg, info, n, d, share, ms_dom, extra)
+    roof = roofline(cfg, info, n, d, share, ms_dom, extra, ms_kp)
     dts = "f64" if dt == np.float64 else "f32"
     tkey = name + (f"_sim{sim[0]}of{sim[1]}" if sim else "")
     hs = roof.get("h_storage")
@@ -319,7 +319,16 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(cfg, info, n, d, world, ms_dom, extra):
+def kp_whole(streams, m, es, world, ms_kp):
+    """The whole K·p against HBM: the bytes every kernel of one K·p must stream — the dominant
+    stream(s) + the SELL passes' streams + the O(m) vectors (p read, the result written, e read: 3 m sizeof(real)
+    per rank share) — over the whole K·p's time (time_kp: kp_device back to back, finalize included)."""
+    b = streams + 3.0 * m * es / world
+    return dict(kp_bytes=b, kp_ms=ms_kp, kp_GBps=b / (ms_kp * 1e-3) / 1e9, kp_frac=b / (ms_kp * 1e-3) / PEAKS["hbm"],
+                kp_bytes_def="dominant stream + SELL pass streams (spmv_bytes) + 3 m sizeof(real) of vectors")
+
+
+def roofline(cfg, info, n, d, world, ms_dom, extra, ms_kp=None):
     kernel, _, _, dtype, layout, _, _ = cfg
     m = n - 1
     s = ms_dom * 1e-3
@@ -341,10 +350,13 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
             alg = (2 * (nnz * (4 + es) + (m + 1) * 8) + 4 * m * es + 2 * d * es) / world
             kname = "sell_spmv_kernel*2+panel_reduce_kernel*2"  # CSC pass + CSR pass
             moved = info["spmv_bytes"]  # what the two SELL passes actually stream (16-bit panel indices)
-            return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
-                        frac=alg / s / PEAKS["hbm"], traffic=None, kernel=kname, launch_ms=ms_dom, alg_bytes=alg,
-                        stream_bytes_per_launch=moved, stream_GBps=moved / s / 1e9,
-                        stream_frac=moved / s / PEAKS["hbm"])  # on the bytes the passes move
+            r = dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
+                     frac=alg / s / PEAKS["hbm"], traffic=None, kernel=kname, launch_ms=ms_dom, alg_bytes=alg,
+                     stream_bytes_per_launch=moved, stream_GBps=moved / s / 1e9,
+                     stream_frac=moved / s / PEAKS["hbm"])  # on the bytes the passes move
+            if ms_kp:
+                r.update(kp_whole(moved, m, es, world, ms_kp))
+            return r
         return dict(bound="hbm", achieved=alg / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
                     frac=alg / s / PEAKS["hbm"], traffic=None, kernel=kname, launch_ms=ms_dom, alg_bytes=alg)
     # sparse Gram pattern (poly / rbf): SURVEY §8(d) 3-RBF / 5 figure, this rank's share of the pairs
@@ -361,7 +373,8 @@ def roofline(cfg, info, n, d, world, ms_dom, extra):
         # the stored row index: 2 B per 4-slot chunk in the indexed layout (exp_layout 1); none with row-start
         # flags (2: the dummies of empty cells are in pair_slots) or runs (3)
         rem = info["pair_slots"] * (2 + hb) + (info["exp_chunks"] * 2 if info["exp_layout"] == 1 else 0)
-        return dict(bound="hbm", achieved=rem / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
+        whole = kp_whole(rem + info["spmv_bytes"], m, es, world, ms_kp) if ms_kp else {}
+        return dict(**whole, bound="hbm", achieved=rem / s / 1e9, peak=PEAKS["hbm"] / 1e9, unit="GB/s",
                     frac=rem / s / PEAKS["hbm"], traffic=None, kernel="exp_hcell_kernel", launch_ms=ms_dom,
                     alg_bytes=rem, alg_bytes_def="remainder stream: slots x (2 + bytes per stored H) + chunks x 2 (run layout: chunks = 0, slots = entries + dummies)",
                     h_storage="bfloat16 (precision bound, DESIGN §5.1.2)" if hb == 2 else f"real ({hb} B)",

@@ -260,6 +260,10 @@ typedef struct {
     int exp_layout;     /* kernel expansion: remainder stream layout — 1 = 4-slot chunks with a stored row index per
                            chunk, 2 = 4-slot chunks whose rows are numbered by row-start flags (no row index),
                            3 = runs (no padding); 0 = no expansion */
+    int exp_dot2;       /* kernel expansion, bfloat16 H: 1 = the remainder's chunk products run on the v_dot2_f32_bf16
+                           kernel (built with EXP_DOT2 and selected: PLSSVM_MI_EXP_DOT2 != 0), 0 = the FMA chain */
+    int centered;       /* kernel expansion: 1 = the finalize forms Q~'s rank-1 terms in the centered form
+                           (engine.hpp ctr_*; PLSSVM_MI_CTR=0 or a caller's own q vector: 0) */
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
 

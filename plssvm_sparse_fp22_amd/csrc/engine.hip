@@ -379,6 +379,8 @@ void engine<T>::finish_setup() {
     MI_HIP_CHECK(hipStreamSynchronize(stream));
     have_data = true;
     have_q = false;
+    q_gen = false;
+    ctr_ok = false;
     cg_active = false;
     graph_reset();
 }
@@ -403,12 +405,17 @@ void engine<T>::generate_q(T *q_out, double *qa_out) {
     } else {
         launch_q_dense<T>(kf(), XT.get(), n_pad, d, m, xlast.get(), q.get(), stream);
     }
-    QA_cost = host_kernel<T>(kernel, degree, gamma, coef0, xlast_h.data(), xlast_h.data(), d) + T(1) / cost;
-    if (q_out && m > 0)
-        MI_HIP_CHECK(hipMemcpyAsync(q_out, q.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
+    ctr_kmm = host_kernel<T>(kernel, degree, gamma, coef0, xlast_h.data(), xlast_h.data(), d);
+    QA_cost = ctr_kmm + T(1) / cost;
+    q_gen_h.resize((size_t) std::max<int64_t>(m, 0));
+    if (m > 0) MI_HIP_CHECK(hipMemcpyAsync(q_gen_h.data(), q.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
     MI_HIP_CHECK(hipStreamSynchronize(stream));
+    if (q_out && m > 0) std::memcpy(q_out, q_gen_h.data(), sizeof(T) * (size_t) m);
     if (qa_out) *qa_out = (double) QA_cost;
     have_q = true;
+    q_gen = true;
+    if (sparse) ctr_setup();
+    graph_reset();
 }
 
 template <typename T>
@@ -419,6 +426,8 @@ void engine<T>::set_q(const T *q_host) {
         return;
     }
     if (m > 0) MI_HIP_CHECK(hipMemcpyAsync(q.get(), q_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
+    // a caller's q equal to the generated one keeps the centered finalize; any other q is used as given
+    q_gen = (int64_t) q_gen_h.size() == m && (m == 0 || std::memcmp(q_host, q_gen_h.data(), sizeof(T) * (size_t) m) == 0);
     if (!have_q) {
         QA_cost = host_kernel<T>(kernel, degree, gamma, coef0, xlast_h.data(), xlast_h.data(), d) + T(1) / cost;
         have_q = true;
@@ -432,11 +441,13 @@ void engine<T>::kp_device(const T *p, T *out, T add, bool overwrite, const cg_sc
     cg_scalars<T> *scp = sc.get();
     // sum(p) and sum(q p): the rank-1 parts of Q~ (QA_cost - q_i - q_j) never enter the tiles (sharded: this
     // rank's rows, then the gathered partials of all ranks)
-    launch_dot2<T>(p + v0, nullptr, q.get() + v0, p + v0, vn, red.get(), status, stream);
+    launch_dot2<T>(p + v0, nullptr, qf() + v0, p + v0, vn, red.get(), status, stream);
     launch_dot_final<T>(gather_partials(red.get(), 3), scp, FIN_SP_SQP, 0, nullptr, 0, nullptr, stream, G);
+    ctr_now = ctr_active();
     kp_raw(p, status);
+    ctr_now = false;
     const int flags = (overwrite ? 1 : 0) | ((sim_world > 0 && sim_rank != 0 && !shard) ? 2 : 0);
-    launch_kp_finalize<T>(raw.get() + v0, q.get() + v0, p + v0, scp, QA_cost, cost_inv(), add, flags, vn, out + v0,
+    launch_kp_finalize<T>(raw.get() + v0, qf() + v0, p + v0, scp, QAf(), cost_inv(), add, flags, vn, out + v0,
                           status, stream);
 }
 
@@ -520,7 +531,7 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
     launch_dot2<T>(r.get() + v0, r.get() + v0, nullptr, nullptr, vn, red.get(), nullptr, stream);
     launch_dot_final<T>(gather_partials(red.get(), 3), sc.get(), FIN_DELTA0, 0, trace.get(), trace_cap, nullptr, stream, G);
     // d = r, with sum d / sum q d for the first Q~d
-    launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, q.get() + v0, nullptr, 1, 1, nullptr, 0, vn, cgp.get(), sc.get(),
+    launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, qf() + v0, nullptr, 1, 1, nullptr, 0, vn, cgp.get(), sc.get(),
                           stream);
     if (gathered && comm != nullptr) psum_pending = true;  // gathered with the first K·p's collective
     else gather_partials(cgp.get(), 0);
@@ -561,17 +572,19 @@ void engine<T>::cg_iter(int reset) {
         slabs = csr.spmv_csr.partial.get();
         P = csr.spmv_csr.P;
     } else {
-        const kp_fin_t fin{ q.get(), dv.get(), psum_in, G, QA_cost, cost_inv(), Ad.get(), pdad };
+        const kp_fin_t fin{ qf(), dv.get(), psum_in, G, QAf(), cost_inv(), Ad.get(), pdad };
         kp_fin_req = raw_only ? nullptr : &fin;
         kp_fin_done = false;
+        ctr_now = ctr_active();
         kp_raw(dv.get(), st);
+        ctr_now = false;
         kp_fin_req = nullptr;
     }
     flush_psum();  // no collective of the K·p carried it
     if (kp_fin_done) {
         kp_fin_done = false;  // the K·p's last kernel formed Ad and the d.Ad partials
     } else if (!(sparse_stored() && factored() && world == 1 && sim_world == 0 && csr.rb_csr.nblk > 0)) {
-        launch_cg_fin_dad<T>(raw.get() + v0, slabs, P, m, q.get() + v0, dv.get() + v0, psum_in, G, QA_cost, cost_inv(),
+        launch_cg_fin_dad<T>(raw.get() + v0, slabs, P, m, qf() + v0, dv.get() + v0, psum_in, G, QAf(), cost_inv(),
                              raw_only, vn, Ad.get() + v0, pdad, sc.get(), stream);
     }
     // x += alpha d; r = b - Q~x every 50th iteration, else r -= alpha Ad   (:119-132)
@@ -582,7 +595,7 @@ void engine<T>::cg_iter(int reset) {
         launch_dot2<T>(r.get() + v0, r.get() + v0, nullptr, nullptr, vn, prr, st, stream);
     }
     // delta = r.r ; stop test ; beta (:135-146); d = beta d + r (:149-151), with sum d / sum q d
-    launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, q.get() + v0, gather_partials(prr, 2), G, 0, trace.get(), trace_cap,
+    launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, qf() + v0, gather_partials(prr, 2), G, 0, trace.get(), trace_cap,
                           vn, psum, sc.get(), stream);
     if (gathered && comm != nullptr) psum_pending = true;  // gathered with the next K·p's first collective
     else gather_partials(psum, 0);

@@ -29,6 +29,7 @@ inline ncclDataType_t nccl_type() {
         }                                                                                                            \
     } while (0)
 
+int exp_dot2_built();  // expand.hip: 1 if the bfloat16 remainder's dot-instruction kernel was compiled (EXP_DOT2)
 void partition_superblocks(int64_t nb, int rank, int world, int64_t &s0, int64_t &s1, int64_t &s_total,
                            int64_t &tiles_total, int64_t &tiles_local);
 
@@ -119,6 +120,24 @@ struct engine : engine_base {
     };
     const kp_fin_t *kp_fin_req = nullptr;
     bool kp_fin_done = false;
+    // Centered rank-1 terms (round 5, kernel expansion): with k_ij = a_i a_j (kappa' + phi_ij) (rbf: a = e, kappa' = 1;
+    // poly: a = 1, phi = c, the kappa terms cancel exactly) the finalize's QA_cost - q_i - q_j + the separable part
+    // is (a_i - a_m)(a_j - a_m) kappa' - h_i - h_j + h_m with h_i = a_i a_m phi(x_i . x_m): the same Q~, but formed
+    // from small quantities instead of O(1) kernel values that cancel to O(gamma |x|^2) — in fp32 the naive sum loses
+    // ~log10(1 / (gamma |x|^2)) digits per K·p (tests/long_trace_cases.py). Inside a finalize-bound K·p the combine's
+    // base is c_i S_c (c = a - a_m, S_c = sum_j cw_j w_j, cw = c / e) and the finalize runs with q -> h,
+    // QA_cost -> h_m + 1/C (+ any difference of a caller's QA_cost from k_mm + 1/C).
+    dev_buf<T> ctr_c, ctr_cw, ctr_h;
+    double ctr_hm = 0;
+    T ctr_kmm = 0;         // k(x_m, x_m) as generate_q's QA_cost has it
+    bool ctr_ok = false;   // the vectors are built and finite (PLSSVM_MI_CTR=0: never)
+    bool q_gen = false;    // the device q is the engine's own k(x_i, x_m)
+    bool ctr_now = false;  // set by kp_device / cg_iter around their K·p: the expansion drops its separable base
+    std::vector<T> q_gen_h;
+    bool ctr_active() const;
+    const T *qf() const { return ctr_active() ? ctr_h.get() : q.get(); }
+    T QAf() const;
+    void ctr_setup();
     cg_scalars<T> polled{};               // the CG scalars read by the last cg_step poll
     // plssvm_mi_set_progress: called by solve_cg after each polled batch of iterations
     void (*progress)(int64_t, int64_t, const double *, double, double, void *) = nullptr;

@@ -750,17 +750,19 @@ __device__ __forceinline__ uint16_t bf16_rne(float f) {
     return (uint16_t) (u >> 16);
 }
 
-// S = sum_j w_j as RED_BLOCKS block partials in dot2_kernel's grid, order and block reduction (bitwise the
-// same partials), writing the remainder stream's bfloat16 copy of w on the way (w16 non-null: hbf16 layouts)
+// S = sum_j w_j (cw non-null: the centered S_c = sum_j cw_j w_j, engine.hpp ctr_*) as RED_BLOCKS block partials
+// in dot2_kernel's grid, order and block reduction (bitwise the same partials), writing the remainder stream's
+// bfloat16 copy of w on the way (w16 non-null: hbf16 layouts)
 template <typename T>
 __global__ __launch_bounds__(256) void exp_wsum_kernel(const T *__restrict__ w, int64_t n, uint16_t *__restrict__ w16,
-                                                       T *__restrict__ partials, const cg_scalars<T> *__restrict__ status) {
+                                                       const T *__restrict__ cw, T *__restrict__ partials,
+                                                       const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
     __shared__ T red[4];
     T s1 = 0;
     for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x) {
         const T v = w[i];
-        s1 += v;
+        s1 += cw != nullptr ? cw[i] * v : v;
         if (w16 != nullptr) w16[i] = bf16_rne((float) v);
     }
 #pragma unroll
@@ -778,35 +780,38 @@ __global__ __launch_bounds__(256) void exp_wsum_kernel(const T *__restrict__ w, 
 // sharded groups with bfloat16 windows: the rank's rows only — w_i = e_i p_i (rbf; e null: w = p, nothing
 // written), its bfloat16 copy, and the rows' share of S = sum_j w_j as RED_BLOCKS block partials (gathered
 // with the group's other partials and summed in rank order: the same S on every rank)
+// (cw non-null: the rows' share of the centered S_c = sum_j cw_j w_j instead, engine.hpp ctr_*)
 template <typename T>
 __global__ __launch_bounds__(256) void exp_wown_kernel(const T *__restrict__ e, const T *__restrict__ p, int64_t ib,
                                                        int64_t ie, T *__restrict__ w, uint16_t *__restrict__ w16,
-                                                       T *__restrict__ partials, const cg_scalars<T> *__restrict__ status) {
+                                                       const T *__restrict__ cw, T *__restrict__ partials,
+                                                       const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
     __shared__ T red[4];
     T s1 = 0;
     const int64_t st = (int64_t) gridDim.x * blockDim.x;
-    auto one = [&](int64_t i, T v, T ev) {
+    auto one = [&](int64_t i, T v, T ev, T cv) {
         if (e != nullptr) {
             v = ev * v;
             w[i] = v;
         }
-        s1 += v;
+        s1 += cw != nullptr ? cv * v : v;
         w16[i] = bf16_rne((float) v);
     };
     int64_t i = ib + (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     // four elements' loads in flight per thread, then summed in the thread's element order (the one-at-a-time bits)
     for (; i + 3 * st < ie; i += 4 * st) {
-        T pv[4], ev[4];
+        T pv[4], ev[4], cv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             pv[u] = p[i + u * st];
             ev[u] = e != nullptr ? e[i + u * st] : T(1);
+            cv[u] = cw != nullptr ? cw[i + u * st] : T(0);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) one(i + u * st, pv[u], ev[u]);
+        for (int u = 0; u < 4; ++u) one(i + u * st, pv[u], ev[u], cv[u]);
     }
-    for (; i < ie; i += st) one(i, p[i], e != nullptr ? e[i] : T(1));
+    for (; i < ie; i += st) one(i, p[i], e != nullptr ? e[i] : T(1), cw != nullptr ? cw[i] : T(0));
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) s1 += __shfl_xor(s1, o);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s1;
@@ -1433,8 +1438,10 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *_
 // panel order — panel_reduce_kernel's sum, bit for bit, without its launch
 // one row of the combine (rows [r0, r1)): the body of exp_combine_kernel, shared with the fused combine +
 // CG finalize so both compile the same arithmetic
+// cb non-null: the centered base cb_i S (engine.hpp ctr_*) in place of e_i S / kappa S
 template <typename T>
-__device__ __forceinline__ T exp_combine_row(const T *__restrict__ e, const T *__restrict__ w, const T *__restrict__ hdiag,
+__device__ __forceinline__ T exp_combine_row(const T *__restrict__ e, const T *__restrict__ cb, const T *__restrict__ w,
+                                             const T *__restrict__ hdiag,
                                              const T *__restrict__ phin, const T *__restrict__ hs,
                                              const T *__restrict__ hslab, int G, const T *__restrict__ jslab, int P,
                                              const T *__restrict__ raw, const T *__restrict__ ssc, T kappa, int64_t i,
@@ -1459,14 +1466,16 @@ __device__ __forceinline__ T exp_combine_row(const T *__restrict__ e, const T *_
     if (overlap_only) {
         v = sc * (t - (double) phin[i] * wi);
     } else {
-        const double base = (e != nullptr ? (double) e[i] : (double) kappa) * (double) ssc[0];
+        const double base =
+            (cb != nullptr ? (double) cb[i] : e != nullptr ? (double) e[i] : (double) kappa) * (double) ssc[0];
         v = base + sc * t;
     }
     return (T) v;
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ e, const T *__restrict__ w,
+__global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ e, const T *__restrict__ cb,
+                                                          const T *__restrict__ w,
                                                           const T *__restrict__ hdiag, const T *__restrict__ phin,
                                                           const T *__restrict__ hs, const T *__restrict__ hslab, int G,
                                                           const T *__restrict__ jslab, int P,
@@ -1480,7 +1489,7 @@ __global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ 
         raw[i] = T(0);
         return;
     }
-    raw[i] = exp_combine_row<T>(e, w, hdiag, phin, hs, hslab, G, jslab, P, raw, ssc, kappa, i, r0, r1, overlap_only);
+    raw[i] = exp_combine_row<T>(e, cb, w, hdiag, phin, hs, hslab, G, jslab, P, raw, ssc, kappa, i, r0, r1, overlap_only);
 }
 
 // the combine of a CG iteration's K·p fused with the iteration's finalize (cg_fin_dad_kernel): rows [r0, r1) =
@@ -1488,7 +1497,7 @@ __global__ __launch_bounds__(256) void exp_combine_kernel(const T *__restrict__ 
 // d.Ad partials bit for bit those of the two launches, raw is not written
 template <typename T>
 __global__ __launch_bounds__(cgk::CG_NT) void exp_combine_fin_kernel(
-    const T *__restrict__ e, const T *__restrict__ w, const T *__restrict__ hdiag, const T *__restrict__ hs,
+    const T *__restrict__ e, const T *__restrict__ cb, const T *__restrict__ w, const T *__restrict__ hdiag, const T *__restrict__ hs,
     const T *__restrict__ hslab, int G, const T *__restrict__ jslab, int P, const T *__restrict__ raw,
     const T *__restrict__ ssc, T kappa, int64_t r0, int64_t r1, const T *__restrict__ q, const T *__restrict__ d,
     const T *__restrict__ psum, int GP, T QA_cost, T cost_inv, T *__restrict__ Ad, T *__restrict__ pdad,
@@ -1502,7 +1511,7 @@ __global__ __launch_bounds__(cgk::CG_NT) void exp_combine_fin_kernel(
     T s1 = 0;
     for (int64_t k = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; k < r1 - r0; k += st) {
         const int64_t i = r0 + k;
-        const T rw = exp_combine_row<T>(e, w, hdiag, nullptr, hs, hslab, G, jslab, P, raw, ssc, kappa, i, r0, r1, 0);
+        const T rw = exp_combine_row<T>(e, cb, w, hdiag, nullptr, hs, hslab, G, jslab, P, raw, ssc, kappa, i, r0, r1, 0);
         const T di = d[i];
         const T v = cgk::cg_fin_value(rw, q[i], di, sp, sqp, QA_cost, cost_inv, 0);
         Ad[i] = v;
@@ -2361,9 +2370,11 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     // unsharded with bfloat16 windows: w, its bfloat16 copy and the S partials in one pass (exp_wown_kernel over
     // all rows: exp_w_kernel's w and exp_wsum_kernel's partials, bit for bit)
     const bool wown_all = !shard && ex.hbf16;
+    // centered finalize (engine.hpp ctr_*): S becomes S_c = sum_j cw_j w_j, the combine's base c_i S_c (rbf) / 0 (poly)
+    const T *cw = ctr_now && kernel == 2 ? ctr_cw.get() : nullptr;
     if (g16 || wown_all) {
         hipLaunchKernelGGL(exp_wown_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, stream, kernel == 2 ? csr.e.get() : nullptr,
-                           p, ib, ie, ex.wv.get(), ex.wv16.get(), red.get(), status);
+                           p, ib, ie, ex.wv.get(), ex.wv16.get(), cw, red.get(), status);
         MI_LAUNCH_CHECK();
         if (kernel == 2) w = ex.wv.get();
     } else if (kernel == 2) {
@@ -2405,7 +2416,7 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
             launch_dot_final<T>(sg, sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream, G);
         } else {
             hipLaunchKernelGGL(exp_wsum_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, stream, w, m,
-                               ex.hbf16 ? ex.wv16.get() : nullptr, red.get(), status);  // S = sum_j w_j (+ bf16 w)
+                               ex.hbf16 ? ex.wv16.get() : nullptr, cw, red.get(), status);  // S = sum_j w_j (+ bf16 w)
             MI_LAUNCH_CHECK();
             launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
         }
@@ -2422,7 +2433,7 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
         gather_input(w);
         if (!wown_all) {
             hipLaunchKernelGGL(exp_wsum_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, stream, w, m,
-                               ex.hbf16 ? ex.wv16.get() : nullptr, red.get(), status);  // S = sum_j w_j (+ bf16 w)
+                               ex.hbf16 ? ex.wv16.get() : nullptr, cw, red.get(), status);  // S = sum_j w_j (+ bf16 w)
             MI_LAUNCH_CHECK();
         }
         const bool sfold = d > 0 && expansion_moments_fused();
@@ -2431,10 +2442,11 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
         expansion_dominant(w, status);
     }
     T kappa = 0;
-    if (kernel == 1) {
+    if (kernel == 1 && !ctr_now) {
         kappa = 1;
         for (int q2 = 0; q2 < degree; ++q2) kappa *= coef0;
     }
+    const T *cb = ctr_now && kernel == 2 ? ctr_c.get() : nullptr;
     // J_i = sum_{f in x_i} sum_k x_if^(k+1) M[f][k]: one SELL pass over this rank's CSR rows (mode 2)
     // (few panels: the combine sums the pass's panel slabs itself, one launch fewer)
     const auto &pc = csr.spmv_csr;
@@ -2447,7 +2459,7 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
         flush_psum();
         const kp_fin_t &f = *kp_fin_req;
         hipLaunchKernelGGL(exp_combine_fin_kernel<T>, dim3(RED_BLOCKS), dim3(cgk::CG_NT), 0, stream,
-                           kernel == 2 ? csr.e.get() : nullptr, w, ex.hdiag.get(), ex.hs.get(),
+                           kernel == 2 ? csr.e.get() : nullptr, cb, w, ex.hdiag.get(), ex.hs.get(),
                            ex.G > 1 ? ex.hslab.get() : nullptr, ex.G, jfuse ? pc.partial.get() : nullptr, (int) pc.P,
                            raw.get(), csr.ssc.get(), kappa, r0, r1, f.q, f.d, f.psum, f.G, f.QA_cost, f.cost_inv, f.Ad,
                            f.pdad, sc.get());
@@ -2457,11 +2469,106 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     }
     if (ie > ib)
         hipLaunchKernelGGL(exp_combine_kernel<T>, dim3((unsigned) ceil_div(ie - ib, 256)), dim3(256), 0, stream,
-                           kernel == 2 ? csr.e.get() : nullptr, w, ex.hdiag.get(), ex.phin.get(), ex.hs.get(),
+                           kernel == 2 ? csr.e.get() : nullptr, cb, w, ex.hdiag.get(), ex.phin.get(), ex.hs.get(),
                            ex.G > 1 ? ex.hslab.get() : nullptr, ex.G, jfuse ? pc.partial.get() : nullptr, (int) pc.P,
                            csr.ssc.get(), kappa, ib, ie, r0, r1, with_base ? 0 : 1, raw.get(), status);
     MI_LAUNCH_CHECK();
     if (!shard) allgather_rows(raw.get());
+}
+
+// ---- centered rank-1 terms of the finalize (engine.hpp ctr_*) -------------------------------------------------
+// per row i < m, in fp64 from the row's entries and the last point x_m (dense, xlast):
+//   rbf:  c_i = e_i - e_m = e_m expm1(gamma (|x_m|^2 - |x_i|^2)),  cw_i = c_i / e_i = -expm1(gamma (|x_i|^2 - |x_m|^2)),
+//         h_i = e_i e_m expm1(2 gamma x_i.x_m)
+//   poly: h_i = (gamma x_i.x_m + c0)^deg - c0^deg as its binomial sum (no cancellation)
+// bad = 1 when a value does not fit the real type (then the plain finalize is used)
+template <typename T>
+__global__ __launch_bounds__(256) void exp_ctr_kernel(int kernel, int degree, double gamma, double coef0,
+                                                      const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+                                                      vals_t<T> val, int64_t m, const T *__restrict__ xlast, double nlast,
+                                                      const T *__restrict__ norms, double em, T *__restrict__ c,
+                                                      T *__restrict__ cw, T *__restrict__ h, int *__restrict__ bad) {
+    const int64_t row = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= m) return;
+    double s = 0;
+    for (int64_t k = rowptr[row]; k < rowptr[row + 1]; ++k) s = fma((double) val[k], (double) xlast[col[k]], s);
+    const double lim = sizeof(T) == 4 ? 1e37 : 1e307;
+    if (kernel == 2) {
+        const double ni = (double) norms[row];
+        const double ei = exp(-gamma * ni);
+        const double ci = em * expm1(gamma * (nlast - ni)), cwi = -expm1(gamma * (ni - nlast));
+        const double hi = ei * em * expm1(2.0 * gamma * s);
+        if (!(fabs(cwi) < lim) || !(fabs(hi) < lim)) *bad = 1;
+        c[row] = (T) ci;
+        cw[row] = (T) cwi;
+        h[row] = (T) hi;
+    } else {
+        const double u = gamma * s;
+        double hi = 0, binom = 1, uk = 1;
+        for (int k = 1; k <= degree; ++k) {
+            binom = binom * (double) (degree - k + 1) / (double) k;
+            uk *= u;
+            double c0p = 1;
+            for (int t = 0; t < degree - k; ++t) c0p *= coef0;
+            hi += binom * c0p * uk;
+        }
+        if (!(fabs(hi) < lim)) *bad = 1;
+        h[row] = (T) hi;
+    }
+}
+
+template <typename T>
+bool engine<T>::ctr_active() const {
+    return ctr_ok && q_gen && sparse && !csr.dense_on && csr.ex.on && !csr.otf_on && (kernel == 1 || kernel == 2);
+}
+
+template <typename T>
+T engine<T>::QAf() const {
+    if (!ctr_active()) return QA_cost;
+    // a caller's QA_cost (plssvm_mi_set_qa_cost) that differs from k_mm + 1/C keeps its difference
+    return (T) (ctr_hm + (double) cost_inv()) + (QA_cost - (ctr_kmm + T(1) / cost));
+}
+
+template <typename T>
+void engine<T>::ctr_setup() {
+    ctr_ok = false;
+    static const int mode = [] {
+        const char *v = std::getenv("PLSSVM_MI_CTR");
+        return v == nullptr ? 1 : std::atoi(v);
+    }();
+    if (mode == 0 || !sparse || csr.dense_on || !csr.ex.on || csr.otf_on || (kernel != 1 && kernel != 2) || m <= 0) return;
+    double nlast = 0;
+    for (int64_t k = 0; k < d; ++k) nlast = std::fma((double) xlast_h[k], (double) xlast_h[k], nlast);
+    const double g = (double) gamma, em = std::exp(-g * nlast);
+    if (kernel == 2) {
+        ctr_hm = -std::expm1(-2.0 * g * nlast);  // e_m^2 expm1(2 gamma |x_m|^2) = 1 - e_m^2
+    } else {
+        double hm = 0, binom = 1, uk = 1;
+        for (int k = 1; k <= degree; ++k) {
+            binom = binom * (double) (degree - k + 1) / (double) k;
+            uk *= g * nlast;
+            double c0p = 1;
+            for (int t = 0; t < degree - k; ++t) c0p *= (double) coef0;
+            hm += binom * c0p * uk;
+        }
+        ctr_hm = hm;
+    }
+    const int64_t len = q.size();
+    ctr_h.alloc(len, stream);
+    if (kernel == 2) {
+        ctr_c.alloc(len, stream);
+        ctr_cw.alloc(len, stream);
+    }
+    dev_buf<int> bad;
+    bad.alloc(1, stream);
+    hipLaunchKernelGGL(exp_ctr_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream, kernel, degree, g,
+                       (double) coef0, csr.rowptr.get(), csr.col.get(), csr.rvals(), m, xlast.get(), nlast, norms.get(),
+                       em, ctr_c.get(), ctr_cw.get(), ctr_h.get(), bad.get());
+    MI_LAUNCH_CHECK();
+    int hb = 0;
+    MI_HIP_CHECK(hipMemcpyAsync(&hb, bad.get(), sizeof(int), hipMemcpyDeviceToHost, stream));
+    MI_HIP_CHECK(hipStreamSynchronize(stream));
+    ctr_ok = hb == 0;
 }
 
 // ---- predict through the expansion (csvm::predict on sparse poly / rbf models) -----------------------
@@ -2754,6 +2861,8 @@ bool engine<T>::expansion_predict(const T *alpha_dev, T alpha_m, T bias, const i
     return hf == 0;
 }
 
+int exp_dot2_built() { return EXP_DOT2 ? 1 : 0; }
+
 #define INST(T)                                                                              \
     template bool engine<T>::expansion_eligible();                                           \
     template void engine<T>::build_expansion(const int64_t *, int64_t, const std::function<std::exception_ptr()> &);                      \
@@ -2764,6 +2873,9 @@ bool engine<T>::expansion_predict(const T *alpha_dev, T alpha_m, T bias, const i
     template bool engine<T>::expansion_moments_fused() const;        \
     template coefs engine<T>::expansion_coefs() const;                                       \
     template void engine<T>::expansion_kp_raw(const T *, const cg_scalars<T> *, bool);      \
+    template bool engine<T>::ctr_active() const;                                              \
+    template T engine<T>::QAf() const;                                                        \
+    template void engine<T>::ctr_setup();                                                     \
     template bool engine<T>::expansion_predict(const T *, T, T, const int64_t *, const int32_t *, const T *, int64_t, \
                                                int64_t, double, double, T, T *);
 INST(float)

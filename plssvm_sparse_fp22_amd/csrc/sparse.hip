@@ -693,6 +693,10 @@ void engine<T>::csc_device(int64_t nnz, dev_buf<int64_t> &cpos_d) {
     hipLaunchKernelGGL(csc_rowid_kernel, dim3((unsigned) ceil_div(m, 4)), dim3(256), 0, stream, csr.rowptr.get(), m,
                        rowid.get(), kid.get());
     MI_LAUNCH_CHECK();
+    {  // test hook: the device sort running out of memory after its first temporaries (the host fallback, setup_csr)
+        const char *e = std::getenv("PLSSVM_MI_CSC");
+        if (e != nullptr && std::strcmp(e, "oom") == 0) throw mi_error(-4, "device CSC: out of memory (test hook)");
+    }
     const uint32_t *keys = reinterpret_cast<const uint32_t *>(csr.col.get());  // columns >= 0: the same order unsigned
     size_t tb = 0;
     MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, key_s.get(), kid.get(), kid_s.get(), n32, 0, end_bit,
@@ -790,12 +794,28 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     std::vector<T> cval_real;
     dev_buf<int64_t> cpos_d;
     double amax = 0.0, nmax = 0.0;  // max x^2 and max |x_i|^2 (kernel expansion eligibility)
-    const bool dev_csc = [&] {
+    bool dev_csc = [&] {
         const char *e = std::getenv("PLSSVM_MI_CSC");
         return nnz > 0 && nnz < (int64_t) INT32_MAX && !(e != nullptr && std::strcmp(e, "host") == 0);
     }();
     if (dev_csc) {
-        csc_device(nnz, cpos_d);
+        // the device sort's temporaries (~16 B per entry + the radix-sort scratch) may not fit where the CSR
+        // does: out of device memory, the host counting sort builds the same arrays, so a rank never
+        // leaves setup here while its peers wait in the next group exchange
+        try {
+            csc_device(nnz, cpos_d);
+        } catch (const std::exception &ex) {
+            if (exception_code(ex) != -4) throw;
+            dev_csc = false;
+            csr.colptr.reset();
+            csr.crow.reset();
+            csr.cval.reset();
+            cpos_d.reset();
+            (void) hipGetLastError();
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+        }
+    }
+    if (dev_csc) {
         crow.resize((size_t) nnz);
         MI_HIP_CHECK(hipMemcpyAsync(colptr.data(), csr.colptr.get(), sizeof(int64_t) * (size_t) (d + 1),
                                     hipMemcpyDeviceToHost, stream));
