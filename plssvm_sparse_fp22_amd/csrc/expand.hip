@@ -728,19 +728,32 @@ __device__ __forceinline__ void exp_row_windows(const int32_t *__restrict__ sj, 
     if (curW >= 0) on_close(curW, kcur);
 }
 
-// per row r (rank-local), window W: count of its non-zero entries with j in W, rounded up to 4 slots
+// per row r (rank-local), window W: count of its non-zero entries with j in W, rounded up to gran (4: chunks, 2: pair
+// flags) slots; the cells without entries are left as they are (0, or a dummy written before)
 template <typename T>
 __global__ __launch_bounds__(256) void exp_cell_count_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
                                                              const int32_t *__restrict__ sj, const T *__restrict__ sv,
-                                                             int64_t R, int64_t nW, int64_t CW, int64_t RB,
+                                                             int64_t R, int64_t nW, int64_t CW, int64_t RB, int64_t gran,
                                                              int64_t *__restrict__ cnt) {
     const int64_t r = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= R) return;
     const int lane = threadIdx.x & 63;
     exp_row_windows<T>(sj, sv, rbeg[r], rend[r], CW, [](int, int) {}, [](int32_t, T, int, int64_t) {},
                        [&](int W, int64_t k) {
-                           if (lane == 0) cnt[exp_cidx(r, W, nW, RB)] = (k + 3) & ~int64_t(3);
+                           if (lane == 0) cnt[exp_cidx(r, W, nW, RB)] = (k + gran - 1) & ~(gran - 1);
                        });
+}
+
+// pair flags: a wave's stream of a window (RPW consecutive cells, exp_cidx) padded to a multiple of 4 slots, the
+// 2 padding slots (H = 0, no flag: they add 0 to the row open at the end) given to the group's last cell — so every
+// (block, wave, window) range starts on a chunk (woff = coff / 4)
+__global__ __launch_bounds__(256) void exp_cell_pad_groups_kernel(int64_t ngroups, int64_t RPW, int64_t *__restrict__ cnt) {
+    const int64_t gi = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (gi >= ngroups) return;
+    int64_t *c = cnt + gi * RPW;
+    int64_t s = 0;
+    for (int64_t k = 0; k < RPW; ++k) s += c[k];
+    if (s & 2) c[RPW - 1] += 2;
 }
 
 // bfloat16 of a float, round to nearest even (finite values)
@@ -877,12 +890,13 @@ __global__ __launch_bounds__(256) void exp_cell_stats_kernel(const int64_t *__re
     }
 }
 
-// the dummies: a (row, window) cell without entries takes one 4-slot chunk
-__global__ __launch_bounds__(256) void exp_cell_fill_empty_kernel(int64_t R, int64_t nW, int64_t RB, int64_t *__restrict__ cnt) {
+// the dummies: a (row, window) cell without entries takes one 4-slot chunk (pair flags: one 2-slot pair)
+__global__ __launch_bounds__(256) void exp_cell_fill_empty_kernel(int64_t R, int64_t nW, int64_t RB, int64_t dsz,
+                                                                  int64_t *__restrict__ cnt) {
     const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= R * nW) return;
     const int64_t idx = exp_cidx(t / nW, t % nW, nW, RB);
-    if (cnt[idx] == 0) cnt[idx] = 4;
+    if (cnt[idx] == 0) cnt[idx] = dsz;
 }
 
 #ifndef EXP_JH
@@ -1051,7 +1065,9 @@ __device__ __forceinline__ void seg_step(double &v, int k) {
 // rows' partial sums (segmented shuffle reduction) into an LDS row accumulator only it writes.
 // Fixed order, no atomics: bitwise reproducible.
 // D2 (bfloat16 H only): the dot instructions (EXP_DOT2) or the FMA chain (PLSSVM_MI_EXP_DOT2=0: tests, A/B)
-template <typename T, int RBB, bool HB, bool RF = false, bool D2 = true>
+// RF: 0 = a stored row index per chunk, 1 = row-start flags per chunk, 2 = row-start flags per slot pair (cells
+// padded to 2 slots instead of 4, see "pair flags" below)
+template <typename T, int RBB, bool HB, int RF = 0, bool D2 = true>
 __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *__restrict__ woff,
                                                                  const uint16_t *__restrict__ hrow,
                                                                  const uint16_t *__restrict__ hjl,
@@ -1154,6 +1170,55 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     // RF: the rows of a window's chunks from their row-start flags (carry = the row before the step's first chunk + 1)
     int carry = 0;
     auto group = [&](const group_regs &g, bool have) {
+        if constexpr (RF == 2) {
+            static_assert(HB && EXP_JH && sizeof(T) == 4, "pair flags: bfloat16 H, side-by-side chunks");
+            // pair flags: bit 14 of the chunk's H0 / H2 marks a row starting at slot 0 / 2. A lane's two pairs give
+            // a01 (slots 0, 1) and a23 (slots 2, 3); t = a01 + a23. With P the inclusive lane prefix of t and E the
+            // exclusive one, a row that starts in lane A (its tail there) and ends in lane B (its head there) sums to
+            // tail_A - P_A + E_B + head_B: lanes with a flag add tail - P to the row they leave open and E + head to
+            // the row their first flag closes; a row inside one lane (pair 0 flagged and pair 1 flagged) adds a01;
+            // lane 63 adds P_63 to the row open at the group's end. Each phase writes distinct rows (one instruction
+            // never updates a row twice); fixed order: bitwise reproducible. The cancellation bound of the prefix
+            // differences is the one of the chunk-flag layout below (bfloat16 H: <= 2^-24 of the group's |H w|).
+            const bool f0 = have && (g.hb.x & 0x4000u) != 0u, f1 = have && (g.hb.y & 0x4000u) != 0u;
+            const uint32_t hx = g.hb.x & ~0x4000u, hy = g.hb.y & ~0x4000u;
+            float a01 = 0.f, a23 = 0.f;
+            if (have) {
+                const u32x2 jj = g.jj;
+                const uint32_t w01 = (uint32_t) wl[jj.x & 0xFFFFu] | ((uint32_t) wl[jj.x >> 16] << 16);
+                const uint32_t w23 = (uint32_t) wl[jj.y & 0xFFFFu] | ((uint32_t) wl[jj.y >> 16] << 16);
+                if constexpr (D2 && EXP_DOT2) {
+                    asm("v_dot2_f32_bf16 %0, %2, %3, 0\n\tv_dot2_f32_bf16 %1, %4, %5, 0\n\ts_nop 1"
+                        : "=&v"(a01), "=&v"(a23)
+                        : "v"(hx), "v"(w01), "v"(hy), "v"(w23));
+                } else {
+                    a01 = __uint_as_float(hx << 16) * __uint_as_float(w01 << 16);
+                    a01 = fmaf(__uint_as_float(hx & 0xFFFF0000u), __uint_as_float(w01 & 0xFFFF0000u), a01);
+                    a23 = __uint_as_float(hy << 16) * __uint_as_float(w23 << 16);
+                    a23 = fmaf(__uint_as_float(hy & 0xFFFF0000u), __uint_as_float(w23 & 0xFFFF0000u), a23);
+                }
+            }
+            const float t = a01 + a23;
+            float P = t;
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x111, 0xF, 0xF, true));  // row_shr:1
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x112, 0xF, 0xF, true));  // row_shr:2
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x114, 0xF, 0xF, true));  // row_shr:4
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x118, 0xF, 0xF, true));  // row_shr:8
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x142, 0xA, 0xF, true));  // row_bcast:15
+            P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x143, 0xC, 0xF, true));  // row_bcast:31
+            const float E = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x138, 0xF, 0xF, true));  // wave_shr:1
+            const unsigned long long b0 = __ballot(f0), b1 = __ballot(f1), bh = __ballot(have);
+            const int below = (int) __builtin_amdgcn_mbcnt_hi((uint32_t) (b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) b0, 0u)) +
+                              (int) __builtin_amdgcn_mbcnt_hi((uint32_t) (b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) b1, 0u));
+            const int row0 = carry + below + (f0 ? 1 : 0) - 1, row1 = row0 + (f1 ? 1 : 0);
+            carry += __popcll(b0) + __popcll(b1);
+            if (bh == 0ull) return;  // a group wholly past the window's end
+            if (f0 || f1) racc[f1 ? row1 : row0] += (f1 ? a23 : t) - P;  // tail: the row left open in this lane
+            if (f0 && f1) racc[row0] += a01;                             // a row inside this lane
+            if ((f0 || f1) && !(lane == 0 && f0)) racc[(f0 ? row0 : row1) - 1] += E + (f0 ? 0.f : a01);  // head
+            if (lane == 63) racc[row1] += P;                             // the row open at the group's end
+            return;
+        }
         int rl = have ? g.rl : -1;
         uint32_t hx = g.hb.x;
         if constexpr (RF) {
@@ -1925,10 +1990,16 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             const long long v = std::atoll(e);
             if (v > 0) cap = v;
         }
-        size_t free_b = 0, total_b = 0;
-        MI_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+        // the one-pass join's slot pool beside the structures the estimate counts: gated on the budget left over by the
+        // estimate, both taken before the SELL plans' host thread allocates — the same choice on every run
+        double room = (double) (csr.budget_b - csr.est_bytes);
+        if (csr.budget_b <= 0) {
+            size_t free_b = 0, total_b = 0;
+            MI_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+            room = 0.4 * (double) free_b;
+        }
         const double pool_b = (double) R * (double) cap * (double) (4 + sizeof(T));
-        if (want && ex.rj_mean > 0.0 && pool_b <= 0.4 * (double) free_b) {
+        if (want && ex.rj_mean > 0.0 && pool_b <= room) {
             sj.alloc(R * cap, stream, false);
             cnt.alloc(R, stream);
             lnz.alloc(3, stream);  // [0] lower pairs with H != 0, [1] max |H| / kernel value (double bits), [2] max count
@@ -2164,18 +2235,24 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             const int64_t CW = ex.CW, ncnt = ex.nblk * RB * ex.nW;
             cnt.alloc(ncnt + 1, stream);
             coff.alloc(ncnt + 1, stream, false);
-            if (R > 0) {
+            auto count_cells = [&](int64_t gran) {
+                if (R <= 0) return;
                 hipLaunchKernelGGL(exp_cell_count_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream,
-                                   rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, RB, cnt.get());
+                                   rbeg, rend, sj.get(), sv.get(), R, ex.nW, CW, RB, gran, cnt.get());
                 MI_LAUNCH_CHECK();
-            }
+            };
+            count_cells(4);
             // flagged chunks (bfloat16 H only): when every |H| < 2 and the dummies of empty cells (16 B each) cost
             // at most half of the row indices they replace (2 B per chunk). PLSSVM_MI_EXP_ROWS=index keeps the
             // row index, =flags forces the flags (when the bit is free)
             ex.rflags = false;
+            ex.rpairs = false;
             if (ex.hbf16 && R > 0) {
                 const char *rs = std::getenv("PLSSVM_MI_EXP_ROWS");
-                const int ropt = rs == nullptr ? 0 : (std::strcmp(rs, "index") == 0 ? -1 : std::strcmp(rs, "flags") == 0 ? 1 : 0);
+                const int ropt = rs == nullptr ? 0
+                                 : std::strcmp(rs, "index") == 0 ? -1
+                                 : std::strcmp(rs, "flags") == 0 ? 1
+                                 : std::strcmp(rs, "pairs") == 0 ? 2 : 0;
                 if (ropt >= 0) {
                     dev_buf<unsigned long long> st;
                     st.alloc(2, stream);
@@ -2186,11 +2263,36 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
                     MI_HIP_CHECK(hipMemcpyAsync(hs2, st.get(), sizeof(hs2), hipMemcpyDeviceToHost, stream));
                     scan(ncnt);  // synchronises; ex.slots = the indexed layout's slots
                     const double chunks = (double) ex.slots / 4.0;
-                    ex.rflags = hs2[1] == 0 && (ropt == 1 || 16.0 * (double) hs2[0] <= 0.5 * 2.0 * chunks);
+                    ex.rflags = hs2[1] == 0 && (ropt >= 1 || 16.0 * (double) hs2[0] <= 0.5 * 2.0 * chunks);
                     if (ex.rflags) {
                         hipLaunchKernelGGL(exp_cell_fill_empty_kernel, dim3((unsigned) ceil_div(R * ex.nW, 256)), dim3(256),
-                                           0, stream, R, ex.nW, RB, cnt.get());
+                                           0, stream, R, ex.nW, RB, (int64_t) 4, cnt.get());
                         MI_LAUNCH_CHECK();
+                    }
+                    // pair flags (round 5): the flags on slot pairs, cells padded to 2 slots instead of 4 (the 4-slot
+                    // padding is ~15 % of the stream on config 5's 2M geometry). Taken when it saves >= 3 % of the
+                    // chunk-flag layout's slots (PLSSVM_MI_EXP_ROWS=pairs forces it, =flags keeps the chunk flags)
+                    if (ex.rflags && ropt != 1) {
+                        scan(ncnt);
+                        const int64_t slots4 = ex.slots;
+                        MI_HIP_CHECK(hipMemsetAsync(cnt.get(), 0, sizeof(int64_t) * (size_t) (ncnt + 1), stream));
+                        count_cells(2);
+                        hipLaunchKernelGGL(exp_cell_fill_empty_kernel, dim3((unsigned) ceil_div(R * ex.nW, 256)), dim3(256),
+                                           0, stream, R, ex.nW, RB, (int64_t) 2, cnt.get());
+                        MI_LAUNCH_CHECK();
+                        const int64_t ngroups = nbv * ex.nW, RPW = RB / EXP_NWV;
+                        hipLaunchKernelGGL(exp_cell_pad_groups_kernel, dim3((unsigned) ceil_div(ngroups, 256)), dim3(256), 0,
+                                           stream, ngroups, RPW, cnt.get());
+                        MI_LAUNCH_CHECK();
+                        scan(ncnt);
+                        ex.rpairs = ropt == 2 || (double) ex.slots <= 0.97 * (double) slots4;
+                        if (!ex.rpairs) {  // back to the chunk-flag counts
+                            MI_HIP_CHECK(hipMemsetAsync(cnt.get(), 0, sizeof(int64_t) * (size_t) (ncnt + 1), stream));
+                            count_cells(4);
+                            hipLaunchKernelGGL(exp_cell_fill_empty_kernel, dim3((unsigned) ceil_div(R * ex.nW, 256)),
+                                               dim3(256), 0, stream, R, ex.nW, RB, (int64_t) 4, cnt.get());
+                            MI_LAUNCH_CHECK();
+                        }
                     }
                 }
             }
@@ -2274,7 +2376,8 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
             }
         } else {
             auto pick = [&](auto hb, auto rf, auto d2) {
-                constexpr bool HB = decltype(hb)::value, RF = decltype(rf)::value, D2 = decltype(d2)::value;
+                constexpr bool HB = decltype(hb)::value, D2 = decltype(d2)::value;
+                constexpr int RF = decltype(rf)::value;
                 switch (ex.RBB) {
                     case 4096: launch(exp_hcell_kernel<T, 4096, HB, RF, D2>); break;
                     case 8192: launch(exp_hcell_kernel<T, 8192, HB, RF, D2>); break;
@@ -2283,14 +2386,19 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
                 }
             };
             const bool dot2 = ex.dot2;
+            using R0 = std::integral_constant<int, 0>;
+            using R1 = std::integral_constant<int, 1>;
+            using R2 = std::integral_constant<int, 2>;
             if constexpr (sizeof(T) == 4) {
-                if (ex.hbf16 && ex.rflags && dot2) pick(std::true_type{}, std::true_type{}, std::true_type{});
-                else if (ex.hbf16 && ex.rflags) pick(std::true_type{}, std::true_type{}, std::false_type{});
-                else if (ex.hbf16 && dot2) pick(std::true_type{}, std::false_type{}, std::true_type{});
-                else if (ex.hbf16) pick(std::true_type{}, std::false_type{}, std::false_type{});
-                else pick(std::false_type{}, std::false_type{}, std::true_type{});
+                if (ex.hbf16 && ex.rpairs && dot2) pick(std::true_type{}, R2{}, std::true_type{});
+                else if (ex.hbf16 && ex.rpairs) pick(std::true_type{}, R2{}, std::false_type{});
+                else if (ex.hbf16 && ex.rflags && dot2) pick(std::true_type{}, R1{}, std::true_type{});
+                else if (ex.hbf16 && ex.rflags) pick(std::true_type{}, R1{}, std::false_type{});
+                else if (ex.hbf16 && dot2) pick(std::true_type{}, R0{}, std::true_type{});
+                else if (ex.hbf16) pick(std::true_type{}, R0{}, std::false_type{});
+                else pick(std::false_type{}, R0{}, std::true_type{});
             } else {
-                pick(std::false_type{}, std::false_type{}, std::true_type{});
+                pick(std::false_type{}, R0{}, std::true_type{});
             }
         }
         MI_LAUNCH_CHECK();  // G > 1: the row sums stay in hslab, summed in g order by exp_combine_kernel

@@ -1027,6 +1027,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             csr.est_bytes = (int64_t) est;
             budget = (int64_t) bud;
         }
+        csr.budget_b = budget;  // read before the SELL plans' host thread allocates (the row join's pool)
         // a failed step of the group: the same error on every rank (the worst code; ERR_OOM = fall back)
         auto agree = [&](int code, const std::string &why) -> int {
             if (!in_group()) return code;

@@ -88,6 +88,7 @@ struct exp_data {
     bool hbf16 = false;
     bool dot2 = true;                 // bfloat16 H: the dot-instruction kernel (PLSSVM_MI_EXP_DOT2=0: the FMA chain)
     bool rflags = false;              // hbf16 chunks without hrow: bit 14 of a chunk's first H marks a row's first chunk
+    bool rpairs = false;              // with rflags: the flags mark slot pairs (cells padded to 2 slots, not 4; layout 4)
     double rj_mean = 0.0, rj_max = 0.0;  // setup's sample of the rank's rows: partners sharing >= 2 features (mean, max)
     double hratio = -1.0;             // row join: max |H_ij| / |kernel value of the pair| (< 0: unknown)
     dev_buf<uint16_t> hrow;           // [nchunks] block-local row of each 4-slot chunk
@@ -135,6 +136,7 @@ struct csr_data {
     // densified fallback (PLSSVM_MI_SPARSE_DENSE): neither stored structure fits the device budget, so
     // X is densified into the engine's XT and every K·p recomputes all pairs on the MFMA tiles
     bool dense_on = false;
+    int64_t budget_b = 0;   // the (group's smallest) device budget of the stored structures, taken before the build
     int64_t est_bytes = 0;  // estimated device bytes of the chosen stored structure (0: not estimated)
     // on-the-fly path (PLSSVM_MI_SPARSE_ONTHEFLY, otf.hip): nothing stored per pair; seg[f][W] = (first
     // entry of CSC column f whose row lies in partner window W (CW rows), column-local; their count)

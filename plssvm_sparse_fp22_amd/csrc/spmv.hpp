@@ -311,6 +311,232 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
     }
 }
 
+// ---- software-pipelined walk (round 5, PLSSVM_MI_SELL_PIPE) ------------------------------------------------
+// The same chunks, entries, products and summation order as sell_spmv_kernel (LDS panels, paired 16-bit indices,
+// real values or paired FP22 words) — bit for bit its results — but a wave issues the loads of its next step (the
+// chunk's next SU entries, or the first SU entries of its next chunk) before it consumes the current one, so its
+// loads stay in flight through the gathers, the products and the chunk switch. Two register sets (A, B) alternate
+// (the loop body is written twice: no copies between them, so no wait for the next loads at the loop's end); the
+// chunk descriptors and slot maps of the next chunk are vector loads issued a chunk ahead (a scalar load would share
+// the LDS counter and stall the gathers). A finished wave's last prefetch re-reads its own chunk (cached, discarded).
+// Measured (round 5, one box, profiles/r05_sell_pipe_ab.json): bitwise the plain walk's results, and no faster —
+// config 3 7 159 vs 7 216 CG it/s, 3-RBF 1 055 vs 1 059, config 5 845 vs 846 (the ISA shows the next step's loads in
+// flight through the consume for the real-valued passes): the passes are not bound by a wave's load latency. Off by
+// default; kept as the measured alternative.
+#ifndef PLSSVM_MI_SELL_PIPE
+#define PLSSVM_MI_SELL_PIPE 0
+#endif
+template <typename T, bool F22>
+struct sell_pipe_regs {
+    static constexpr int SU = sell_unroll<F22>(), SU2 = SU / 2;
+    uint32_t ip[SU2];                                  // paired 16-bit panel indices
+    u32x3_a4 vw[F22 ? SU2 : 1];                        // FP22: the 3 words holding an entry pair
+    T v[F22 ? 1 : SU];                                 // real values
+    int seg;                                           // the step's chunk's slot map (loaded with its entries)
+};
+
+template <typename T, bool F22, int KC = 1, int MODE = 0>
+__global__ __launch_bounds__(SELL_NT) void sell_spmv_pipe_kernel(const sell_chunk *__restrict__ chunks,
+                                                                 const int32_t *__restrict__ perm,
+                                                                 const uint16_t *__restrict__ idx, vals_t<T> val,
+                                                                 const int32_t *__restrict__ bchunk,
+                                                                 const T *__restrict__ x, int64_t xn, int64_t W,
+                                                                 int64_t nseg, int nchp, T *__restrict__ out,
+                                                                 const cg_scalars<T> *__restrict__ status) {
+    static_assert(SELL_IDX2 && !SELL_VAL2 && (!F22 || SELL_F22PAIR), "the pipelined walk covers the default layouts");
+    constexpr int XC = MODE == 2 ? KC : 1;
+    constexpr int OC = MODE == 1 ? KC : 1;
+    constexpr int XW = sell_width<T>();
+    constexpr int SU = sell_unroll<F22>(), SU2 = SU / 2;
+    using R = sell_pipe_regs<T, F22>;
+    __shared__ T xs[XW];
+    if (status != nullptr && status->converged) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int blk = (int) xcd_remap(blockIdx.x, gridDim.x);
+    const int c0 = bchunk[blk], c1 = bchunk[blk + 1];
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t *ip32 = reinterpret_cast<const uint32_t *>(idx);
+    // a chunk descriptor through the vector memory path (in order with the step loads; see above)
+    auto desc = [&](int c) -> sell_chunk {
+        int cv = c;
+        asm volatile("" : "+v"(cv));
+        return chunks[cv];
+    };
+    // the streams through buffer descriptors (host-checked: < 2^31 bytes each): every per-step offset is a scalar
+    // (soffset), the lanes' offsets constants — no per-load vector address arithmetic. Paired FP22 chunks start at
+    // multiples of 128 entries, so entry pair p = off + 128 pj + 2 lane starts at bit 22 (off + 128 pj) (a word
+    // boundary) + 44 lane: word 11 (off + 128 pj) / 16 + (44 lane) / 32, shift (44 lane) % 32, per-lane constants
+    const __amdgpu_buffer_rsrc_t rs_ip = __builtin_amdgcn_make_buffer_rsrc((void *) ip32, (short) 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc(
+        F22 ? (void *) val.v22 : (void *) val.v, (short) 0, 0x7FFFFFFF, 0x00020000);
+    const int vo_ip = 4 * lane, vo_v = F22 ? 4 * ((44 * lane) >> 5) : (int) sizeof(T) * lane;
+    const int sh0 = (44 * lane) & 31;
+    auto load = [&](R &r, int64_t off, int width, int j) {
+        const int lastp = max((width >> 1) - 1, 0);
+#pragma unroll
+        for (int u2 = 0; u2 < SU2; ++u2) {
+            const int64_t pj = min((j >> 1) + u2, lastp);
+            r.ip[u2] = __builtin_amdgcn_raw_buffer_load_b32(rs_ip, vo_ip, (int) (4 * ((off >> 1) + pj * 64)), 2);
+            if constexpr (F22) {
+                const auto w3 = __builtin_amdgcn_raw_buffer_load_b96(rs_v, vo_v, (int) (4 * (11 * (off + 128 * pj) / 16)), 2);
+                r.vw[u2] = u32x3_a4{ w3[0], w3[1], w3[2] };
+            }
+        }
+        if constexpr (!F22) {
+            const int last = max(width - 1, 0);
+#pragma unroll
+            for (int u = 0; u < SU; ++u) {
+                const int so = (int) (sizeof(T) * (off + (int64_t) min(j + u, last) * 64));
+                if constexpr (sizeof(T) == 4) {
+                    r.v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, vo_v, so, 2));
+                } else {
+                    const auto d2 = __builtin_amdgcn_raw_buffer_load_b64(rs_v, vo_v, so, 2);
+                    r.v[u] = __longlong_as_double((long long) (((uint64_t) d2[1] << 32) | d2[0]));
+                }
+            }
+        }
+    };
+    for (int cb = c0; cb < c1;) {
+        const int q = chunks[cb].q;
+        const int ce = min(c1, (q + 1) * nchp);
+        T *o = out + (int64_t) q * nseg * OC;
+        {
+            if (cb != c0) __syncthreads();
+            const T *xg = x + (int64_t) q * W * XC;
+            const int xl = (int) min((int64_t) W, xn - (int64_t) q * W) * XC;
+            using V = __attribute__((ext_vector_type(4))) float;
+            constexpr int EV = 16 / (int) sizeof(T);
+            constexpr int VPER = XW / EV / SELL_NT;
+            static_assert(VPER * EV * SELL_NT == XW, "panel width must be a multiple of 16 B per thread");
+            if (xl == XW && (reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
+                V t[VPER];
+#pragma unroll
+                for (int u = 0; u < VPER; ++u) t[u] = reinterpret_cast<const V *>(xg)[tid + u * SELL_NT];
+#pragma unroll
+                for (int u = 0; u < VPER; ++u) reinterpret_cast<V *>(xs)[tid + u * SELL_NT] = t[u];
+            } else {
+                constexpr int XPER = XW / SELL_NT;
+                for (int u = 0; u < XPER; ++u) {
+                    const int k = tid + u * SELL_NT;
+                    xs[k] = k < xl ? xg[k] : T(0);
+                }
+            }
+            __syncthreads();
+        }
+        const int cw0 = cb + wave;
+        const int nk = cw0 < ce ? (ce - cw0 + SELL_WAVES - 1) / SELL_WAVES : 0;  // this wave's chunks of the panel
+        if (nk > 0) {
+            // the wave's chunk descriptors, lane l holding its chunk l (+ 64 b): read with v_readlane at a chunk switch,
+            // so the walk issues no descriptor load (a wave with more than 64 chunks reloads them, rarely)
+            int64_t dl_off = 0;
+            int dl_w = 0;
+            auto batch = [&](int b) {
+                const int k = b * 64 + lane;
+                const sell_chunk d = k < nk ? chunks[cw0 + SELL_WAVES * k] : sell_chunk{ 0, 0, 0 };
+                dl_off = d.off;
+                dl_w = d.width;
+            };
+            auto rl64 = [](int64_t v, int l) -> int64_t {
+                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t) v, l);
+                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t) ((uint64_t) v >> 32), l);
+                return (int64_t) (((uint64_t) hi << 32) | lo);
+            };
+            batch(0);
+            int k = 0;  // the current chunk: cw0 + 16 k
+            int64_t ch_off = rl64(dl_off, 0);
+            int ch_w = __builtin_amdgcn_readlane(dl_w, 0);
+            int64_t nx_off = ch_off;  // the next chunk (itself when there is none; its step re-reads are discarded)
+            int nx_w = ch_w;
+            if (nk > 1) {
+                nx_off = rl64(dl_off, 1);
+                nx_w = __builtin_amdgcn_readlane(dl_w, 1);
+            }
+            R ra, rb;
+            ra.seg = perm[(int64_t) cw0 * 64 + lane];
+            load(ra, ch_off, ch_w, 0);
+            int j = 0;
+            T acc[OC];
+#pragma unroll
+            for (int kk = 0; kk < OC; ++kk) acc[kk] = T(0);
+            auto step = [&](const R &cur, R &nxt) -> bool {
+                const int w = ch_w;
+                const bool last = j + SU >= w;
+                // every step issues the same loads (no merge of load paths, so the compiler's wait counts stay exact):
+                // the next step's entries (selected position) and its chunk's slot map
+                const int kn = last && k + 1 < nk ? k + 1 : k;
+                nxt.seg = perm[(int64_t) (cw0 + SELL_WAVES * kn) * 64 + lane];
+                load(nxt, last ? nx_off : ch_off, last ? nx_w : w, last ? 0 : j + SU);
+                // consume the current step (sell_spmv_kernel's arithmetic and order)
+#pragma unroll
+                for (int u2 = 0; u2 < SU2; ++u2) {
+                    T vv[2];
+                    if constexpr (F22) {
+                        const int sh = sh0;
+                        const u32x3_a4 ww = cur.vw[u2];
+                        const uint64_t lo = ((uint64_t) ww.y << 32) | ww.x;
+                        const uint32_t k0 = (uint32_t) (lo >> sh) & 0x3FFFFFu;
+                        const int sh1 = sh + 22;
+                        const uint64_t hi = ((uint64_t) ww.z << 32) | ww.y;
+                        const uint32_t k1 = (uint32_t) (sh1 >= 32 ? hi >> (sh1 - 32) : lo >> sh1) & 0x3FFFFFu;
+                        vv[0] = (T) fp22_decode(k0);
+                        vv[1] = (T) fp22_decode(k1);
+                    } else {
+                        vv[0] = cur.v[2 * u2];
+                        vv[1] = cur.v[2 * u2 + 1];
+                    }
+                    const uint32_t pr = cur.ip[u2];
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int u = 2 * u2 + t;
+                        const int64_t ci = t == 0 ? (int64_t) (pr & 0xFFFFu) : (int64_t) (pr >> 16);
+                        const T v = j + u < w ? vv[t] : T(0);
+                        if constexpr (MODE == 0) {
+                            acc[0] = fma(v, xs[ci], acc[0]);
+                        } else if constexpr (MODE == 1) {
+                            T tt = v * xs[ci];
+#pragma unroll
+                            for (int k = 0; k < KC; ++k) {
+                                acc[k] += tt;
+                                tt *= v;
+                            }
+                        } else {
+                            const int64_t cx = ci * KC;
+                            T h = xs[cx + KC - 1];
+#pragma unroll
+                            for (int k = KC - 2; k >= 0; --k) h = fma(h, v, xs[cx + k]);
+                            acc[0] = fma(h, v, acc[0]);
+                        }
+                    }
+                }
+                if (!last) {
+                    j += SU;
+                    return true;
+                }
+                if (cur.seg >= 0) {
+#pragma unroll
+                    for (int kk = 0; kk < OC; ++kk) o[(int64_t) kk * nseg + cur.seg] = acc[kk];
+                }
+#pragma unroll
+                for (int kk = 0; kk < OC; ++kk) acc[kk] = T(0);
+                if (k + 1 >= nk) return false;
+                ++k;
+                j = 0;
+                ch_off = nx_off;
+                ch_w = nx_w;
+                if (k + 1 < nk) {
+                    if (((k + 1) & 63) == 0) batch((k + 1) >> 6);
+                    nx_off = rl64(dl_off, (k + 1) & 63);
+                    nx_w = __builtin_amdgcn_readlane(dl_w, (k + 1) & 63);
+                }
+                return true;
+            };
+            while (step(ra, rb) && step(rb, ra)) {
+            }
+        }
+        cb = ce;
+    }
+}
+
 // out[s] = sum_q partial[q][s]. Many panels (split): a block of 256 threads takes 64 segments and its
 // 4 waves each sum one quarter of the panels (coalesced 64-segment rows, 8 loads in flight); the
 // quarters are added in order through LDS — a fixed order, so deterministic. The CSC pass has few
@@ -355,7 +581,17 @@ inline void launch_panel_spmv_t(const spmv_plan<T> &pl, const T *x, int64_t xn, 
     const bool f22 = pl.val22.get() != nullptr;
     T *dst = pl.P > 1 ? pl.partial.get() : out;
     const dim3 grid((unsigned) pl.nblocks), block(SELL_NT);
-    if (pl.ldsx) {
+    bool done = false;
+    if constexpr (PLSSVM_MI_SELL_PIPE != 0) {
+        if (pl.ldsx) {
+            auto k = f22 ? sell_spmv_pipe_kernel<T, true, KC, MODE> : sell_spmv_pipe_kernel<T, false, KC, MODE>;
+            hipLaunchKernelGGL(k, grid, block, 0, stream, pl.chunks.get(), pl.perm.get(), pl.idx16.get(), pl.vals(),
+                               pl.bchunk.get(), x, xn, pl.W, pl.nseg, (int) pl.nchp, dst, status);
+            done = true;
+        }
+    }
+    if (done) {
+    } else if (pl.ldsx) {
         auto k = f22 ? sell_spmv_kernel<T, true, true, KC, MODE> : sell_spmv_kernel<T, true, false, KC, MODE>;
         hipLaunchKernelGGL(k, grid, block, 0, stream, pl.chunks.get(), pl.perm.get(), pl.idx16.get(), pl.vals(),
                            pl.bchunk.get(), x, xn, pl.W, pl.nseg, (int) pl.nchp, dst, status);

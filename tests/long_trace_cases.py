@@ -97,6 +97,9 @@ CASES = {
     # kernel expansion in fp32, bfloat16 H, flagged chunks (the 3-RBF / config-5 layout)
     "rbf_f32_bf16_flags": ("rbf", np.float32, ("group", 300, 3, 15, 1e3), ("x2", 4e-3), 0.0, 1e6, "expansion",
                            {"PLSSVM_MI_EXP_ROWS": "flags"}, {"exp_hbytes": 2, "exp_layout": 2, "centered": 1}),
+    # the same set and layout with pair flags (round 5: cells padded to 2 slots, expand.hip "pair flags")
+    "rbf_f32_bf16_pairs": ("rbf", np.float32, ("group", 300, 3, 15, 1e3), ("x2", 4e-3), 0.0, 1e6, "expansion",
+                           {"PLSSVM_MI_EXP_ROWS": "pairs"}, {"exp_hbytes": 2, "exp_layout": 4, "centered": 1}),
     # the same with 2 features per group (pairs share 2 features) and with 10 (gamma from the curvature rule)
     "rbf_f32_bf16_flags_b": ("rbf", np.float32, ("group", 300, 2, 16, 1e3), ("x2", 4e-3), 0.0, 1e6, "expansion",
                              {"PLSSVM_MI_EXP_ROWS": "flags"}, {"exp_hbytes": 2, "exp_layout": 2, "centered": 1}),

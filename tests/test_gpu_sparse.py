@@ -546,16 +546,54 @@ def test_expansion_row_flags_equal_row_index(rbb, groups, sim, shape, monkeypatc
     np.testing.assert_array_equal(out["flags"][2], out["index"][2])
 
 
+@pytest.mark.parametrize("rbb,groups,sim", [("auto", "0", None), ("4096", "1", None), ("8192", "3", None),
+                                             ("32768", "2", None), ("auto", "0", (1, 3)), ("auto", "0", (2, 8))])
+@pytest.mark.parametrize("shape", [(140000, 3000, 20), (150000, 200000, 6), (60000, 1500, 12)])
+def test_expansion_row_pairs_equal_row_flags(rbb, groups, sim, shape, monkeypatch):
+    """Pair flags (round 5, info exp_layout 4: bit 14 of H0 / H2 marks a row starting at a chunk's slot 0 / 2, cells
+    padded to 2 slots instead of 4, a window's stream of a wave padded to whole chunks at its end) against the chunk
+    flags: the same stored values and products, the row sums formed as prefix differences per slot pair instead of
+    per chunk — equal to 2^-20 of the rows' overlap magnitude (the bfloat16 bound's cancellation, expand.hip), fewer
+    slots, across accumulator classes, window groups, simulated ranks, three partner windows, a set whose cells are
+    nearly all empty (2-slot dummies) and a small-cell set (60000 x 1500 @ 12: cells of 1-3 entries)."""
+    n, d, k = shape
+    csr, _ = datagen.sparse_csr(n, d, k, seed=23, dtype=np.float32)
+    x = np.random.default_rng(9).uniform(-1, 2, n - 1).astype(np.float32)
+    if rbb != "auto":
+        monkeypatch.setenv("PLSSVM_MI_EXP_RBB", rbb)
+        monkeypatch.setenv("PLSSVM_MI_EXP_G", groups)
+    out = {}
+    for rows in ("flags", "pairs"):
+        monkeypatch.setenv("PLSSVM_MI_EXP_ROWS", rows)
+        with sparse_svm(csr, "rbf", np.float32, sim=sim, algo="expansion") as svm:
+            svm.setup_data_on_device()
+            info = svm.info()
+            assert info["exp_hbytes"] == 2
+            out[rows] = (info["exp_layout"], info["pair_slots"], svm.kp_part(x, "kernel").astype(np.float64),
+                         svm.kp_part(x, "overlap").astype(np.float64), svm.kp_part(np.abs(x), "overlap").astype(np.float64))
+            # bitwise reproducible run to run
+            np.testing.assert_array_equal(svm.kp_part(x, "overlap").astype(np.float64), out[rows][3])
+    assert out["flags"][0] == 2 and out["pairs"][0] == 4
+    assert out["pairs"][1] <= out["flags"][1]
+    # scale: the overlap of |x| (plus 2^-10 of its largest row) and the fp32 rounding of the compared values themselves
+    # (both are rounded to float once: a row's two results may differ in their last bits)
+    mag = np.abs(out["flags"][4]) + 2.0 ** -10 * np.abs(out["flags"][4]).max()
+    for q in (2, 3):
+        tol = 2.0 ** -20 * mag + 2.0 ** -22 * np.abs(out["flags"][q])
+        assert np.all(np.abs(out["pairs"][q] - out["flags"][q]) <= tol), (q, np.max(np.abs(out["pairs"][q] - out["flags"][q]) - tol))
+
+
 def test_expansion_row_flags_default_and_oracle(oracle):
-    """The default layout on a BASELINE-like set is the flagged one, and its K·p equals the oracle (fp32 bar)."""
+    """The default layout on a BASELINE-like set is a flagged one (chunk flags, or pair flags where they save >= 3 %
+    of the slots), and its K·p equals the oracle (fp32 bar)."""
     csr, _ = datagen.sparse_csr(20000, 3000, 20, seed=17, dtype=np.float32)
     with sparse_svm(csr, "rbf", np.float32, algo="expansion") as svm:
         svm.setup_data_on_device()
-        assert svm.info()["exp_layout"] == 2
+        assert svm.info()["exp_layout"] in (2, 4)
     check_sparse_kp(oracle, csr, "rbf", np.float32, algo="expansion")
 
 
-@pytest.mark.parametrize("rows", ["index", "flags"])
+@pytest.mark.parametrize("rows", ["index", "flags", "pairs"])
 def test_expansion_dot2_equals_fma_path(oracle, rows, monkeypatch):
     """The bfloat16 remainder's chunk products as two v_dot2_f32_bf16 instructions (inline assembly with a
     hand-placed hazard wait, expand.hip EXP_DOT2) against the FMA chain of the same kernel
@@ -574,7 +612,7 @@ def test_expansion_dot2_equals_fma_path(oracle, rows, monkeypatch):
         with sparse_svm(csr, "rbf", np.float32, algo="expansion") as svm:
             svm.setup_data_on_device()
             info = svm.info()
-            assert info["exp_hbytes"] == 2 and info["exp_layout"] == (2 if rows == "flags" else 1), info
+            assert info["exp_hbytes"] == 2 and info["exp_layout"] == {"index": 1, "flags": 2, "pairs": 4}[rows], info
             assert info["pairs"] > 100000
             if dot2 == "1" and info["exp_dot2"] == 0:  # built without the dot kernel, nothing to compare
                 pytest.skip("libplssvm_mi355x built without EXP_DOT2 (toolchain other than the one it was verified on)")
