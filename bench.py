@@ -176,7 +176,7 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
     tkey = name + (f"_sim{sim[0]}of{sim[1]}" if sim else "")
     hs = roof.get("h_storage")
     tag = None if hs is None else ("bf16" if hs.startswith("bfloat16") else "real") + \
-        ("_pairs" if "pairs" in roof.get("stream_layout", "") else "_flags" if "flags" in roof.get("stream_layout", "") else "")
+        ("_pairs" if "slot pair" in roof.get("stream_layout", "") else "_flags" if "flags" in roof.get("stream_layout", "") else "")
     roof["traffic"], roof["traffic_source"] = pmc_traffic(tkey, n, d, world, roof["kernel"], dts, kern,
                                                           cfg is CONFIGS[name], tag)
     if roof["traffic"] and roof["bound"] == "hbm":

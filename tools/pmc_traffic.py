@@ -27,7 +27,8 @@ def layout_tag(roof):
     hs = roof.get("h_storage")
     if hs is None:
         return None
-    return ("bf16" if hs.startswith("bfloat16") else "real") + ("_flags" if "flags" in roof.get("stream_layout", "") else "")
+    lay = roof.get("stream_layout", "")
+    return ("bf16" if hs.startswith("bfloat16") else "real") + ("_pairs" if "slot pair" in lay else "_flags" if "flags" in lay else "")
 
 
 def find(pattern):
