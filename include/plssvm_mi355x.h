@@ -265,6 +265,8 @@ typedef struct {
                            kernel (built with EXP_DOT2 and selected: PLSSVM_MI_EXP_DOT2 != 0), 0 = the FMA chain */
     int centered;       /* kernel expansion: 1 = the finalize forms Q~'s rank-1 terms in the centered form
                            (engine.hpp ctr_*; PLSSVM_MI_CTR=0 or a caller's own q vector: 0) */
+    int exp_lt;         /* kernel expansion: 1 = the remainder's rows came from the lower-triangle join + transpose
+                           (one rank holding every row; PLSSVM_MI_EXP_LT=0: the full join) */
 } plssvm_mi_info;
 PLSSVM_MI_API int plssvm_mi_get_info(const plssvm_mi_ctx *ctx, plssvm_mi_info *info);
 

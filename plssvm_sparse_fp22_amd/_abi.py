@@ -54,7 +54,8 @@ class Info(ctypes.Structure):
                                             "val_fmt", "rbf_factored")] + [("pair_slots", ctypes.c_int64), ("spmv_bytes", ctypes.c_int64)] + \
                [("rbf_small_args", ctypes.c_int), ("sparse_algo", ctypes.c_int), ("exp_terms", ctypes.c_int),
                 ("exp_waves", ctypes.c_int), ("exp_chunks", ctypes.c_int64), ("exp_hbytes", ctypes.c_int),
-                ("exp_layout", ctypes.c_int), ("exp_dot2", ctypes.c_int), ("centered", ctypes.c_int)]
+                ("exp_layout", ctypes.c_int), ("exp_dot2", ctypes.c_int), ("centered", ctypes.c_int),
+                ("exp_lt", ctypes.c_int)]
 
 
 class BackendError(RuntimeError):

@@ -244,6 +244,78 @@ __global__ __launch_bounds__(256) void exp_iota_kernel(uint32_t *__restrict__ v,
     if (t < n) v[t] = (uint32_t) t;
 }
 
+// lower-triangle join (build_expansion): a lower pair's row and H travel together through the transpose's sort
+template <typename T>
+struct lt_val {
+    T h;
+    int32_t i;
+};
+
+// row r's lower list (slots r cap .. r cap + cnt[r]) to the compact arrays at loff[r]: partner keys and (row, H);
+// one wave per row, coalesced
+template <typename T>
+__global__ __launch_bounds__(256) void exp_lt_compact_kernel(const int32_t *__restrict__ sj, const T *__restrict__ sv,
+                                                             const int64_t *__restrict__ cnt, const int64_t *__restrict__ loff,
+                                                             int64_t R, int64_t cap, uint32_t *__restrict__ lk,
+                                                             lt_val<T> *__restrict__ lv) {
+    const int64_t r = (int64_t) blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t b = loff[r];
+    for (int64_t k = lane; k < cnt[r]; k += 64) {
+        lk[b + k] = (uint32_t) sj[r * cap + k];
+        lv[b + k] = lt_val<T>{ sv[r * cap + k], (int32_t) r };
+    }
+}
+
+// per row j: its upper pairs are the run of key j in the sorted keys: ustart[j] = first, tot[j] = lower + upper count
+// (R + 1 entries: tot[R] = 0 for the scan's total)
+__global__ __launch_bounds__(256) void exp_lt_runs_kernel(const uint32_t *__restrict__ ks, int64_t NL,
+                                                          const int64_t *__restrict__ lcnt, int64_t R,
+                                                          int64_t *__restrict__ ustart, int64_t *__restrict__ tot) {
+    const int64_t j = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > R) return;
+    if (j == R) {
+        tot[R] = 0;
+        return;
+    }
+    auto lb = [&](uint32_t key) {
+        int64_t lo = 0, hi = NL;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (ks[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    const int64_t a = lb((uint32_t) j), b = lb((uint32_t) j + 1u);
+    ustart[j] = a;
+    tot[j] = lcnt[j] + (b - a);
+}
+
+// the symmetric rows: lower pair q (compact order) at off8[i] + (q - loff[i]); sorted pair p (partner j) at
+// off8[j] + lcnt[j] + (p - ustart[j]) — both coalesced
+template <typename T>
+__global__ __launch_bounds__(256) void exp_lt_place_kernel(const uint32_t *__restrict__ lk, const lt_val<T> *__restrict__ lv,
+                                                           const uint32_t *__restrict__ ks, const lt_val<T> *__restrict__ vs,
+                                                           int64_t NL, const int64_t *__restrict__ loff,
+                                                           const int64_t *__restrict__ lcnt,
+                                                           const int64_t *__restrict__ ustart,
+                                                           const int64_t *__restrict__ off8, int32_t *__restrict__ hj,
+                                                           T *__restrict__ hv) {
+    const int64_t q = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= NL) return;
+    const lt_val<T> a = lv[q];
+    const int64_t pl = off8[a.i] + (q - loff[a.i]);
+    hj[pl] = (int32_t) lk[q];
+    hv[pl] = a.h;
+    const uint32_t j = ks[q];
+    const lt_val<T> b = vs[q];
+    const int64_t pu = off8[j] + lcnt[j] + (q - ustart[j]);
+    hj[pu] = b.i;
+    hv[pu] = b.h;
+}
+
 // ---- row join: the remainder's symmetric rows built per row (default; PLSSVM_MI_EXP_JOIN=sort keeps the
 // column-join sort below) ------------------------------------------------------------------------------
 #ifndef RJ_NT_OPT
@@ -283,6 +355,9 @@ constexpr int RJ_PMAX = 256;   // passes per row at most (more: the rank takes t
 // Slot mode (off8 == nullptr, sj != nullptr; the default one-pass join): partner k of row r at sj[r cap + k]
 // for k < cap, cnt[r] = the row's count (also beyond cap: *cnt_max lets the host redo such rows by the two
 // passes), no pads — the count pass is not needed.
+// Lower mode (cposl != nullptr, round 5): only the partners j < i — the passes cover rows [0, i) and each column's
+// range ends at row i's own entry (cposl: the CSR entry's CSC position), so a row reads on average half of its
+// incidences; the other triangle is the transpose of these lists (build_expansion).
 __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__restrict__ rowptr,
                                                             const int32_t *__restrict__ col,
                                                             const int64_t *__restrict__ colptr,
@@ -290,7 +365,8 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
                                                             int64_t *__restrict__ cnt, const int64_t *__restrict__ off8,
                                                             int32_t *__restrict__ sj, unsigned int *__restrict__ ovf,
                                                             int pmax, int64_t cap, unsigned long long *__restrict__ cnt_max,
-                                                            const int64_t *__restrict__ csplit, int nsplit) {
+                                                            const int64_t *__restrict__ csplit, int nsplit,
+                                                            const int64_t *__restrict__ cposl = nullptr) {
     __shared__ uint32_t bm[RJ_BMW];
     __shared__ int32_t rep[RJ_LCAP];
     __shared__ int32_t zcol[RJ_ECAP];
@@ -322,7 +398,9 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
     constexpr int64_t SPAN_MAX = (int64_t) RJ_BMW * 32;
     int64_t span = SPAN_MAX;
     int passes = 0;
-    for (int64_t R0 = 0; R0 < m;) {
+    const bool lower = cposl != nullptr;
+    const int64_t Rend = lower ? i : m;  // partner rows [0, Rend)
+    for (int64_t R0 = 0; R0 < Rend;) {
         if (++passes > pmax) {  // uniform
             if ((!wr || slots) && tid == 0) {
                 cnt[r] = 0;
@@ -330,13 +408,39 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
             }
             return;
         }
-        const int64_t R1 = min(m, R0 + span);
+        const int64_t R1 = min(Rend, R0 + span);
         for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
         if (tid == 0) nrep_s = 0;
         // a pass over part of the partner rows reads only that part of each column (rows ascend within a
         // column: two binary searches per feature), not every incidence of the row once per pass
-        const bool whole = R0 == 0 && R1 >= m;
-        if (!whole) {
+        const bool whole = !lower && R0 == 0 && R1 >= m;
+        if (lower) {
+            // lower mode: each bound from the column's start (R0 = 0), the setup's table (a full-span boundary), row
+            // i's own position (R1 = i) or a binary search
+            for (int e = tid; e < ne; e += RJ_NT) {
+                const int64_t a = cst[e], b = a + (zoff[e + 1] - zoff[e]);
+                const int32_t f = zcol[e];
+                auto first_ge = [&](int64_t Rb) -> int64_t {
+                    if (csplit != nullptr && Rb % SPAN_MAX == 0) return csplit[(int64_t) f * nsplit + Rb / SPAN_MAX];
+                    int64_t lo = a, hi = b;
+                    while (lo < hi) {
+                        const int64_t mid = (lo + hi) >> 1;
+                        if (crow[mid] < Rb) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    return lo;
+                };
+                const int64_t lo = R0 == 0 ? a : first_ge(R0);
+                const int64_t lo2 = R1 == i ? cposl[e0 + e] : first_ge(R1);
+                pst[e] = lo;
+                pzoff[e + 1] = (int32_t) (lo2 - lo);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                pzoff[0] = 0;
+                for (int e = 0; e < ne; ++e) pzoff[e + 1] += pzoff[e];
+            }
+        } else if (!whole) {
             // a pass of the full span starts and ends where every row's passes do: the column positions come from the
             // setup's table (one load per feature) instead of two binary searches (a chain of dependent loads)
             const bool tab = csplit != nullptr && R0 % SPAN_MAX == 0 && (R1 >= m || R1 % SPAN_MAX == 0);
@@ -1982,7 +2086,131 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
         }
         read_lnz();
     };
-    if (row_join && R > 0) {
+    // Lower-triangle join (round 5; one rank holding every row): each row joins only its partners j < i (half the
+    // incidences), H is formed once per unordered pair, and the upper lists are the transpose — a stable radix sort
+    // of the lower pairs by partner (rows stay ascending within a partner). The symmetric rows, their partners and
+    // their H are bit for bit those of the full join (H_ij = H_ji: commutative products, features in ascending
+    // order). PLSSVM_MI_EXP_LT=0 keeps the full join. Anything unusual (a row beyond its slots, a dense cluster,
+    // out of memory) falls back to the full join below.
+    auto lt_join = [&]() -> bool {
+        const char *lte = std::getenv("PLSSVM_MI_EXP_LT");
+        const char *rj = std::getenv("PLSSVM_MI_EXP_RJ");
+        if ((lte != nullptr && std::strcmp(lte, "0") == 0) || (rj != nullptr && std::strcmp(rj, "twopass") == 0)) return false;
+        if (!(row_join && R > 0 && R == m && r0 == 0 && !shard && world == 1 && sim_world == 0 && cpos != nullptr &&
+              ex.rj_mean > 0.0 && m < (int64_t) INT32_MAX))
+            return false;
+        int64_t cap = round_up(std::max<int64_t>({ (int64_t) (2.0 * ex.rj_mean), (int64_t) (1.5 * ex.rj_max), 64 }), 8);
+        if (const char *e = std::getenv("PLSSVM_MI_EXP_RJ_CAP")) {
+            const long long v = std::atoll(e);
+            if (v > 0) cap = v;
+        }
+        const double room = csr.budget_b > 0 ? (double) (csr.budget_b - csr.est_bytes) : 0.0;
+        if ((double) R * (double) cap * (double) (4 + sizeof(T)) > room) return false;
+        try {
+            dev_buf<int32_t> ls;
+            dev_buf<T> lv;
+            dev_buf<int64_t> lcnt, lb, le;
+            ls.alloc(R * cap, stream, false);
+            lcnt.alloc(R + 1, stream);
+            lnz.alloc(3, stream);
+            dev_buf<unsigned int> ovf;
+            ovf.alloc(1, stream);
+            hipLaunchKernelGGL(exp_rowjoin_kernel, dim3((unsigned) R), dim3(RJ_NT), 0, stream, csr.rowptr.get(),
+                               csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, lcnt.get(), (const int64_t *) nullptr,
+                               ls.get(), ovf.get(), rj_pmax, cap, lnz.get() + 2, csplit.get(), nsplit, cpos);
+            MI_LAUNCH_CHECK();
+            unsigned long long cmax = 0ull;
+            unsigned int ov = 0u;
+            MI_HIP_CHECK(hipMemcpyAsync(&ov, ovf.get(), sizeof(ov), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipMemcpyAsync(&cmax, lnz.get() + 2, sizeof(cmax), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            if (ov != 0u || (int64_t) cmax > cap) return false;
+            pt.mark("expansion: row join, lower triangle");
+            lv.alloc(R * cap, stream, false);
+            lb.alloc(R, stream, false);
+            le.alloc(R, stream, false);
+            hipLaunchKernelGGL(exp_pool_range_kernel, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream, lcnt.get(),
+                               R, cap, lb.get(), le.get());
+            MI_LAUNCH_CHECK();
+            hipLaunchKernelGGL(exp_rowjoin_h_kernel<T>, dim3((unsigned) R), dim3(RJH_NT), 0, stream, csr.rowptr.get(),
+                               csr.col.get(), csr.val.get(), r0, phi, kbase, lb.get(), le.get(), ls.get(), lv.get(),
+                               lnz.get(), lnz.get() + 1);
+            MI_LAUNCH_CHECK();
+            read_lnz();  // pairs with H != 0 and the H bound: the lower pairs are every unordered pair
+            pt.mark("expansion: row join, lower triangle (H)");
+            // compact lower pairs, in row order (rows ascending, partners ascending)
+            dev_buf<int64_t> loff;
+            loff.alloc(R + 1, stream, false);
+            auto excl = [&](const int64_t *in, int64_t *out, int64_t n1) {
+                size_t tb = 0;
+                MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int) n1, stream));
+                dev_buf<unsigned char> t;
+                t.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
+                MI_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t.get(), tb, in, out, (int) n1, stream));
+            };
+            excl(lcnt.get(), loff.get(), R + 1);  // lcnt[R] = 0 (allocated zeroed)
+            int64_t NL = 0;
+            MI_HIP_CHECK(hipMemcpyAsync(&NL, loff.get() + R, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            if (NL >= (int64_t) INT32_MAX) return false;
+            const int64_t NLa = std::max<int64_t>(NL, 1);
+            dev_buf<uint32_t> lk, ks;
+            dev_buf<lt_val<T>> lvv, vs;
+            lk.alloc(NLa, stream, false);
+            lvv.alloc(NLa, stream, false);
+            hipLaunchKernelGGL(exp_lt_compact_kernel<T>, dim3((unsigned) ceil_div(R, 4)), dim3(256), 0, stream, ls.get(),
+                               lv.get(), lcnt.get(), loff.get(), R, cap, lk.get(), lvv.get());
+            MI_LAUNCH_CHECK();
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            ls.reset(), lv.reset(), lb.reset(), le.reset();
+            // the transpose: a stable sort of the pairs by partner (their row order kept within a partner)
+            ks.alloc(NLa, stream, false);
+            vs.alloc(NLa, stream, false);
+            if (NL > 0) {
+                int end_bit = 1;
+                while (end_bit < 32 && (int64_t(1) << end_bit) < m) ++end_bit;
+                size_t tb = 0;
+                MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, lk.get(), ks.get(), lvv.get(), vs.get(), (int) NL,
+                                                                0, end_bit, stream));
+                dev_buf<unsigned char> t;
+                t.alloc((int64_t) std::max<size_t>(tb, 16), stream, false);
+                MI_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(t.get(), tb, lk.get(), ks.get(), lvv.get(), vs.get(), (int) NL,
+                                                                0, end_bit, stream));
+            }
+            // the symmetric rows: row r = its lower list, then its upper list (ascending partners throughout)
+            dev_buf<int64_t> tot, ustart;
+            tot.alloc(R + 1, stream, false);
+            ustart.alloc(R + 1, stream, false);
+            hipLaunchKernelGGL(exp_lt_runs_kernel, dim3((unsigned) ceil_div(R + 1, 256)), dim3(256), 0, stream, ks.get(), NL,
+                               lcnt.get(), R, ustart.get(), tot.get());
+            MI_LAUNCH_CHECK();
+            off8.alloc(R + 1, stream, false);
+            excl(tot.get(), off8.get(), R + 1);
+            MI_HIP_CHECK(hipMemcpyAsync(&nslot8, off8.get() + R, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            sj.alloc(std::max<int64_t>(nslot8, 8), stream, false);
+            sv.alloc(std::max<int64_t>(nslot8, 8), stream, false);
+            if (NL > 0) {
+                hipLaunchKernelGGL(exp_lt_place_kernel<T>, dim3((unsigned) ceil_div(NL, 256)), dim3(256), 0, stream, lk.get(),
+                                   lvv.get(), ks.get(), vs.get(), NL, loff.get(), lcnt.get(), ustart.get(), off8.get(),
+                                   sj.get(), sv.get());
+                MI_LAUNCH_CHECK();
+            }
+            MI_HIP_CHECK(hipStreamSynchronize(stream));
+            rbeg = off8.get();
+            rend = off8.get() + 1;
+            pt.mark("expansion: row join, transpose");
+            return true;
+        } catch (const std::exception &e) {
+            if (exception_code(e) != -4) throw;
+            (void) hipGetLastError();
+            sj.reset(), sv.reset(), off8.reset();
+            rbeg = rend = nullptr;
+            return false;
+        }
+    };
+    if (lt_join()) ex.lt = true;
+    if (row_join && R > 0 && rbeg == nullptr) {
         const char *rj = std::getenv("PLSSVM_MI_EXP_RJ");
         const bool want = !(rj != nullptr && std::strcmp(rj, "twopass") == 0);
         int64_t cap = round_up(std::max<int64_t>({ (int64_t) (2.0 * ex.rj_mean), (int64_t) (1.5 * ex.rj_max), 64 }), 8);

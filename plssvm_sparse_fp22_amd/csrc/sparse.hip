@@ -1059,8 +1059,10 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                     csr.csc_r1 = local ? r1 : m;
                     // the two SELL plans (host work + uploads on a stream of their own) run on a host thread while
                     // the GPU builds the remainder's rows; build_expansion joins it before the group agreement
-                    std::exception_ptr plan_fail;
-                    hipStream_t ps = nullptr;
+                    // (round 5: the CSR plan needs no CSC values, so it runs on a thread of its own from the start; the
+                    // CSC plan's thread first fetches the CSC values — the two plans' host work overlaps)
+                    std::exception_ptr plan_fail, plan_fail2;
+                    hipStream_t ps = nullptr, ps2 = nullptr;
                     std::thread plans([&] {
                         try {
                             phase_timer tp;
@@ -1071,22 +1073,35 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                             build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0,
                                                rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22, csc_gen(csr.csc_r0, csr.csc_r1),
                                                blocks, ps, 0, 1, csr.ex.KM);
-                            build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks,
-                                               ps, 0, csr.ex.KM, 1);
                             MI_HIP_CHECK(hipStreamSynchronize(ps));
-                            tp.mark("setup_csr: SELL plans (host thread, beside the row join)");
+                            tp.mark("setup_csr: SELL plan CSC (host thread, beside the row join)");
                         } catch (...) {
                             plan_fail = std::current_exception();
+                        }
+                    });
+                    std::thread plans2([&] {
+                        try {
+                            phase_timer tp;
+                            MI_HIP_CHECK(hipSetDevice(device));
+                            MI_HIP_CHECK(hipStreamCreateWithFlags(&ps2, hipStreamNonBlocking));
+                            build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks,
+                                               ps2, 0, csr.ex.KM, 1);
+                            MI_HIP_CHECK(hipStreamSynchronize(ps2));
+                            tp.mark("setup_csr: SELL plan CSR (host thread, beside the row join)");
+                        } catch (...) {
+                            plan_fail2 = std::current_exception();
                         }
                     });
                     bool joined = false;
                     auto join_plans = [&]() -> std::exception_ptr {
                         if (!joined) {
                             plans.join();
+                            plans2.join();
                             joined = true;
                             if (ps != nullptr) (void) hipStreamDestroy(ps);
+                            if (ps2 != nullptr) (void) hipStreamDestroy(ps2);
                         }
-                        return plan_fail;
+                        return plan_fail ? plan_fail : plan_fail2;
                     };
                     try {
                         build_expansion(cpos_d.get(), max_inc, join_plans);

@@ -89,6 +89,7 @@ struct exp_data {
     bool dot2 = true;                 // bfloat16 H: the dot-instruction kernel (PLSSVM_MI_EXP_DOT2=0: the FMA chain)
     bool rflags = false;              // hbf16 chunks without hrow: bit 14 of a chunk's first H marks a row's first chunk
     bool rpairs = false;              // with rflags: the flags mark slot pairs (cells padded to 2 slots, not 4; layout 4)
+    bool lt = false;                  // the symmetric rows came from the lower-triangle join + transpose
     double rj_mean = 0.0, rj_max = 0.0;  // setup's sample of the rank's rows: partners sharing >= 2 features (mean, max)
     double hratio = -1.0;             // row join: max |H_ij| / |kernel value of the pair| (< 0: unknown)
     dev_buf<uint16_t> hrow;           // [nchunks] block-local row of each 4-slot chunk

@@ -695,3 +695,30 @@ def test_expansion_row_join_column_split_table(monkeypatch):
             out[mode] = (svm.kp_part(x, "overlap"), info["pairs"], info["pair_slots"])
     assert out["table"][1:] == out["search"][1:] and out["table"][1] > 0
     np.testing.assert_array_equal(out["table"][0], out["search"][0])
+
+
+@pytest.mark.parametrize("kernel,dtype,shape", [("rbf", np.float32, (140000, 3000, 20)), ("rbf", np.float64, (20000, 2000, 16)),
+                                                ("polynomial", np.float64, (3000, 50, 20)),
+                                                ("rbf", np.float32, (1_100_001, 20000, 4))])
+def test_expansion_lower_triangle_join_bitwise(kernel, dtype, shape, monkeypatch):
+    """The lower-triangle row join (round 5: each row joins only its partners j < i — every column read up to the
+    row's own entry — H once per unordered pair, the upper lists by a stable radix sort of the pairs by partner)
+    against the full row join (PLSSVM_MI_EXP_LT=0): the same symmetric rows, H bit for bit (H_ij = H_ji), so the same
+    pairs, slots and K·p bits — incl. dense-ish rows (3000 x 50 @ 40 %) and 1.1M rows, whose lower lists span two
+    bitmap passes (the column split table below row i, row i's own CSC position as the last bound)."""
+    n, d, k = shape
+    csr, _ = datagen.sparse_csr(n, d, k, seed=31, dtype=dtype)
+    x = np.random.default_rng(4).uniform(-1, 2, n - 1).astype(dtype)
+    out = {}
+    for lt in ("1", "0"):
+        monkeypatch.setenv("PLSSVM_MI_EXP_LT", lt)
+        with sparse_svm(csr, kernel, dtype, algo="expansion", coef0=1.0) as svm:
+            svm.setup_data_on_device()
+            info = svm.info()
+            assert info["sparse_algo"] == pm._abi.SPARSE_EXPANSION
+            out[lt] = (info["exp_lt"], info["pairs"], info["pair_slots"], info["exp_hbytes"],
+                       svm.kp_part(x, "kernel"), svm.kp_part(x, "overlap"))
+    assert out["1"][0] == 1 and out["0"][0] == 0
+    assert out["1"][1:4] == out["0"][1:4]
+    np.testing.assert_array_equal(out["1"][4], out["0"][4])
+    np.testing.assert_array_equal(out["1"][5], out["0"][5])
