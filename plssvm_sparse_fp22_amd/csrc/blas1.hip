@@ -228,19 +228,22 @@ __global__ __launch_bounds__(CG_NT) void cg_upd_rr_kernel(T *__restrict__ x, T *
     if (!reset) store_partial1(s1, red, prr);
 }
 
-template <typename T>
+template <typename T, bool W>
 __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, const T *__restrict__ r,
                                                           const T *__restrict__ q, const T *__restrict__ prr, int G,
                                                           int init, double *trace, int64_t trace_cap, int64_t m,
-                                                          T *__restrict__ psum, cg_scalars<T> *sc) {
+                                                          T *__restrict__ psum, cg_scalars<T> *sc, dir_w_t<T> wo) {
     if (sc->converged) return;
     __shared__ T red[CG_NT / 64], bc[1];
     const int64_t i0 = (int64_t) blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t) gridDim.x * blockDim.x;
-    T dv[CG_PRE], rv[CG_PRE], qv[CG_PRE];
+    T dv[CG_PRE], rv[CG_PRE], qv[CG_PRE], ev[CG_PRE], cv[CG_PRE];
 #pragma unroll
     for (int e = 0; e < CG_PRE; ++e) {
         const int64_t i = i0 + e * st;
-        if (i < m) dv[e] = init ? T(0) : d[i], rv[e] = r[i], qv[e] = q[i];
+        if (i < m) {
+            dv[e] = init ? T(0) : d[i], rv[e] = r[i], qv[e] = q[i];
+            if constexpr (W) ev[e] = wo.e != nullptr ? wo.e[i] : T(1), cv[e] = wo.cw != nullptr ? wo.cw[i] : T(0);
+        }
     }
     T beta = 0;
     if (!init) {
@@ -258,8 +261,8 @@ __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, c
         }
         if (conv) return;  // the same decision in every block
     }
-    T s1 = 0, s2 = 0;
-    auto one = [&](int64_t i, T d_, T r_, T q_) {
+    T s1 = 0, s2 = 0, s3 = 0;
+    auto one = [&](int64_t i, T d_, T r_, T q_, T e_, T c_) {
         T dn;
         if (init) {
             dn = r_;
@@ -270,14 +273,26 @@ __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, c
         d[i] = dn;
         s1 += dn;
         s2 += q_ * dn;
+        if constexpr (W) w_elem(i, dn, e_, c_, wo.e, wo.cw, wo.w, wo.w16, s3);
     };
 #pragma unroll
     for (int e = 0; e < CG_PRE; ++e) {
         const int64_t i = i0 + e * st;
-        if (i < m) one(i, dv[e], rv[e], qv[e]);
+        if (i < m) {
+            if constexpr (W) one(i, dv[e], rv[e], qv[e], ev[e], cv[e]);
+            else one(i, dv[e], rv[e], qv[e], T(1), T(0));
+        }
     }
-    for (int64_t i = i0 + CG_PRE * st; i < m; i += st) one(i, init ? T(0) : d[i], r[i], q[i]);
+    for (int64_t i = i0 + CG_PRE * st; i < m; i += st) {
+        if constexpr (W)
+            one(i, init ? T(0) : d[i], r[i], q[i], wo.e != nullptr ? wo.e[i] : T(1), wo.cw != nullptr ? wo.cw[i] : T(0));
+        else one(i, init ? T(0) : d[i], r[i], q[i], T(1), T(0));
+    }
     store_partials(s1, s2, red, psum);
+    if constexpr (W) {
+        __syncthreads();
+        store_partial1(s3, red, wo.spart);
+    }
 }
 
 }  // namespace
@@ -301,9 +316,13 @@ void launch_cg_upd_rr(T *x, T *r, const T *d, const T *Ad, const T *b, int reset
 
 template <typename T>
 void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int G, int init, double *trace,
-                        int64_t trace_cap, int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s) {
-    hipLaunchKernelGGL(cg_dir_sums_kernel<T>, dim3(RED_BLOCKS), dim3(CG_NT), 0, s, d, r, q, prr, G, init, trace,
-                       trace_cap, m, psum, sc);
+                        int64_t trace_cap, int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s, const dir_w_t<T> *wout) {
+    if (wout != nullptr)
+        hipLaunchKernelGGL((cg_dir_sums_kernel<T, true>), dim3(RED_BLOCKS), dim3(CG_NT), 0, s, d, r, q, prr, G, init,
+                           trace, trace_cap, m, psum, sc, *wout);
+    else
+        hipLaunchKernelGGL((cg_dir_sums_kernel<T, false>), dim3(RED_BLOCKS), dim3(CG_NT), 0, s, d, r, q, prr, G, init,
+                           trace, trace_cap, m, psum, sc, dir_w_t<T>{});
     MI_LAUNCH_CHECK();
 }
 
@@ -367,7 +386,7 @@ void launch_cg_direction(T *d, const T *r, int64_t m, const cg_scalars<T> *sc, h
     template void launch_cg_upd_rr<T>(T *, T *, const T *, const T *, const T *, int, const T *, int, int64_t, T *, \
                                       cg_scalars<T> *, hipStream_t);                                                \
     template void launch_cg_dir_sums<T>(T *, const T *, const T *, const T *, int, int, double *, int64_t, int64_t, \
-                                        T *, cg_scalars<T> *, hipStream_t);
+                                        T *, cg_scalars<T> *, hipStream_t, const dir_w_t<T> *);
 INST(float)
 INST(double)
 #undef INST

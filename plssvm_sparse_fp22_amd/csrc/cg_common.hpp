@@ -124,5 +124,26 @@ __device__ __forceinline__ T cg_acc(T s, T a, T b) {
     return s + a * b;
 }
 
+// bfloat16 of a float, round to nearest even (finite values)
+__device__ __forceinline__ uint16_t bf16_rne(float f) {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t) (u >> 16);
+}
+
+// element i of the kernel expansion's w pass: w_i = e_i p_i (e null: w = p, not written), its bfloat16 copy, and
+// the S term (cw non-null: the centered cw_i w_i) added to s — one definition for exp_wown_kernel and the
+// direction update that carries it (blas1.hip), so both give the same bits
+template <typename T>
+__device__ __forceinline__ void w_elem(int64_t i, T v, T ev, T cv, const T *e, const T *cw, T *__restrict__ w,
+                                       uint16_t *__restrict__ w16, T &s) {
+    if (e != nullptr) {
+        v = ev * v;
+        w[i] = v;
+    }
+    s += cw != nullptr ? cv * v : v;
+    w16[i] = bf16_rne((float) v);
+}
+
 }  // namespace cgk
 }  // namespace plssvm_mi

@@ -87,6 +87,7 @@ engine<T>::engine(int kernel_, int degree_, double gamma_, double coef0_, double
     MI_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     sc.alloc(1, stream);
     red.alloc(2 * RED_BLOCKS, stream);
+    wsp.alloc(2 * RED_BLOCKS, stream);
     cgp.alloc(6 * RED_BLOCKS, stream);
 }
 
@@ -531,8 +532,11 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
     launch_dot2<T>(r.get() + v0, r.get() + v0, nullptr, nullptr, vn, red.get(), nullptr, stream);
     launch_dot_final<T>(gather_partials(red.get(), 3), sc.get(), FIN_DELTA0, 0, trace.get(), trace_cap, nullptr, stream, G);
     // d = r, with sum d / sum q d for the first Q~d
+    dir_w_t<T> wo{};
+    const bool fw = dir_w_fill(wo);
     launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, qf() + v0, nullptr, 1, 1, nullptr, 0, vn, cgp.get(), sc.get(),
-                          stream);
+                          stream, fw ? &wo : nullptr);
+    w_pre = fw ? dv.get() : nullptr;
     if (gathered && comm != nullptr) psum_pending = true;  // gathered with the first K·p's collective
     else gather_partials(cgp.get(), 0);
     run = 0;
@@ -595,8 +599,12 @@ void engine<T>::cg_iter(int reset) {
         launch_dot2<T>(r.get() + v0, r.get() + v0, nullptr, nullptr, vn, prr, st, stream);
     }
     // delta = r.r ; stop test ; beta (:135-146); d = beta d + r (:149-151), with sum d / sum q d
+    // (kernel expansion, bfloat16 windows: with the next K·p's w pass, dir_w_fill)
+    dir_w_t<T> wo{};
+    const bool fw = dir_w_fill(wo);
     launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, qf() + v0, gather_partials(prr, 2), G, 0, trace.get(), trace_cap,
-                          vn, psum, sc.get(), stream);
+                          vn, psum, sc.get(), stream, fw ? &wo : nullptr);
+    w_pre = fw ? dv.get() : nullptr;
     if (gathered && comm != nullptr) psum_pending = true;  // gathered with the next K·p's first collective
     else gather_partials(psum, 0);
 }
@@ -628,14 +636,21 @@ template <typename T>
 void engine<T>::graph_capture() {
     if (cg_graph == nullptr) {
         hipGraph_t g = nullptr;
+        // a block forms its first w itself (the replay may follow any other K·p); w_pre stays what the launched
+        // work left, graph_w_end is what a replay leaves
+        const T *keep = w_pre;
+        w_pre = nullptr;
         MI_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
         try {
             for (int k = 0; k < CG_RESET; ++k) cg_iter(k == CG_RESET - 1 ? 1 : 0);
         } catch (...) {
             (void) hipStreamEndCapture(stream, &g);
             if (g) (void) hipGraphDestroy(g);
+            w_pre = keep;
             throw;
         }
+        graph_w_end = w_pre;
+        w_pre = keep;
         MI_HIP_CHECK(hipStreamEndCapture(stream, &g));
         const hipError_t e = hipGraphInstantiate(&cg_graph, g, nullptr, nullptr, 0);
         (void) hipGraphDestroy(g);
@@ -647,6 +662,7 @@ template <typename T>
 void engine<T>::graph_block() {
     graph_capture();
     MI_HIP_CHECK(hipGraphLaunch(cg_graph, stream));
+    w_pre = graph_w_end;
 }
 
 template <typename T>

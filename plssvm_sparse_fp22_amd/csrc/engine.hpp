@@ -100,6 +100,13 @@ struct engine : engine_base {
 
     // ---- vectors (n_pad, zero padded) ----
     dev_buf<T> partial, q, pv, ret, x, r, dv, Ad, b, raw, w, red;
+    // kernel expansion with bfloat16 windows (round 5): the S partials of the w pass (exp_wown_kernel, or the direction
+    // update that carries it: dir_w_fill); w_pre = the vector whose w, bfloat16 copy and S partials are in place
+    // (set after a carrying direction update of dv, cleared by any other w pass), graph_w_end = w_pre after a
+    // captured iteration block
+    dev_buf<T> wsp;
+    const T *w_pre = nullptr, *graph_w_end = nullptr;
+    bool dir_w_fill(dir_w_t<T> &o);
     dev_buf<T> cgp;  // fused CG partials: [0, 2R) sum d / sum q d, [2R, 4R) d.Ad, [4R, 6R) r.r
     dev_buf<cg_scalars<T>> sc;
     dev_buf<double> trace;

@@ -860,12 +860,7 @@ __global__ __launch_bounds__(256) void exp_cell_pad_groups_kernel(int64_t ngroup
     if (s & 2) c[RPW - 1] += 2;
 }
 
-// bfloat16 of a float, round to nearest even (finite values)
-__device__ __forceinline__ uint16_t bf16_rne(float f) {
-    uint32_t u = __float_as_uint(f);
-    u += 0x7FFFu + ((u >> 16) & 1u);
-    return (uint16_t) (u >> 16);
-}
+using cgk::bf16_rne;
 
 // S = sum_j w_j (cw non-null: the centered S_c = sum_j cw_j w_j, engine.hpp ctr_*) as RED_BLOCKS block partials
 // in dot2_kernel's grid, order and block reduction (bitwise the same partials), writing the remainder stream's
@@ -899,46 +894,35 @@ __global__ __launch_bounds__(256) void exp_wsum_kernel(const T *__restrict__ w, 
 // with the group's other partials and summed in rank order: the same S on every rank)
 // (cw non-null: the rows' share of the centered S_c = sum_j cw_j w_j instead, engine.hpp ctr_*)
 template <typename T>
-__global__ __launch_bounds__(256) void exp_wown_kernel(const T *__restrict__ e, const T *__restrict__ p, int64_t ib,
-                                                       int64_t ie, T *__restrict__ w, uint16_t *__restrict__ w16,
-                                                       const T *__restrict__ cw, T *__restrict__ partials,
-                                                       const cg_scalars<T> *__restrict__ status) {
+__global__ __launch_bounds__(cgk::CG_NT) void exp_wown_kernel(const T *__restrict__ e, const T *__restrict__ p,
+                                                             int64_t ib, int64_t ie, T *__restrict__ w,
+                                                             uint16_t *__restrict__ w16, const T *__restrict__ cw,
+                                                             T *__restrict__ partials,
+                                                             const cg_scalars<T> *__restrict__ status) {
     if (status != nullptr && status->converged) return;
-    __shared__ T red[4];
+    __shared__ T red[cgk::CG_NT / 64];
     T s1 = 0;
-    const int64_t st = (int64_t) gridDim.x * blockDim.x;
-    auto one = [&](int64_t i, T v, T ev, T cv) {
-        if (e != nullptr) {
-            v = ev * v;
-            w[i] = v;
-        }
-        s1 += cw != nullptr ? cv * v : v;
-        w16[i] = bf16_rne((float) v);
-    };
-    int64_t i = ib + (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    // four elements' loads in flight per thread, then summed in the thread's element order (the one-at-a-time bits)
-    for (; i + 3 * st < ie; i += 4 * st) {
+    // the fused CG kernels' grid and element order (cg_dir_sums_kernel carries this pass in a CG iteration: the
+    // same partials bit for bit); four elements' loads in flight per thread, summed in the thread's element order
+    const int64_t n = ie - ib, st = (int64_t) gridDim.x * blockDim.x;
+    const T *pp = p + ib, *ep = e != nullptr ? e + ib : nullptr, *cp = cw != nullptr ? cw + ib : nullptr;
+    T *wp = w + ib;
+    uint16_t *w16p = w16 + ib;
+    int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * st < n; i += 4 * st) {
         T pv[4], ev[4], cv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            pv[u] = p[i + u * st];
-            ev[u] = e != nullptr ? e[i + u * st] : T(1);
-            cv[u] = cw != nullptr ? cw[i + u * st] : T(0);
+            pv[u] = pp[i + u * st];
+            ev[u] = ep != nullptr ? ep[i + u * st] : T(1);
+            cv[u] = cp != nullptr ? cp[i + u * st] : T(0);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) one(i + u * st, pv[u], ev[u], cv[u]);
+        for (int u = 0; u < 4; ++u) cgk::w_elem(i + u * st, pv[u], ev[u], cv[u], ep, cp, wp, w16p, s1);
     }
-    for (; i < ie; i += st) one(i, p[i], e != nullptr ? e[i] : T(1), cw != nullptr ? cw[i] : T(0));
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) s1 += __shfl_xor(s1, o);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s1;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        T t = 0;
-        for (int v = 0; v < 4; ++v) t += red[v];
-        partials[blockIdx.x] = t;
-        partials[RED_BLOCKS + blockIdx.x] = T(0);
-    }
+    for (; i < n; i += st)
+        cgk::w_elem(i, pp[i], ep != nullptr ? ep[i] : T(1), cp != nullptr ? cp[i] : T(0), ep, cp, wp, w16p, s1);
+    cgk::store_partial1(s1, red, partials);
 }
 
 template <typename T>
@@ -2692,6 +2676,31 @@ void engine<T>::expansion_mscale(const cg_scalars<T> *status) {
     MI_LAUNCH_CHECK();
 }
 
+// The CG direction update carries the next K·p's w pass (round 5): with bfloat16 windows the K·p of d starts with
+// exp_wown_kernel over the rows the direction update has just written (w = e d, its bfloat16 copy, S partials); the
+// update forms them in its own element loop (cgk::w_elem, the same grid and order: the same bits) and the K·p skips
+// the launch. Sharded: the rank's rows, whose w the group then gathers as before. PLSSVM_MI_DIR_W=0: off.
+template <typename T>
+bool engine<T>::dir_w_fill(dir_w_t<T> &o) {
+    static const bool on = [] {
+        const char *e = std::getenv("PLSSVM_MI_DIR_W");
+        return e == nullptr || std::atoi(e) != 0;
+    }();
+    if (!on || !sparse_stored() || factored() || csr.otf_on || !csr.ex.on || !csr.ex.hbf16) return false;
+    if (shard) {  // expansion_kp_raw's g16 over [r0, r1)
+        const bool rgrp = comm != nullptr && cstream != nullptr;
+        if (d <= 0 || !(rgrp || sim_world > 0) || v0 != r0 || vn != r1 - r0) return false;
+    } else if (v0 != 0 || vn != m) {  // wown_all over [0, m)
+        return false;
+    }
+    o.e = kernel == 2 ? csr.e.get() + v0 : nullptr;
+    o.w = kernel == 2 ? csr.ex.wv.get() + v0 : nullptr;
+    o.w16 = csr.ex.wv16.get() + v0;
+    o.cw = ctr_active() && kernel == 2 ? ctr_cw.get() + v0 : nullptr;
+    o.spart = wsp.get();
+    return true;
+}
+
 template <typename T>
 void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool with_base) {
     auto &ex = csr.ex;
@@ -2708,10 +2717,17 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     const bool wown_all = !shard && ex.hbf16;
     // centered finalize (engine.hpp ctr_*): S becomes S_c = sum_j cw_j w_j, the combine's base c_i S_c (rbf) / 0 (poly)
     const T *cw = ctr_now && kernel == 2 ? ctr_cw.get() : nullptr;
+    // the w pass's S partials (spt): wsp for exp_wown_kernel and the direction update that carries it (w_pre == p:
+    // done, dir_w_fill), red for exp_wsum_kernel
+    T *spt = (g16 || wown_all) ? wsp.get() : red.get();
+    const bool pre = (g16 || wown_all) && w_pre != nullptr && w_pre == p;
+    w_pre = nullptr;  // any other w pass below overwrites w, its copy and the partials
     if (g16 || wown_all) {
-        hipLaunchKernelGGL(exp_wown_kernel<T>, dim3(RED_BLOCKS), dim3(256), 0, stream, kernel == 2 ? csr.e.get() : nullptr,
-                           p, ib, ie, ex.wv.get(), ex.wv16.get(), cw, red.get(), status);
-        MI_LAUNCH_CHECK();
+        if (!pre) {
+            hipLaunchKernelGGL(exp_wown_kernel<T>, dim3(RED_BLOCKS), dim3(cgk::CG_NT), 0, stream,
+                               kernel == 2 ? csr.e.get() : nullptr, p, ib, ie, ex.wv.get(), ex.wv16.get(), cw, spt, status);
+            MI_LAUNCH_CHECK();
+        }
         if (kernel == 2) w = ex.wv.get();
     } else if (kernel == 2) {
         if (ie > ib)
@@ -2734,7 +2750,7 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
         if (g16) {
             MI_NCCL_CHECK(ncclAllGather(ex.wv16.get() + (int64_t) rank * chunk, ex.wv16.get(), (size_t) chunk, ncclBfloat16,
                                         comm, cstream));
-            MI_NCCL_CHECK(ncclAllGather(red.get(), sg, (size_t) (2 * RED_BLOCKS), nccl_type<T>(), comm, cstream));
+            MI_NCCL_CHECK(ncclAllGather(spt, sg, (size_t) (2 * RED_BLOCKS), nccl_type<T>(), comm, cstream));
         } else {
             MI_NCCL_CHECK(ncclAllGather(const_cast<T *>(w) + (int64_t) rank * chunk, const_cast<T *>(w), (size_t) chunk,
                                         nccl_type<T>(), comm, cstream));
@@ -2762,8 +2778,8 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
     } else if (g16) {
         // S from w's partials: inside the moment reduce when the moment pass has one (one launch fewer)
         const bool sfold = d > 0 && expansion_moments_fused();
-        if (!sfold) launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
-        expansion_moments(w, status, sfold ? red.get() : nullptr, 1);
+        if (!sfold) launch_dot_final<T>(spt, sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+        expansion_moments(w, status, sfold ? spt : nullptr, 1);
         expansion_dominant(w, status);
     } else {
         gather_input(w);
@@ -2773,8 +2789,8 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
             MI_LAUNCH_CHECK();
         }
         const bool sfold = d > 0 && expansion_moments_fused();
-        if (!sfold) launch_dot_final<T>(red.get(), sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
-        expansion_moments(w, status, sfold ? red.get() : nullptr, 1);
+        if (!sfold) launch_dot_final<T>(spt, sc.get(), FIN_PLAIN, 0, nullptr, 0, csr.ssc.get(), stream);
+        expansion_moments(w, status, sfold ? spt : nullptr, 1);
         expansion_dominant(w, status);
     }
     T kappa = 0;
@@ -3209,6 +3225,7 @@ int exp_dot2_built() { return EXP_DOT2 ? 1 : 0; }
     template bool engine<T>::expansion_moments_fused() const;        \
     template coefs engine<T>::expansion_coefs() const;                                       \
     template void engine<T>::expansion_kp_raw(const T *, const cg_scalars<T> *, bool);      \
+    template bool engine<T>::dir_w_fill(dir_w_t<T> &);                                        \
     template bool engine<T>::ctr_active() const;                                              \
     template T engine<T>::QAf() const;                                                        \
     template void engine<T>::ctr_setup();                                                     \

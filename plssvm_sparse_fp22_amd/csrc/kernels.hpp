@@ -127,9 +127,20 @@ void launch_cg_upd_rr(T *x, T *r, const T *d, const T *Ad, const T *b, int reset
                       T *prr, cg_scalars<T> *sc, hipStream_t s);
 // delta = r.r (prr), stop test, beta; d = beta d + r (init: d = r, scalars untouched);
 // sum d / sum q d partials -> psum. The iteration index is sc->iters (trace[iters + 1] = delta, iters += 1).
+// wout non-null (kernel expansion with bfloat16 windows, round 5): the next K·p's first kernel rides along — w = e d
+// (e null: w = d, not written), its bfloat16 copy and the S partials (cw non-null: the centered S_c), in
+// exp_wown_kernel's grid, element order and block reduction (bitwise its partials)
+template <typename T>
+struct dir_w_t {
+    const T *e;
+    T *w;
+    uint16_t *w16;
+    const T *cw;
+    T *spart;
+};
 template <typename T>
 void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int G, int init, double *trace, int64_t trace_cap,
-                        int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s);
+                        int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s, const dir_w_t<T> *wout = nullptr);
 
 // ---- sparse (CSR / FP22) ------------------------------------------------------------------------
 // declared in sparse.hpp

@@ -921,14 +921,36 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         csr.csc_r1 = local ? r1 : m;
         const bool f22 = val_fmt == PLSSVM_MI_VAL_FP22 && sell_fp22_stream();
         const int64_t blocks = sell_target_blocks();
-        need_cval_h(stream);
-        // the K·p reads only the SELL streams: no device CSC
-        cpos_d.reset(), csr.colptr.reset(), csr.crow.reset(), csr.cval.reset();
-        build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22,
-                           csc_gen(csr.csc_r0, csr.csc_r1), blocks, stream);
-        build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks, stream);
-        if (world == 1 && sim_world == 0 && rowblock_fused_enabled())  // CG iterations: CSR pass + finalize in one launch
-            build_rowblock_plan<T>(csr.rb_csr, m, d, f22, csr_gen(0), blocks, stream);
+        // the CSR-side plans need no CSC values: a host thread builds them (uploads on a stream of its own) while this
+        // thread fetches the CSC values and builds the CSC plan (round 5)
+        std::exception_ptr rfail;
+        hipStream_t rs = nullptr;
+        std::thread rplans([&] {
+            try {
+                MI_HIP_CHECK(hipSetDevice(device));
+                MI_HIP_CHECK(hipStreamCreateWithFlags(&rs, hipStreamNonBlocking));
+                build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks, rs);
+                if (world == 1 && sim_world == 0 && rowblock_fused_enabled())  // CG: CSR pass + finalize in one launch
+                    build_rowblock_plan<T>(csr.rb_csr, m, d, f22, csr_gen(0), blocks, rs);
+                MI_HIP_CHECK(hipStreamSynchronize(rs));
+            } catch (...) {
+                rfail = std::current_exception();
+            }
+        });
+        std::exception_ptr cfail;
+        try {
+            need_cval_h(stream);
+            // the K·p reads only the SELL streams: no device CSC
+            cpos_d.reset(), csr.colptr.reset(), csr.crow.reset(), csr.cval.reset();
+            build_spmv_plan<T>(csr.spmv_csc, d, csr.csc_r1 - csr.csc_r0, rowptr[csr.csc_r1] - rowptr[csr.csc_r0], f22,
+                               csc_gen(csr.csc_r0, csr.csc_r1), blocks, stream);
+        } catch (...) {
+            cfail = std::current_exception();
+        }
+        rplans.join();
+        if (rs != nullptr) (void) hipStreamDestroy(rs);
+        if (cfail) std::rethrow_exception(cfail);
+        if (rfail) std::rethrow_exception(rfail);
         pt.mark("setup_csr: SELL plans");
         return;
     }
