@@ -318,14 +318,18 @@ __global__ __launch_bounds__(256) void exp_lt_place_kernel(const uint32_t *__res
 
 // ---- row join: the remainder's symmetric rows built per row (default; PLSSVM_MI_EXP_JOIN=sort keeps the
 // column-join sort below) ------------------------------------------------------------------------------
+// 512-thread workgroups with a 64 KiB bitmap (round 5): ~79 KiB of LDS each, so two rows are joined per CU at once
+// (their incidence reads in flight together, one row's barriers and scans under the other's reads); the rounds-3/4
+// 1024-thread form with a 128 KiB bitmap held one row per CU (`-DRJ_NT_OPT=1024 -DRJ_BMW_OPT=32768`): join 25 % /
+// 13 % slower on 3-RBF / config 5 in a same-box A/B (profiles/r05_join_ab.json), though a pass covers twice the rows
 #ifndef RJ_NT_OPT
-#define RJ_NT_OPT 1024
+#define RJ_NT_OPT 512
 #endif
 #ifndef RJ_BMW_OPT
-#define RJ_BMW_OPT 32768
+#define RJ_BMW_OPT 16384
 #endif
 constexpr int RJ_NT = RJ_NT_OPT;
-constexpr int RJ_BMW = RJ_BMW_OPT;  // bitmap words: 1 048 576 partner rows per pass (128 KiB of LDS)
+constexpr int RJ_BMW = RJ_BMW_OPT;  // bitmap words: 524 288 partner rows per pass (64 KiB of LDS)
 constexpr int RJ_LCAP = 2048;  // repeat sightings held per pass (more: the pass range is halved)
 constexpr int RJ_ECAP = 256;   // entries of row i held in LDS (longer rows: the sort join)
 constexpr int RJ_WPT = RJ_BMW / RJ_NT;
@@ -2103,6 +2107,10 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
                                csr.col.get(), csr.colptr.get(), csr.crow.get(), m, r0, lcnt.get(), (const int64_t *) nullptr,
                                ls.get(), ovf.get(), rj_pmax, cap, lnz.get() + 2, csplit.get(), nsplit, cpos);
             MI_LAUNCH_CHECK();
+            // the H buffers are mapped while the join runs (a multi-GB hipMalloc is tens of ms of host time)
+            lv.alloc(R * cap, stream, false);
+            lb.alloc(R, stream, false);
+            le.alloc(R, stream, false);
             unsigned long long cmax = 0ull;
             unsigned int ov = 0u;
             MI_HIP_CHECK(hipMemcpyAsync(&ov, ovf.get(), sizeof(ov), hipMemcpyDeviceToHost, stream));
@@ -2110,9 +2118,6 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             MI_HIP_CHECK(hipStreamSynchronize(stream));
             if (ov != 0u || (int64_t) cmax > cap) return false;
             pt.mark("expansion: row join, lower triangle");
-            lv.alloc(R * cap, stream, false);
-            lb.alloc(R, stream, false);
-            le.alloc(R, stream, false);
             hipLaunchKernelGGL(exp_pool_range_kernel, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream, lcnt.get(),
                                R, cap, lb.get(), le.get());
             MI_LAUNCH_CHECK();
