@@ -318,18 +318,20 @@ __global__ __launch_bounds__(256) void exp_lt_place_kernel(const uint32_t *__res
 
 // ---- row join: the remainder's symmetric rows built per row (default; PLSSVM_MI_EXP_JOIN=sort keeps the
 // column-join sort below) ------------------------------------------------------------------------------
-// 512-thread workgroups with a 64 KiB bitmap (round 5): ~79 KiB of LDS each, so two rows are joined per CU at once
-// (their incidence reads in flight together, one row's barriers and scans under the other's reads); the rounds-3/4
-// 1024-thread form with a 128 KiB bitmap held one row per CU (`-DRJ_NT_OPT=1024 -DRJ_BMW_OPT=32768`): join 25 % /
-// 13 % slower on 3-RBF / config 5 in a same-box A/B (profiles/r05_join_ab.json), though a pass covers twice the rows
+// 512-thread workgroups with a 32 KiB bitmap (round 5): 47 KiB of LDS and 75 VGPRs each, so three rows are joined
+// per CU at once (their incidence reads in flight together, one row's barriers and scans under the others' reads).
+// The rounds-3/4 form (1024 threads, 128 KiB bitmap: `-DRJ_NT_OPT=1024 -DRJ_BMW_OPT=32768`) held one row per CU;
+// same-box A/Bs (profiles/r05_join_ab.json): the 3-RBF / config-5 join 0.18–0.21 / 0.29 s there, 0.14–0.17 / 0.24–0.25 s
+// with two rows per CU (512 threads, 64 KiB), 0.12 / 0.21 s with three — more passes per row (262 144 partner rows each)
+// cost less than the parallelism gains
 #ifndef RJ_NT_OPT
 #define RJ_NT_OPT 512
 #endif
 #ifndef RJ_BMW_OPT
-#define RJ_BMW_OPT 16384
+#define RJ_BMW_OPT 8192
 #endif
 constexpr int RJ_NT = RJ_NT_OPT;
-constexpr int RJ_BMW = RJ_BMW_OPT;  // bitmap words: 524 288 partner rows per pass (64 KiB of LDS)
+constexpr int RJ_BMW = RJ_BMW_OPT;  // bitmap words: 262 144 partner rows per pass (32 KiB of LDS)
 constexpr int RJ_LCAP = 2048;  // repeat sightings held per pass (more: the pass range is halved)
 constexpr int RJ_ECAP = 256;   // entries of row i held in LDS (longer rows: the sort join)
 constexpr int RJ_WPT = RJ_BMW / RJ_NT;
@@ -362,7 +364,12 @@ constexpr int RJ_PMAX = 256;   // passes per row at most (more: the rank takes t
 // Lower mode (cposl != nullptr, round 5): only the partners j < i — the passes cover rows [0, i) and each column's
 // range ends at row i's own entry (cposl: the CSR entry's CSC position), so a row reads on average half of its
 // incidences; the other triangle is the transpose of these lists (build_expansion).
-__global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__restrict__ rowptr,
+#if defined(RJ_WPE_OPT) && RJ_WPE_OPT > 0  // compile the join for this many waves per SIMD (a register cap)
+#define RJ_WPE_ATTR __attribute__((amdgpu_waves_per_eu(RJ_WPE_OPT)))
+#else
+#define RJ_WPE_ATTR
+#endif
+__global__ __launch_bounds__(RJ_NT) RJ_WPE_ATTR void exp_rowjoin_kernel(const int64_t *__restrict__ rowptr,
                                                             const int32_t *__restrict__ col,
                                                             const int64_t *__restrict__ colptr,
                                                             const int32_t *__restrict__ crow, int64_t m, int64_t r0,
@@ -413,7 +420,12 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
             return;
         }
         const int64_t R1 = min(Rend, R0 + span);
-        for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
+        // the bitmap words of this pass's range only (words L < nw, owned by threads < tcnt): a short range — every
+        // lower-triangle row's first pass is [0, i) — clears, counts and enumerates only its part of the bitmap
+        const int64_t nw = (R1 - R0 + 31) >> 5;
+        const int tcnt = (int) min((int64_t) RJ_NT, (nw + RJ_WPT - 1) / RJ_WPT);
+        if (tid < tcnt)
+            for (int w = 0; w < RJ_WPT; ++w) bm[w * RJ_NT + tid] = 0u;
         if (tid == 0) nrep_s = 0;
         // a pass over part of the partner rows reads only that part of each column (rows ascend within a
         // column: two binary searches per feature), not every incidence of the row once per pass
@@ -515,7 +527,8 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
             __syncthreads();
             continue;
         }
-        for (int q = tid; q < RJ_BMW; q += RJ_NT) bm[q] = 0u;
+        if (tid < tcnt)
+            for (int w = 0; w < RJ_WPT; ++w) bm[w * RJ_NT + tid] = 0u;
         __syncthreads();
         for (int q = tid; q < nr; q += RJ_NT) {
             const int64_t j = rep[q] - R0;
@@ -523,8 +536,10 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
         }
         __syncthreads();
         int c = 0;
+        if (tid < tcnt) {
 #pragma unroll 8
-        for (int w = 0; w < RJ_WPT; ++w) c += __popc(bm[w * RJ_NT + tid]);
+            for (int w = 0; w < RJ_WPT; ++w) c += __popc(bm[w * RJ_NT + tid]);
+        }
         // exclusive block scan of c (wave scans + wave totals)
         int incl = c;
 #pragma unroll
@@ -542,7 +557,7 @@ __global__ __launch_bounds__(RJ_NT) void exp_rowjoin_kernel(const int64_t *__res
         }
         if (wr) {
             int pos = before + incl - c;
-            for (int w = 0; w < RJ_WPT; ++w) {
+            for (int w = 0; w < (tid < tcnt ? RJ_WPT : 0); ++w) {
                 uint32_t word = bm[w * RJ_NT + tid];
                 while (word) {
                     const int b = __ffs(word) - 1;
