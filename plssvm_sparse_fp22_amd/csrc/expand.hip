@@ -613,6 +613,12 @@ __global__ __launch_bounds__(256) void exp_colsplit_kernel(const int64_t *__rest
 // sequential sum of the sort join; rbf: a product recurrence without the expm1 of s_ij, in the body). The next
 // partner's row bounds are loaded one step ahead. Pads (sj < 0): j = i, H = 0. lower_nz += #(j < i, H != 0 in T).
 constexpr int RJH_NT = 256;
+// a wave-uniform 64-bit value into scalar registers
+__device__ __forceinline__ int64_t rj_uni64(int64_t v) {
+    const uint32_t lo = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) v);
+    const uint32_t hi = (uint32_t) __builtin_amdgcn_readfirstlane((int) (uint32_t) ((uint64_t) v >> 32));
+    return (int64_t) (((uint64_t) hi << 32) | lo);
+}
 constexpr int RJ_HS = 2048;  // hash slots for row i's features (<= RJ_ECAP keys)
 __device__ __forceinline__ int rj_hash(int32_t f) { return (int) (((uint32_t) f * 2654435761u) >> (32 - 11)); }
 #ifndef RJH_WPE
@@ -648,16 +654,43 @@ __global__ __launch_bounds__(RJH_NT) __attribute__((amdgpu_waves_per_eu(RJH_WPE,
     __syncthreads();
     unsigned long long lnz = 0ull;
     double rmax = 0.0;
-    const int64_t q0 = rbeg[r], q1 = rend[r];
+    // The partner bookkeeping is wave-uniform and kept in scalar registers (readfirstlane): the partner loop, the step
+    // loop and the entry addresses (scalar base + 32-bit lane offset) cost no VALU. The prefetches stay vector loads
+    // (an opaque zero offset): a scalar load would share lgkmcnt with the LDS probes and be waited for at once. A
+    // partner's row bounds are loaded one partner ahead, its index two ahead.
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const int64_t q0 = rj_uni64(rbeg[r]), q1 = rj_uni64(rend[r]);
     constexpr int NW = RJH_NT / 64;
-    int64_t q = q0 + wave;
-    int64_t jn = q < q1 ? sj[q] : -1, kbn = 0, ken = 0;
-    if (jn >= 0) kbn = rowptr[jn], ken = rowptr[jn + 1];
+    // buffer loads (always vector memory instructions) through descriptors built in scalar registers: the row's
+    // partner list from its start (offsets < 2^31 B), a partner's two row bounds as one 16-byte load
+    const __amdgpu_buffer_rsrc_t rs_sj = __builtin_amdgcn_make_buffer_rsrc((void *) (sj + q0), (short) 0, 0x7FFFFFFF, 0x00020000);
+    auto load_j = [&](int64_t qq) -> uint32_t {
+        return qq < q1 ? __builtin_amdgcn_raw_buffer_load_b32(rs_sj, 0, (int) ((qq - q0) * 4), 0) : 0xFFFFFFFFu;
+    };
+    using u32x4 = decltype(__builtin_amdgcn_raw_buffer_load_b128(rs_sj, 0, 0, 0));
+    auto load_bounds = [&](int64_t jj) -> u32x4 {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *) (rowptr + jj), (short) 0, 16, 0x00020000);
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, 0);
+    };
+    auto uni_lo = [](u32x4 v) {
+        return (int64_t) (((uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((int) v[1]) << 32) |
+                          (uint32_t) __builtin_amdgcn_readfirstlane((int) v[0]));
+    };
+    auto uni_hi = [](u32x4 v) {
+        return (int64_t) (((uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((int) v[3]) << 32) |
+                          (uint32_t) __builtin_amdgcn_readfirstlane((int) v[2]));
+    };
+    int64_t q = q0 + wv;
+    int64_t jn = (int32_t) __builtin_amdgcn_readfirstlane((int) load_j(q));
+    u32x4 bn = {};
+    if (jn >= 0) bn = load_bounds(jn);
+    uint32_t jnn = load_j(q + NW);
     for (; q < q1; q += NW) {
-        const int64_t j = jn, kb = kbn, ke = ken;
-        const int64_t qn = q + NW;  // the next partner of this wave, one step ahead
-        jn = qn < q1 ? sj[qn] : -1;
-        if (jn >= 0) kbn = rowptr[jn], ken = rowptr[jn + 1];
+        const int64_t j = jn;
+        const int64_t kb = j >= 0 ? uni_lo(bn) : 0, ke = j >= 0 ? uni_hi(bn) : 0;
+        jn = (int32_t) __builtin_amdgcn_readfirstlane((int) jnn);  // the next partner: its bounds now, the one after's index
+        if (jn >= 0) bn = load_bounds(jn);
+        jnn = load_j(q + 2 * NW);
         if (j < 0) {  // pad
             if (lane == 0) {
                 sj[q] = (int32_t) i;
@@ -671,13 +704,14 @@ __global__ __launch_bounds__(RJH_NT) __attribute__((amdgpu_waves_per_eu(RJH_WPE,
         const bool rbf = phi.rbf != 0;
         double sd = 0.0, sphi = 0.0, P = 0.0;
         for (int64_t k0 = kb; k0 < ke; k0 += 64) {
-            const int64_t k = k0 + lane;
+            const int32_t *ck = col + k0;
+            const T *vkp = val + k0;
             double a = 0.0, pa = 0.0;
             bool hit = false;
-            if (k < ke) {
+            if (lane < ke - k0) {
                 // the value is loaded with the feature (one latency per partner, not a second one after the probe)
-                const int32_t f = col[k];
-                const T vk = val[k];
+                const int32_t f = ck[lane];
+                const T vk = vkp[lane];
                 int h = rj_hash(f);
                 int32_t key;
                 while ((key = hkey[h]) >= 0 && key != f) h = (h + 1) & (RJ_HS - 1);
