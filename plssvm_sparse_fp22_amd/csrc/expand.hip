@@ -624,7 +624,25 @@ __device__ __forceinline__ int rj_hash(int32_t f) { return (int) (((uint32_t) f 
 #ifndef RJH_WPE
 #define RJH_WPE 8  // waves per SIMD the H kernel is compiled for (<= 64 VGPRs: 8 resident 256-thread workgroups per CU)
 #endif
-template <typename T>
+// rbf phi in float (exp_rowjoin_h_kernel<float, true>): expm1(2 g a), a degree-5 Taylor polynomial where |2 g a| < 2^-7
+// (truncation < 2^-35 / 720 relative), expm1f otherwise
+__device__ __forceinline__ float rj_phi32(float g2, float a) {
+    const float u = g2 * a;
+    if (fabsf(u) < 0x1p-7f) {
+        float p = 1.0f / 120.0f;
+        p = fmaf(p, u, 1.0f / 24.0f);
+        p = fmaf(p, u, 1.0f / 6.0f);
+        p = fmaf(p, u, 0.5f);
+        p = fmaf(p, u, 1.0f);
+        return p * u;
+    }
+    return expm1f(u);
+}
+// F32 (round 5; float contexts, rbf): the shared features' products, their phi and the product recurrence in float.
+// The recurrence has no cancellation (two shared features: H = E_a E_b), so H keeps float's relative accuracy, which
+// is what the float (or bfloat16) stream stores anyway; the fp64 evaluation cost twice the VALU cycles per partner of
+// this VALU-bound kernel. Poly (H = c(s) - sum c(a_f) cancels) and fp64 contexts keep fp64.
+template <typename T, bool F32 = false>
 __global__ __launch_bounds__(RJH_NT) __attribute__((amdgpu_waves_per_eu(RJH_WPE, RJH_WPE))) void exp_rowjoin_h_kernel(const int64_t *__restrict__ rowptr,
                                                                const int32_t *__restrict__ col,
                                                                const T *__restrict__ val, int64_t r0, phi_fn phi,
@@ -701,12 +719,13 @@ __global__ __launch_bounds__(RJH_NT) __attribute__((amdgpu_waves_per_eu(RJH_WPE,
         // rbf: with E_f = expm1(2 g x_if x_jf), 1 + E(s_ij) = prod_f (1 + E_f), so H = prod (1 + E_f) - 1 - sum E_f
         // accumulates over the shared features (ascending) as Q += P E_f, P += E_f + P E_f (P = prod - 1): no
         // expm1 of s_ij and no cancellation (two shared features: H = E_a E_b exactly). poly: H = c(s) - sum c(a_f).
-        const bool rbf = phi.rbf != 0;
-        double sd = 0.0, sphi = 0.0, P = 0.0;
+        using A = typename std::conditional<F32, float, double>::type;
+        const bool rbf = F32 || phi.rbf != 0;
+        A sd = 0, sphi = 0, P = 0;
         for (int64_t k0 = kb; k0 < ke; k0 += 64) {
             const int32_t *ck = col + k0;
             const T *vkp = val + k0;
-            double a = 0.0, pa = 0.0;
+            A a = 0, pa = 0;
             bool hit = false;
             if (lane < ke - k0) {
                 // the value is loaded with the feature (one latency per partner, not a second one after the probe)
@@ -716,8 +735,9 @@ __global__ __launch_bounds__(RJH_NT) __attribute__((amdgpu_waves_per_eu(RJH_WPE,
                 int32_t key;
                 while ((key = hkey[h]) >= 0 && key != f) h = (h + 1) & (RJ_HS - 1);
                 if (key == f) {
-                    a = (double) zval[hidx[h]] * (double) vk;
-                    pa = phi(a);
+                    a = (A) zval[hidx[h]] * (A) vk;
+                    if constexpr (F32) pa = rj_phi32((float) phi.g2, a);
+                    else pa = phi(a);
                     hit = true;
                 }
             }
@@ -725,9 +745,9 @@ __global__ __launch_bounds__(RJH_NT) __attribute__((amdgpu_waves_per_eu(RJH_WPE,
             while (mask) {  // wave-uniform: the shared features in ascending order
                 const int b = __ffsll((long long) mask) - 1;
                 mask &= mask - 1;
-                const double pb = __shfl(pa, b);
+                const A pb = __shfl(pa, b);
                 if (rbf) {
-                    const double t = P * pb;
+                    const A t = P * pb;
                     sphi += t;  // Q
                     P += pb + t;
                 } else {
@@ -736,8 +756,8 @@ __global__ __launch_bounds__(RJH_NT) __attribute__((amdgpu_waves_per_eu(RJH_WPE,
                 }
             }
         }
-        const double ps = rbf ? P : phi(sd);  // E(s) or c(s)
-        const T h = (T) (rbf ? sphi : ps - sphi);
+        const double ps = rbf ? (double) P : phi((double) sd);  // E(s) or c(s)
+        const T h = (T) (rbf ? sphi : (A) (ps - (double) sphi));
         // |H| relative to the pair's kernel value without the e_i e_j factor (rbf 1 + E(s), poly kappa + c(s));
         // the division only when it can raise the maximum (wave-uniform values)
         const double kv = fabs(kbase + ps), ah = fabs((double) h);
@@ -2114,13 +2134,24 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
     // count pass), cap from the setup's sample of the rank's rows (estimate_expansion_bytes); a row beyond its
     // slots: the two passes with the counts this pass took. PLSSVM_MI_EXP_RJ=twopass: count pass + write pass.
     bool have_cnt = false;  // cnt[] holds every row's exact partner count (a slot pass whose cap was too small)
-    auto h_pass = [&]() {  // H of every listed partner, then the pairs count and the H bound
-        if (R > 0) {
-            hipLaunchKernelGGL(exp_rowjoin_h_kernel<T>, dim3((unsigned) R), dim3(RJH_NT), 0, stream, csr.rowptr.get(),
-                               csr.col.get(), csr.val.get(), r0, phi, kbase, rbeg, rend, sj.get(), sv.get(), lnz.get(),
+    // the H kernel: float evaluation for rbf in a float context (exp_rowjoin_h_kernel's F32; PLSSVM_MI_EXP_H64=1: fp64)
+    static const bool h64 = [] {
+        const char *e = std::getenv("PLSSVM_MI_EXP_H64");
+        return e != nullptr && std::atoi(e) != 0;
+    }();
+    auto launch_h = [&](const int64_t *hb, const int64_t *he, int32_t *hj, T *hv) {
+        if (sizeof(T) == 4 && phi.rbf != 0 && !h64)
+            hipLaunchKernelGGL((exp_rowjoin_h_kernel<T, true>), dim3((unsigned) R), dim3(RJH_NT), 0, stream,
+                               csr.rowptr.get(), csr.col.get(), csr.val.get(), r0, phi, kbase, hb, he, hj, hv, lnz.get(),
                                lnz.get() + 1);
-            MI_LAUNCH_CHECK();
-        }
+        else
+            hipLaunchKernelGGL((exp_rowjoin_h_kernel<T, false>), dim3((unsigned) R), dim3(RJH_NT), 0, stream,
+                               csr.rowptr.get(), csr.col.get(), csr.val.get(), r0, phi, kbase, hb, he, hj, hv, lnz.get(),
+                               lnz.get() + 1);
+        MI_LAUNCH_CHECK();
+    };
+    auto h_pass = [&]() {  // H of every listed partner, then the pairs count and the H bound
+        if (R > 0) launch_h(rbeg, rend, sj.get(), sv.get());
         read_lnz();
     };
     // Lower-triangle join (round 5; one rank holding every row): each row joins only its partners j < i (half the
@@ -2170,10 +2201,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             hipLaunchKernelGGL(exp_pool_range_kernel, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream, lcnt.get(),
                                R, cap, lb.get(), le.get());
             MI_LAUNCH_CHECK();
-            hipLaunchKernelGGL(exp_rowjoin_h_kernel<T>, dim3((unsigned) R), dim3(RJH_NT), 0, stream, csr.rowptr.get(),
-                               csr.col.get(), csr.val.get(), r0, phi, kbase, lb.get(), le.get(), ls.get(), lv.get(),
-                               lnz.get(), lnz.get() + 1);
-            MI_LAUNCH_CHECK();
+            launch_h(lb.get(), le.get(), ls.get(), lv.get());
             read_lnz();  // pairs with H != 0 and the H bound: the lower pairs are every unordered pair
             pt.mark("expansion: row join, lower triangle (H)");
             // compact lower pairs, in row order (rows ascending, partners ascending)
