@@ -2135,7 +2135,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
     // slots: the two passes with the counts this pass took. PLSSVM_MI_EXP_RJ=twopass: count pass + write pass.
     bool have_cnt = false;  // cnt[] holds every row's exact partner count (a slot pass whose cap was too small)
     // the H kernel: float evaluation for rbf in a float context (exp_rowjoin_h_kernel's F32; PLSSVM_MI_EXP_H64=1: fp64)
-    static const bool h64 = [] {
+    const bool h64 = [] {
         const char *e = std::getenv("PLSSVM_MI_EXP_H64");
         return e != nullptr && std::atoi(e) != 0;
     }();
@@ -2764,10 +2764,8 @@ void engine<T>::expansion_mscale(const cg_scalars<T> *status) {
 // the launch. Sharded: the rank's rows, whose w the group then gathers as before. PLSSVM_MI_DIR_W=0: off.
 template <typename T>
 bool engine<T>::dir_w_fill(dir_w_t<T> &o) {
-    static const bool on = [] {
-        const char *e = std::getenv("PLSSVM_MI_DIR_W");
-        return e == nullptr || std::atoi(e) != 0;
-    }();
+    const char *env = std::getenv("PLSSVM_MI_DIR_W");
+    const bool on = env == nullptr || std::atoi(env) != 0;
     if (!on || !sparse_stored() || factored() || csr.otf_on || !csr.ex.on || !csr.ex.hbf16) return false;
     if (shard) {  // expansion_kp_raw's g16 over [r0, r1)
         const bool rgrp = comm != nullptr && cstream != nullptr;

@@ -722,3 +722,48 @@ def test_expansion_lower_triangle_join_bitwise(kernel, dtype, shape, monkeypatch
     assert out["1"][1:4] == out["0"][1:4]
     np.testing.assert_array_equal(out["1"][4], out["0"][4])
     np.testing.assert_array_equal(out["1"][5], out["0"][5])
+
+
+@pytest.mark.parametrize("shape", [(20000, 3000, 20), (3000, 50, 20)])
+def test_expansion_float_h_equals_fp64_h(shape, monkeypatch):
+    """Round 5: in a float context the rbf remainder H is evaluated in float (exp_rowjoin_h_kernel<float, true>: the
+    product recurrence of the shared features' expm1 has no cancellation) — against the fp64 evaluation
+    (PLSSVM_MI_EXP_H64=1): the same pairs and slots, the same H storage decision, and the overlap sums within float
+    rounding of their magnitude (2^-20 of the |x| overlap; the dense-ish 3000 x 50 @ 40 % set shares up to ~20 features
+    per pair, so H there is far from the two-feature E_a E_b)."""
+    n, d, k = shape
+    csr, _ = datagen.sparse_csr(n, d, k, seed=29, dtype=np.float32)
+    x = np.random.default_rng(5).uniform(-1, 2, n - 1).astype(np.float32)
+    out = {}
+    for h64 in ("0", "1"):
+        monkeypatch.setenv("PLSSVM_MI_EXP_H64", h64)
+        with sparse_svm(csr, "rbf", np.float32, algo="expansion") as svm:
+            svm.setup_data_on_device()
+            info = svm.info()
+            out[h64] = (info["pairs"], info["pair_slots"], info["exp_hbytes"], svm.kp_part(x, "overlap").astype(np.float64),
+                        svm.kp_part(np.abs(x), "overlap").astype(np.float64))
+    assert out["0"][:3] == out["1"][:3]
+    mag = np.abs(out["1"][4]) + 2.0 ** -10 * np.abs(out["1"][4]).max()
+    dev = np.abs(out["0"][3] - out["1"][3])
+    assert np.all(dev <= 2.0 ** -20 * mag + 2.0 ** -22 * np.abs(out["1"][3])), dev.max()
+
+
+def test_cg_direction_update_carrying_w_is_bitwise(monkeypatch):
+    """Round 5: the CG direction update forms the next K·p's w pass (w = e d, its bfloat16 copy, the S partials) in its
+    own element loop (PLSSVM_MI_DIR_W, default on) — the same grid, element order and block reduction as
+    exp_wown_kernel, so a whole learn() (a graph-captured 50-iteration block, the run-49 reset, ten iterations after
+    it) gives the same bits with and without it. (The sharded RCCL form is covered by the one-rank RCCL group tests,
+    bitwise against no group.)"""
+    csr, y = datagen.sparse_csr(6000, 1500, 12, seed=31, dtype=np.float32)
+    out = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("PLSSVM_MI_DIR_W", on)
+        with sparse_svm(csr, "rbf", np.float32, algo="expansion", y=y, cost=1e4) as svm:
+            svm.params.epsilon = 1e-30
+            svm.setup_data_on_device()
+            assert svm.info()["exp_hbytes"] == 2
+            svm.learn(imax=60)
+            out[on] = (np.asarray(svm.trace, np.float64), svm.alpha.copy(), svm.iters)
+    assert out["1"][2] == out["0"][2] == 60
+    np.testing.assert_array_equal(out["1"][0], out["0"][0])
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
