@@ -737,6 +737,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     n_pad = std::max<int64_t>(nb, 1) * KP_TILE;
     d_pad = d;
     csr = csr_data<T>{};
+    rb_cg_state = -1;  // the row-block CG pass is checked again for the new plan
     csr.val_fmt = val_fmt;
     const int64_t nnz = rowptr[m];  // rows 0..m-1
     csr.nnz = nnz;

@@ -33,6 +33,7 @@
 #include "buffer.hpp"
 #include "fp22.hpp"
 #include "kernels.hpp"
+#include "cg_common.hpp"
 
 namespace plssvm_mi {
 
@@ -834,14 +835,80 @@ struct rb_plan {
     }
 };
 
-template <typename T, bool F22>
+// The rest of a CG iteration carried by the row-block pass (round 5, one GPU, non-reset iterations): after the
+// finalize, a grid barrier, then every block sums the d.Ad partials (dot_final's order), forms alpha and updates x, r
+// of its own rows (Ad and d still in registers: no Ad round trip), a second barrier, then every block sums the r.r
+// partials, takes the stop test / beta and updates d of its rows with the sum d / sum q d partials — cg_upd_rr and
+// cg_dir_sums_kernel's arithmetic (products rounded before the adds), two launches and 20 MB of vector traffic fewer.
+// The blocks are all resident (one per CU, grid <= the CUs, checked on the host); each barrier's wait is bounded:
+// past ~0.2 s a block sets the timeout flag and leaves (the host then reports the failure instead of hanging).
+// Measured (round 5, config 3, one box, profiles/r05_rowblock_cg_ab.json): 0.156 ms per CG iteration against 0.139 ms
+// for the three launches (one-level barrier: 0.176 ms) — the two barriers cost more than the two kernel boundaries and
+// the 20 MB they save; results within the CG-trace tests' bars. Off by default (PLSSVM_MI_RB_CG=1).
+template <typename T>
+struct rb_cg_args {
+    T *xv = nullptr, *rv = nullptr, *dw = nullptr;  // x, r, d (d written by the direction update)
+    T *prr = nullptr, *psum_out = nullptr;           // r.r partials, sum d / sum q d partials (RED_BLOCKS layout)
+    cg_scalars<T> *sc = nullptr;
+    double *trace = nullptr;
+    int64_t trace_cap = 0;
+    unsigned *bar = nullptr;  // RBB_WORDS: group counters, root counter, generation, timeout flag
+};
+
+// grid barrier of nb resident blocks, two levels: blocks arrive on one of RBB_G group counters (block b on b % RBB_G,
+// each counter on its own 64-byte line), the last of a group on the root counter, the last of all bumps the
+// generation — one same-address atomic chain of 256 device-scope adds measured ~20 us per barrier, 16 + 16 far less.
+// Agent-scope release / acquire: the partials written before it are visible to every XCD after it. False when the
+// wait timed out (bar[RBB_FLAG] set).
+constexpr int RBB_G = 16, RBB_STRIDE = 16, RBB_ROOT = RBB_G * RBB_STRIDE, RBB_GEN = RBB_ROOT + RBB_STRIDE,
+              RBB_FLAG = RBB_GEN + RBB_STRIDE, RBB_WORDS = RBB_FLAG + RBB_STRIDE;
+template <typename S>
+__device__ __forceinline__ bool rb_grid_sync(unsigned *bar, unsigned nb, S *ok_s) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        const unsigned ng = nb < (unsigned) RBB_G ? nb : (unsigned) RBB_G;
+        const unsigned gi = blockIdx.x % ng, gsize = (nb - gi + ng - 1) / ng;
+        const unsigned g = __hip_atomic_load(bar + RBB_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        bool last = false;
+        if (__hip_atomic_fetch_add(bar + gi * RBB_STRIDE, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+            __hip_atomic_store(bar + gi * RBB_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_fetch_add(bar + RBB_ROOT, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
+                __hip_atomic_store(bar + RBB_ROOT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(bar + RBB_GEN, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                last = true;
+            }
+        }
+        if (!last) {
+            const uint64_t t0 = wall_clock64();  // constant rate (100 MHz on MI355X)
+            // relaxed polls (an acquire per poll invalidates the cache each time), one acquire fence after the wait
+            while (__hip_atomic_load(bar + RBB_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > 20000000ull) {
+                    ok = 0;
+                    __hip_atomic_store(bar + RBB_FLAG, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        *ok_s = S(ok);
+    }
+    __syncthreads();
+    return *ok_s != S(0);
+}
+
+template <typename T, bool F22, bool CG = false>
 __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
     const sell_chunk *__restrict__ chunks, const int32_t *__restrict__ perm, const uint16_t *__restrict__ idx,
     vals_t<T> val, const int32_t *__restrict__ bpc, int64_t P, int64_t W, int64_t RBK, const T *__restrict__ x,
     int64_t xn, int64_t nrows, const T *__restrict__ q, const T *__restrict__ d, const T *__restrict__ psum,
-    T QA_cost, T cost_inv, T *__restrict__ Ad, T *__restrict__ pdad, const cg_scalars<T> *__restrict__ status) {
+    T QA_cost, T cost_inv, T *__restrict__ Ad, T *__restrict__ pdad, const cg_scalars<T> *__restrict__ status,
+    rb_cg_args<T> cg = {}) {
     constexpr int XW = rb_width<T>(), RB = rb_rows<T>();
     constexpr int SU = sell_unroll<F22>();
+    constexpr int RPT = (RB + SELL_NT - 1) / SELL_NT;  // rows per thread (CG: kept in registers)
     __shared__ T xs[XW];
     __shared__ T racc[RB];
     T *red = racc, *bc = racc + SELL_WAVES;  // block-reduction scratch (before / after the accumulator's use)
@@ -929,7 +996,11 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
     }
     __syncthreads();
     T s1 = 0;
-    for (int t = tid; t < rows; t += SELL_NT) {
+    T avr[CG ? RPT : 1], dvr[CG ? RPT : 1], qvr[CG ? RPT : 1];
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int t = tid + u * SELL_NT;
+        if (t >= rows) break;
         const int64_t i = row0 + t;
         const T rw = racc[t], qi = q[i], di = d[i];
         T v;
@@ -938,7 +1009,11 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
             v = rw + (QA_cost - qi) * sp - sqp + cost_inv * di;
             v = T(0) + T(1) * v;
         }
-        Ad[i] = v;
+        if constexpr (CG) {
+            avr[u] = v, dvr[u] = di, qvr[u] = qi;
+        } else {
+            Ad[i] = v;
+        }
         s1 += di * v;
     }
 #pragma unroll
@@ -950,10 +1025,84 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
         T t = 0;
         for (int w2 = 0; w2 < SELL_WAVES; ++w2) t += red[w2];
         pdad[blk] = t;
+        if constexpr (CG) pdad[RED_BLOCKS + blk] = T(0);
     }
     // the consumer sums RED_BLOCKS partials: the slots past this launch's blocks are zero
     if (blk == 0)
-        for (int b = (int) gridDim.x + tid; b < RED_BLOCKS; b += SELL_NT) pdad[b] = T(0);
+        for (int b = (int) gridDim.x + tid; b < RED_BLOCKS; b += SELL_NT) {
+            pdad[b] = T(0);
+            if constexpr (CG) pdad[RED_BLOCKS + b] = T(0);
+        }
+    if constexpr (CG) {
+#pragma clang fp contract(off)  // cg_upd_rr / cg_dir_sums: products rounded before the adds
+        const unsigned nb = gridDim.x;
+        T *red2 = racc + 2 * SELL_WAVES, *bc2 = racc + 3 * SELL_WAVES, *ok_s = racc + 4 * SELL_WAVES;  // scratch
+        auto total = [&](const T *parts) {  // partials_total1: the RED_BLOCKS partials in dot_final's order
+            T a = 0;
+            for (int i2 = tid; i2 < RED_BLOCKS; i2 += SELL_NT) a += parts[i2];
+            return cgk::block_sum_all(a, red2, bc2);
+        };
+        if (!rb_grid_sync(cg.bar, nb, ok_s)) return;
+        // cg_upd_rr_kernel: alpha = delta / d.Ad; x += alpha d; r -= alpha Ad; r.r partials
+        const T dAd = total(pdad);
+        const T delta = cg.sc->delta;
+        const T alpha = delta / dAd;
+        if (blk == 0 && tid == 0) cg.sc->dAd = dAd, cg.sc->alpha = alpha, cg.sc->delta_prev = delta;
+        T rnr[RPT];
+        T srr = 0;
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+            const int t = tid + u * SELL_NT;
+            if (t >= rows) break;
+            const int64_t i = row0 + t;
+            const T xi = cg.xv[i], ri = cg.rv[i];
+            const T tx = alpha * dvr[u];
+            cg.xv[i] = xi + tx;
+            const T ua = alpha * avr[u];
+            const T rn = ri - ua;
+            cg.rv[i] = rn;
+            rnr[u] = rn;
+            srr += rn * rn;
+        }
+        {
+            const T b1 = cgk::block_sum(srr, red2);
+            if (tid == 0) cg.prr[blk] = b1, cg.prr[RED_BLOCKS + blk] = T(0);
+            if (blk == 0)
+                for (int b = (int) nb + tid; b < RED_BLOCKS; b += SELL_NT) cg.prr[b] = T(0), cg.prr[RED_BLOCKS + b] = T(0);
+        }
+        if (!rb_grid_sync(cg.bar, nb, ok_s)) return;
+        // cg_dir_sums_kernel: delta = r.r, stop test, beta; d = beta d + r; sum d / sum q d partials
+        const T rr = total(cg.prr);
+        const bool conv = rr <= cg.sc->eps2delta0;
+        const T beta = rr / delta;  // = sc->delta_prev (written by block 0 above)
+        if (blk == 0 && tid == 0) {
+            const int64_t run = cg.sc->iters;
+            cg.sc->delta = rr;
+            cg.sc->iters = run + 1;
+            if (cg.trace && run + 1 < cg.trace_cap) cg.trace[run + 1] = (double) rr;
+            if (conv) cg.sc->converged = 1;
+            else cg.sc->beta = beta;
+        }
+        if (conv) return;  // the same decision in every block
+        T sd = 0, sqd = 0;
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+            const int t = tid + u * SELL_NT;
+            if (t >= rows) break;
+            const int64_t i = row0 + t;
+            const T tb = beta * dvr[u];
+            const T dn = tb + rnr[u];
+            cg.dw[i] = dn;
+            sd += dn;
+            sqd += qvr[u] * dn;
+        }
+        const T b1 = cgk::block_sum(sd, red2);
+        __syncthreads();
+        const T b2 = cgk::block_sum(sqd, red2);
+        if (tid == 0) cg.psum_out[blk] = b1, cg.psum_out[RED_BLOCKS + blk] = b2;
+        if (blk == 0)
+            for (int b = (int) nb + tid; b < RED_BLOCKS; b += SELL_NT) cg.psum_out[b] = T(0), cg.psum_out[RED_BLOCKS + b] = T(0);
+    }
 }
 
 template <typename T>
@@ -964,7 +1113,19 @@ inline void launch_rowblock_fin(const rb_plan<T> &pl, const T *w, int64_t xn, co
     auto k = pl.val22.get() ? sell_rowblock_fin_kernel<T, true> : sell_rowblock_fin_kernel<T, false>;
     hipLaunchKernelGGL(k, dim3((unsigned) pl.nblk), dim3(SELL_NT), 0, stream, pl.chunks.get(), pl.perm.get(),
                        pl.idx16.get(), pl.vals(), pl.bpc.get(), pl.P, pl.W, pl.RBK, w, xn, pl.nrows, q, d, psum,
-                       QA_cost, cost_inv, Ad, pdad, status);
+                       QA_cost, cost_inv, Ad, pdad, status, rb_cg_args<T>{});
+    MI_LAUNCH_CHECK();
+}
+
+// the row-block pass carrying the iteration's x / r and direction updates (sell_rowblock_fin_kernel<..., true>)
+template <typename T>
+inline void launch_rowblock_cg(const rb_plan<T> &pl, const T *w, int64_t xn, const T *q, const T *d, const T *psum,
+                               T QA_cost, T cost_inv, T *pdad, const rb_cg_args<T> &cg, hipStream_t stream) {
+    if (pl.nblk <= 0) return;
+    auto k = pl.val22.get() ? sell_rowblock_fin_kernel<T, true, true> : sell_rowblock_fin_kernel<T, false, true>;
+    hipLaunchKernelGGL(k, dim3((unsigned) pl.nblk), dim3(SELL_NT), 0, stream, pl.chunks.get(), pl.perm.get(),
+                       pl.idx16.get(), pl.vals(), pl.bpc.get(), pl.P, pl.W, pl.RBK, w, xn, pl.nrows, q, d, psum,
+                       QA_cost, cost_inv, (T *) nullptr, pdad, cg.sc, cg);
     MI_LAUNCH_CHECK();
 }
 
