@@ -767,3 +767,28 @@ def test_cg_direction_update_carrying_w_is_bitwise(monkeypatch):
     assert out["1"][2] == out["0"][2] == 60
     np.testing.assert_array_equal(out["1"][0], out["0"][0])
     np.testing.assert_array_equal(out["1"][1], out["0"][1])
+
+
+def test_rowblock_cg_pass_matches_default(monkeypatch):
+    """The row-block CSR pass carrying the CG x / r and direction updates behind two grid barriers (PLSSVM_MI_RB_CG=1,
+    off by default: measured slower, spmv.hpp) against the default three launches, on the long-trace sparse linear set
+    (tests/long_trace_cases.py: the oracle reproduces itself to 1e-9 over 71 iterations): the same recurrence with the
+    r.r and sum d partials per row block, so the 61 residuals (the run-49 reset runs the default kernels in both) agree
+    to 1e-9 and the alphas after 70 iterations to 1e-9 of their largest."""
+    import long_trace_cases as lc
+
+    s = lc.load("linear_f64_sparse")
+    out = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("PLSSVM_MI_RB_CG", on)
+        p = pm.Parameter("linear", gamma=float(s["gamma"]), coef0=float(s["coef0"]), cost=s["cost"], epsilon=s["eps"],
+                         real_type=np.float64)
+        p.csr = s["csr"]
+        p.labels = s["y"]
+        with pm.CSVM(p, kp_mode="factored") as svm:
+            svm.learn(imax=lc.IMAX)
+            out[on] = (np.asarray(svm.trace, np.float64), svm.alpha.astype(np.float64), svm.iters)
+    assert out["0"][2] == out["1"][2] == lc.IMAX
+    dev = np.abs(out["1"][0][:61] / out["0"][0][:61] - 1)
+    assert np.all(dev <= 1e-9), dev.max()
+    assert np.abs(out["1"][1] - out["0"][1]).max() <= 1e-9 * np.abs(out["0"][1]).max()
