@@ -624,8 +624,7 @@ void engine<T>::cg_iter(int reset) {
 
 // the row-block CG pass needs every workgroup resident at once (grid barriers): one per CU with the whole LDS, so
 // the plan's blocks must not exceed the CUs (a partitioned device reports fewer). Off by default (PLSSVM_MI_RB_CG=1:
-// on): measured slower than the three launches it replaces (profiles/r05_rowblock_cg_ab.json) — each grid barrier's
-// device-scope atomics and L2 write-back / invalidate cost more than a kernel boundary.
+// on): measured no faster than the three launches it replaces (profiles/r05_rowblock_cg_ab.json).
 template <typename T>
 bool engine<T>::rowblock_cg_usable() {
     if (rb_cg_state < 0) {

@@ -842,9 +842,9 @@ struct rb_plan {
 // cg_dir_sums_kernel's arithmetic (products rounded before the adds), two launches and 20 MB of vector traffic fewer.
 // The blocks are all resident (one per CU, grid <= the CUs, checked on the host); each barrier's wait is bounded:
 // past ~0.2 s a block sets the timeout flag and leaves (the host then reports the failure instead of hanging).
-// Measured (round 5, config 3, one box, profiles/r05_rowblock_cg_ab.json): 0.156 ms per CG iteration against 0.139 ms
-// for the three launches (one-level barrier: 0.176 ms) — the two barriers cost more than the two kernel boundaries and
-// the 20 MB they save; results within the CG-trace tests' bars. Off by default (PLSSVM_MI_RB_CG=1).
+// Measured (round 5, config 3, one box, profiles/r05_rowblock_cg_ab.json): with this light barrier 0.139 ms per CG
+// iteration, equal to the three launches (fenced two-level barrier 0.156 ms, one-level 0.176 ms) — the 20 MB saved pay
+// for the two barriers and no more; results within the CG-trace tests' bars. Off by default (PLSSVM_MI_RB_CG=1).
 template <typename T>
 struct rb_cg_args {
     T *xv = nullptr, *rv = nullptr, *dw = nullptr;  // x, r, d (d written by the direction update)
@@ -858,31 +858,47 @@ struct rb_cg_args {
 // grid barrier of nb resident blocks, two levels: blocks arrive on one of RBB_G group counters (block b on b % RBB_G,
 // each counter on its own 64-byte line), the last of a group on the root counter, the last of all bumps the
 // generation — one same-address atomic chain of 256 device-scope adds measured ~20 us per barrier, 16 + 16 far less.
-// Agent-scope release / acquire: the partials written before it are visible to every XCD after it. False when the
-// wait timed out (bar[RBB_FLAG] set).
+// False when the wait timed out (bar[RBB_FLAG] set).
 constexpr int RBB_G = 16, RBB_STRIDE = 16, RBB_ROOT = RBB_G * RBB_STRIDE, RBB_GEN = RBB_ROOT + RBB_STRIDE,
               RBB_FLAG = RBB_GEN + RBB_STRIDE, RBB_WORDS = RBB_FLAG + RBB_STRIDE;
+// Light form (no L2 write-back / invalidate): everything one block hands to another inside the kernel — the d.Ad and
+// r.r partials — is written and read with agent-scope atomic stores / loads (sc1: at the coherence point, past every
+// XCD's L2), every wave waits for its stores before the barrier, and the counters are agent-scope atomics; the
+// vectors each block reads and writes are its own rows (kernel boundaries order them for the next launch).
+template <typename T>
+__device__ __forceinline__ void rb_st(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T rb_ld(const T *p) {
+    return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <typename S>
 __device__ __forceinline__ bool rb_grid_sync(unsigned *bar, unsigned nb, S *ok_s) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's partial stores have reached the coherence point
     __syncthreads();
     if (threadIdx.x == 0) {
         int ok = 1;
         const unsigned ng = nb < (unsigned) RBB_G ? nb : (unsigned) RBB_G;
         const unsigned gi = blockIdx.x % ng, gsize = (nb - gi + ng - 1) / ng;
         const unsigned g = __hip_atomic_load(bar + RBB_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
         bool last = false;
-        if (__hip_atomic_fetch_add(bar + gi * RBB_STRIDE, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+        if (__hip_atomic_fetch_add(bar + gi * RBB_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
             __hip_atomic_store(bar + gi * RBB_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__hip_atomic_fetch_add(bar + RBB_ROOT, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __builtin_amdgcn_s_waitcnt(0);
+            if (__hip_atomic_fetch_add(bar + RBB_ROOT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
                 __hip_atomic_store(bar + RBB_ROOT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_fetch_add(bar + RBB_GEN, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                __builtin_amdgcn_s_waitcnt(0);  // the counters are reset before anyone can arrive again
+                __hip_atomic_fetch_add(bar + RBB_GEN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 last = true;
             }
         }
         if (!last) {
             const uint64_t t0 = wall_clock64();  // constant rate (100 MHz on MI355X)
-            // relaxed polls (an acquire per poll invalidates the cache each time), one acquire fence after the wait
             while (__hip_atomic_load(bar + RBB_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
                 __builtin_amdgcn_s_sleep(1);
                 if (wall_clock64() - t0 > 20000000ull) {
@@ -892,7 +908,7 @@ __device__ __forceinline__ bool rb_grid_sync(unsigned *bar, unsigned nb, S *ok_s
                 }
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
         *ok_s = S(ok);
     }
     __syncthreads();
@@ -1024,14 +1040,22 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
     if (tid == 0) {
         T t = 0;
         for (int w2 = 0; w2 < SELL_WAVES; ++w2) t += red[w2];
-        pdad[blk] = t;
-        if constexpr (CG) pdad[RED_BLOCKS + blk] = T(0);
+        if constexpr (CG) {
+            rb_st(pdad + blk, t);
+            pdad[RED_BLOCKS + blk] = T(0);
+        } else {
+            pdad[blk] = t;
+        }
     }
     // the consumer sums RED_BLOCKS partials: the slots past this launch's blocks are zero
     if (blk == 0)
         for (int b = (int) gridDim.x + tid; b < RED_BLOCKS; b += SELL_NT) {
-            pdad[b] = T(0);
-            if constexpr (CG) pdad[RED_BLOCKS + b] = T(0);
+            if constexpr (CG) {
+                rb_st(pdad + b, T(0));
+                pdad[RED_BLOCKS + b] = T(0);
+            } else {
+                pdad[b] = T(0);
+            }
         }
     if constexpr (CG) {
 #pragma clang fp contract(off)  // cg_upd_rr / cg_dir_sums: products rounded before the adds
@@ -1039,7 +1063,7 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
         T *red2 = racc + 2 * SELL_WAVES, *bc2 = racc + 3 * SELL_WAVES, *ok_s = racc + 4 * SELL_WAVES;  // scratch
         auto total = [&](const T *parts) {  // partials_total1: the RED_BLOCKS partials in dot_final's order
             T a = 0;
-            for (int i2 = tid; i2 < RED_BLOCKS; i2 += SELL_NT) a += parts[i2];
+            for (int i2 = tid; i2 < RED_BLOCKS; i2 += SELL_NT) a += rb_ld(parts + i2);
             return cgk::block_sum_all(a, red2, bc2);
         };
         if (!rb_grid_sync(cg.bar, nb, ok_s)) return;
@@ -1066,9 +1090,9 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
         }
         {
             const T b1 = cgk::block_sum(srr, red2);
-            if (tid == 0) cg.prr[blk] = b1, cg.prr[RED_BLOCKS + blk] = T(0);
+            if (tid == 0) rb_st(cg.prr + blk, b1), cg.prr[RED_BLOCKS + blk] = T(0);
             if (blk == 0)
-                for (int b = (int) nb + tid; b < RED_BLOCKS; b += SELL_NT) cg.prr[b] = T(0), cg.prr[RED_BLOCKS + b] = T(0);
+                for (int b = (int) nb + tid; b < RED_BLOCKS; b += SELL_NT) rb_st(cg.prr + b, T(0)), cg.prr[RED_BLOCKS + b] = T(0);
         }
         if (!rb_grid_sync(cg.bar, nb, ok_s)) return;
         // cg_dir_sums_kernel: delta = r.r, stop test, beta; d = beta d + r; sum d / sum q d partials
