@@ -30,6 +30,7 @@ inline ncclDataType_t nccl_type() {
     } while (0)
 
 int exp_dot2_built();  // expand.hip: 1 if the bfloat16 remainder's dot-instruction kernel was compiled (EXP_DOT2)
+void exp_load_code_object();  // expand.hip: its code object loaded (one kernel's attributes queried)
 void partition_superblocks(int64_t nb, int rank, int world, int64_t &s0, int64_t &s1, int64_t &s_total,
                            int64_t &tiles_total, int64_t &tiles_local);
 

@@ -3295,6 +3295,11 @@ bool engine<T>::expansion_predict(const T *alpha_dev, T alpha_m, T bias, const i
 
 int exp_dot2_built() { return EXP_DOT2 ? 1 : 0; }
 
+void exp_load_code_object() {
+    hipFuncAttributes a;
+    (void) hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&exp_rowjoin_kernel));
+}
+
 #define INST(T)                                                                              \
     template bool engine<T>::expansion_eligible();                                           \
     template void engine<T>::build_expansion(const int64_t *, int64_t, const std::function<std::exception_ptr()> &);                      \

@@ -724,6 +724,31 @@ template <typename T>
 void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void *val, int val_fmt, int64_t n_,
                           int64_t d_) {
     phase_timer pt;
+    // HIP loads expand.hip's code object (11 MB of device code) at the first launch of one of its kernels, ~0.1 s into
+    // the expansion's build on the critical path of a process's first sparse setup: a host thread loads it now, beside
+    // the CSR check, the uploads and the CSC sort (sparse.hip kernels), and is joined before the expansion
+    // (PLSSVM_MI_EXP_PRELOAD=0: off)
+    struct loader_t {
+        std::thread t;
+        void join() {
+            if (t.joinable()) t.join();
+        }
+        ~loader_t() { join(); }
+    } exp_loader;
+    {
+        static bool loaded = false;  // once per process
+        const char *pe = std::getenv("PLSSVM_MI_EXP_PRELOAD");
+        if (!loaded && !(pe != nullptr && std::atoi(pe) == 0) && n_ > 1 && rowptr[n_ - 1] > 0) {
+            loaded = true;
+            try {
+                const int dev = device;
+                exp_loader.t = std::thread([dev] {
+                    if (hipSetDevice(dev) == hipSuccess) exp_load_code_object();
+                });
+            } catch (...) {  // no thread: the kernels load at their first launch
+            }
+        }
+    }
     host_check_csr<T>(rowptr, col, n_, d_);
     if (!val && rowptr[n_] > 0) throw mi_error(-1, "CSR values missing");
     if (val_fmt != PLSSVM_MI_VAL_REAL && val_fmt != PLSSVM_MI_VAL_FP22) throw mi_error(-1, "unknown value format");
