@@ -138,6 +138,15 @@ typedef int (*plssvm_mi_exchange_fn)(void *buf, int64_t count, int real_bytes, i
 PLSSVM_MI_API int plssvm_mi_comm_init_host(plssvm_mi_ctx *ctx, int rank, int world_size, plssvm_mi_exchange_fn fn,
                                            void *user);
 
+/* Group failure protocol of a one-process multi-GPU group (one host thread per context, e.g. the csvm<T> adapter
+ * over every visible GPU, include/plssvm_mi355x_group.hpp): when one rank's call fails, the caller aborts every
+ * context of the group from its own thread — an RCCL communicator is released with ncclCommAbort, so a rank waiting
+ * in a collective returns — and every call of an aborted context (also the one in progress) fails with
+ * PLSSVM_MI_ERR_RCCL. The reference ends its device threads the same way: a backend_exception on any device ends the
+ * OpenMP region (src/plssvm/backends/gpu_csvm.cpp:366-386). May be called from any thread, concurrently with a call
+ * on the same context; the context can then only be destroyed. */
+PLSSVM_MI_API int plssvm_mi_comm_abort(plssvm_mi_ctx *ctx);
+
 /* Host-only (no GPU needed): the work split of the implicit matrix for m = n - 1 rows.
  * out4 = { first super-block, end super-block, total tiles, tiles owned by `rank` } where a tile
  * is 128x128 of the lower triangle and a super-block 8x8 tiles (linear index I(I+1)/2 + J). */
@@ -179,9 +188,14 @@ PLSSVM_MI_API int plssvm_mi_kp(plssvm_mi_ctx *ctx, const void *q, const void *p,
  *   PLSSVM_MI_PART_OVERLAP : sparse poly/rbf only — sum over j != i sharing a feature with i of
  *                            (k_ij - kappa_ij) p_j, kappa_ij the value non-overlapping pairs take
  *                            (e_i e_j for rbf, coef0^degree for poly): exactly the per-pair work of the
- *                            sparse K·p kernels, without the separable and diagonal terms. */
+ *                            sparse K·p kernels, without the separable and diagonal terms;
+ *   PLSSVM_MI_PART_REMAINDER: the sparse kernel expansion only — its stored remainder stream alone,
+ *                            sum over j != i sharing >= 2 features of a_i a_j H_ij p_j (H_ij = phi(s_ij) -
+ *                            sum_f phi(x_if x_jf); a = e for rbf, 1 for poly) in the stored layout (bfloat16 H
+ *                            and windows where the setup chose them), without the column-moment terms. */
 #define PLSSVM_MI_PART_KERNEL 0
 #define PLSSVM_MI_PART_OVERLAP 1
+#define PLSSVM_MI_PART_REMAINDER 2
 PLSSVM_MI_API int plssvm_mi_kp_part(plssvm_mi_ctx *ctx, const void *p, void *out, int part);
 
 /* gpu_csvm::solver_CG (src/plssvm/backends/gpu_csvm.cpp:186-324) with the OpenMP backend's

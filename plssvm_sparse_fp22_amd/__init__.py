@@ -294,10 +294,11 @@ class CSVM:
 
     def kp_part(self, p, part="kernel"):
         """Test hook (plssvm_mi_kp_part): 'kernel' = sum_j k(x_i, x_j) p_j; 'overlap' = the sparse
-        poly/rbf overlap sum (the per-pair work of the sparse kernels only)."""
+        poly/rbf overlap sum (the per-pair work of the sparse kernels only); 'remainder' = the kernel
+        expansion's stored remainder stream alone (pairs sharing >= 2 features, in the stored layout)."""
         pp = np.ascontiguousarray(p, dtype=self.dtype)
         out = np.zeros(max(self.m, 1), dtype=self.dtype)
-        code = {"kernel": _abi.PART_KERNEL, "overlap": _abi.PART_OVERLAP}[part]
+        code = {"kernel": _abi.PART_KERNEL, "overlap": _abi.PART_OVERLAP, "remainder": _abi.PART_REMAINDER}[part]
         self._check(_abi.lib().plssvm_mi_kp_part(self._ctx, _ptr(pp), _ptr(out), code))
         return out[: self.m]
 

@@ -31,13 +31,13 @@ EXPORTS = (
     "plssvm_mi_solve_cg", "plssvm_mi_cg_begin", "plssvm_mi_cg_step", "plssvm_mi_cg_result", "plssvm_mi_learn",
     "plssvm_mi_time_kp", "plssvm_mi_get_info", "plssvm_mi_partition",
     "plssvm_mi_update_w", "plssvm_mi_predict_dense", "plssvm_mi_predict_csr", "plssvm_mi_setup_coo",
-    "plssvm_mi_comm_init_host", "plssvm_mi_kp_part", "plssvm_mi_set_progress",
+    "plssvm_mi_comm_init_host", "plssvm_mi_kp_part", "plssvm_mi_set_progress", "plssvm_mi_comm_abort",
 )
 OPT_SIM_RANK = 2
 OPT_RBF_FORM = 3
 OPT_SPARSE_ALGO = 4
 SPARSE_AUTO, SPARSE_PATTERN, SPARSE_EXPANSION, SPARSE_DENSE, SPARSE_ONTHEFLY = 0, 1, 2, 3, 4
-PART_KERNEL, PART_OVERLAP = 0, 1
+PART_KERNEL, PART_OVERLAP, PART_REMAINDER = 0, 1, 2
 XCHG_ALLREDUCE, XCHG_ALLGATHER = 0, 1
 # int fn(void *buf, int64_t count, int real_bytes, int op, void *user)   (plssvm_mi_exchange_fn)
 EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
@@ -113,6 +113,7 @@ def _declare(L):
         "plssvm_mi_partition": ([I64, I, I, PI64], I),
         "plssvm_mi_comm_init_host": ([P, I, I, EXCHANGE_FN, P], I),
         "plssvm_mi_kp_part": ([P, P, P, I], I),
+        "plssvm_mi_comm_abort": ([P], I),
         "plssvm_mi_set_progress": ([P, PROGRESS_FN, P], I),
     }
     for name, (args, res) in sig.items():

@@ -25,6 +25,10 @@ struct plssvm_mi_ctx {
             } else {
                 f(*static_cast<engine<double> *>(eng.get()));
             }
+            if (eng->comm_aborted) {  // the group was aborted while (or before) this call ran: its results are void
+                err = "the group was aborted by another rank";
+                return PLSSVM_MI_ERR_RCCL;
+            }
             err.clear();
             return PLSSVM_MI_OK;
         } catch (const mi_error &e) {
@@ -154,6 +158,12 @@ int plssvm_mi_get_unique_id(void *id_out) {
 int plssvm_mi_comm_init(plssvm_mi_ctx *ctx, int rank, int world_size, const void *unique_id) {
     if (!ctx || (world_size > 1 && !unique_id)) return PLSSVM_MI_ERR_ARG;
     return ctx->call([&](auto &e) { e.comm_init(rank, world_size, unique_id); });
+}
+
+int plssvm_mi_comm_abort(plssvm_mi_ctx *ctx) {
+    if (!ctx) return PLSSVM_MI_ERR_ARG;
+    ctx->eng->comm_abort();  // no ctx->call: this runs beside the context's own thread, which may be inside a call
+    return PLSSVM_MI_OK;
 }
 
 int plssvm_mi_comm_init_host(plssvm_mi_ctx *ctx, int rank, int world_size, plssvm_mi_exchange_fn fn, void *user) {

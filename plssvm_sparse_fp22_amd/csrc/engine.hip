@@ -144,10 +144,30 @@ void engine<T>::comm_init(int rank_, int world_, const void *uid) {
     }
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
-    MI_NCCL_CHECK(ncclCommInitRank(&comm, world, id, rank));
+    comm_aborted = false;
+    {
+        ncclComm_t c = nullptr;
+        const ncclResult_t rc = ncclCommInitRank(&c, world, id, rank);  // blocks until every rank joined
+        if (rc != ncclSuccess)
+            throw mi_error(-3, std::string("RCCL error '") + ncclGetErrorString(rc) + "' (ncclCommInitRank)");
+        std::lock_guard<std::mutex> lk(comm_mu);
+        comm = c;
+    }
     if (cstream == nullptr) {
         MI_HIP_CHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
         for (auto &e : cev) MI_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+}
+
+// called from another host thread while this engine's own thread may be inside a collective: ncclCommAbort makes the
+// pending RCCL kernels return; the engine's later RCCL calls throw (MI_NCCL_CHECK), its destructor skips the destroy
+template <typename T>
+void engine<T>::comm_abort() {
+    std::lock_guard<std::mutex> lk(comm_mu);
+    comm_aborted = true;
+    if (comm != nullptr) {
+        (void) ncclCommAbort(comm);
+        comm = nullptr;
     }
 }
 
@@ -162,6 +182,7 @@ void engine<T>::comm_init_host(int rank_, int world_, int (*fn)(void *, int64_t,
         (void) ncclCommDestroy(comm);
         comm = nullptr;
     }
+    comm_aborted = false;
     rank = rank_;
     world = world_;
     xchg = fn;
@@ -492,20 +513,30 @@ void engine<T>::kp_host(const T *q_host, const T *p, T *ret_host, T add) {
 }
 
 // test hook: one part of Q~p (PLSSVM_MI_PART_KERNEL: sum_j k_ij p_j; PLSSVM_MI_PART_OVERLAP: the
-// sparse overlap sum only), after the group exchange
+// sparse overlap sum only; PLSSVM_MI_PART_REMAINDER: the kernel expansion's stored remainder stream only), after the
+// group exchange
 template <typename T>
 void engine<T>::kp_part(const T *p_host, T *out_host, int part) {
     need_data();
-    if (part != 0 && part != 1) throw mi_error(-1, "unknown K·p part");
+    if (part < 0 || part > 2) throw mi_error(-1, "unknown K·p part");
     if (part == 1 && !(sparse_stored() && !factored()))
         throw mi_error(-5, "the overlap part exists for the stored sparse poly/rbf paths only");
+    if (part == 2 && !(sparse_stored() && !factored() && csr.ex.on && !csr.otf_on))
+        throw mi_error(-5, "the remainder part exists for the sparse kernel expansion only");
     MI_HIP_CHECK(hipSetDevice(device));
     cg_active = false;
     MI_HIP_CHECK(hipMemsetAsync(sc.get(), 0, sizeof(cg_scalars<T>), stream));
     if (m > 0) {
         MI_HIP_CHECK(hipMemcpyAsync(pv.get(), p_host, sizeof(T) * (size_t) m, hipMemcpyHostToDevice, stream));
-        if (part == 1) sparse_kp_raw(pv.get(), nullptr, false);
-        else kp_raw(pv.get(), nullptr);
+        part_mode = part;
+        try {
+            if (part != 0) sparse_kp_raw(pv.get(), nullptr, false);
+            else kp_raw(pv.get(), nullptr);
+        } catch (...) {
+            part_mode = 0;
+            throw;
+        }
+        part_mode = 0;
         if (gathered) allgather_rows(raw.get());
         MI_HIP_CHECK(hipMemcpyAsync(out_host, raw.get(), sizeof(T) * (size_t) m, hipMemcpyDeviceToHost, stream));
     }

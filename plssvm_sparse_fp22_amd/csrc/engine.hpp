@@ -5,8 +5,10 @@
 #include <rccl/rccl.h>
 #include <rocblas/rocblas.h>
 
+#include <atomic>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -21,9 +23,15 @@ inline ncclDataType_t nccl_type() {
     return sizeof(T) == 8 ? ncclFloat64 : ncclFloat32;
 }
 
+// an RCCL call of an engine member: under comm_mu, refused once plssvm_mi_comm_abort has released the communicator
 #define MI_NCCL_CHECK(expr)                                                                                          \
     do {                                                                                                             \
-        ncclResult_t r_ = (expr);                                                                                    \
+        ncclResult_t r_;                                                                                             \
+        {                                                                                                            \
+            std::lock_guard<std::mutex> lk_(this->comm_mu);                                                         \
+            if (this->comm_aborted) throw ::plssvm_mi::mi_error(-3, "the group was aborted by another rank");      \
+            r_ = (expr);                                                                                             \
+        }                                                                                                            \
         if (r_ != ncclSuccess) {                                                                                     \
             throw ::plssvm_mi::mi_error(-3, std::string("RCCL error '") + ncclGetErrorString(r_) + "' (" #expr ")"); \
         }                                                                                                            \
@@ -36,6 +44,12 @@ void partition_superblocks(int64_t nb, int rank, int world, int64_t &s0, int64_t
 
 struct engine_base {
     virtual ~engine_base() = default;
+    // plssvm_mi_comm_abort (another thread of a one-process multi-GPU group, after a peer failed): the communicator
+    // is aborted (ncclCommAbort releases a rank waiting in a collective) and every later RCCL call of the engine
+    // fails (MI_NCCL_CHECK); the C ABI reports any call that ran into the abort as failed
+    std::mutex comm_mu;
+    std::atomic<bool> comm_aborted{ false };
+    virtual void comm_abort() = 0;
 };
 
 template <typename T>
@@ -52,6 +66,7 @@ struct engine : engine_base {
     // ---- multi-GPU row-block group ----
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
+    void comm_abort() override;
     // host-staged exchange (plssvm_mi_comm_init_host): the reference's device_reduction transport
     int (*xchg)(void *, int64_t, int, int, void *) = nullptr;
     void *xchg_user = nullptr;
@@ -169,6 +184,7 @@ struct engine : engine_base {
     void comm_init(int rank_, int world_, const void *uid);
     void comm_init_host(int rank_, int world_, int (*fn)(void *, int64_t, int, int, void *), void *user);
     void kp_part(const T *p_host, T *out_host, int part);  // test hook, PLSSVM_MI_PART_*
+    int part_mode = 0;  // kp_part in progress: PLSSVM_MI_PART_* (the expansion's combine writes that part)
     void setup_dense(const T *X, int64_t n_, int64_t d_);
     void setup_csr(const int64_t *rowptr, const int32_t *col, const void *val, int val_fmt, int64_t n_, int64_t d_);
     void finish_setup();

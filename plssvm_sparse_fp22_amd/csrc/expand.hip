@@ -1238,7 +1238,8 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
                                                                  int64_t m, int64_t r0, int64_t R, int64_t nW,
                                                                  int64_t RB, int64_t nI, int G, T *__restrict__ hs,
                                                                  T *__restrict__ hslab,
-                                                                 const cg_scalars<T> *__restrict__ status) {
+                                                                 const cg_scalars<T> *__restrict__ status, int wdrop = 0) {
+    // wdrop = 1: test-only ablation (PLSSVM_MI_EXP_ABLATE bit 2), the last window of every row block is skipped
     // RB (rows per block, a multiple of 16) <= RBC, the accumulator's capacity. G > 1 window groups:
     // block (I, g) streams only windows [g nW / G, (g + 1) nW / G) of its rows and writes its row sums
     // to hslab[g][rows] (summed in g order by exp_combine_kernel); the blocks of one XCD share g,
@@ -1255,7 +1256,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     if (status != nullptr && status->converged) return;
     const int64_t bx = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t I = bx % nI, g = bx / nI;
-    const int64_t W0 = g * nW / G, W1 = (g + 1) * nW / G;
+    const int64_t W0 = g * nW / G, W1 = (g + 1) * nW / G - (wdrop && g == G - 1 && nW > 0 ? 1 : 0);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the wave's offsets are scalar loads
     for (int t = tid; t < RB; t += NT) racc[t] = T(0);
@@ -1689,7 +1690,9 @@ __device__ __forceinline__ T exp_combine_row(const T *__restrict__ e, const T *_
     const double t = (double) J + (double) hdiag[i] * wi + (double) h;
     const double sc = e != nullptr ? (double) e[i] : 1.0;
     double v;
-    if (overlap_only) {
+    if (overlap_only == 2) {  // PLSSVM_MI_PART_REMAINDER: the remainder stream's row sum alone
+        v = sc * (double) h;
+    } else if (overlap_only) {
         v = sc * (t - (double) phin[i] * wi);
     } else {
         const double base =
@@ -2637,7 +2640,8 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
 }
 
 // timing/test-only ablations (results are wrong when non-zero): PLSSVM_MI_EXP_ABLATE bit 0 = drop the
-// stored remainder H of the multi-feature pairs, bit 1 = keep only the first term of phi's polynomial
+// stored remainder H of the multi-feature pairs, bit 1 = keep only the first term of phi's polynomial, bit 2 =
+// the remainder stream skips the last partner window of every row block (chunk layouts)
 int exp_ablate() {
     static const int v = [] {
         const char *s = std::getenv("PLSSVM_MI_EXP_ABLATE");
@@ -2654,7 +2658,7 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
         auto launch = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned) (ex.nblk * ex.G)), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
                                ex.hrow.get(), ex.hjl.get(), ex.hv.get(), ex.hv16.get(), w, ex.wv16.get(), m, r0, r1 - r0, ex.nW,
-                               (int64_t) ex.RB, ex.nblk, ex.G, ex.hs.get(), ex.hslab.get(), status);
+                               (int64_t) ex.RB, ex.nblk, ex.G, ex.hs.get(), ex.hslab.get(), status, (exp_ablate() & 4) ? 1 : 0);
         };
         auto launch_run = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned) (ex.nblk * ex.G)), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
@@ -2903,7 +2907,7 @@ void engine<T>::expansion_kp_raw(const T *p, const cg_scalars<T> *status, bool w
         hipLaunchKernelGGL(exp_combine_kernel<T>, dim3((unsigned) ceil_div(ie - ib, 256)), dim3(256), 0, stream,
                            kernel == 2 ? csr.e.get() : nullptr, cb, w, ex.hdiag.get(), ex.phin.get(), ex.hs.get(),
                            ex.G > 1 ? ex.hslab.get() : nullptr, ex.G, jfuse ? pc.partial.get() : nullptr, (int) pc.P,
-                           csr.ssc.get(), kappa, ib, ie, r0, r1, with_base ? 0 : 1, raw.get(), status);
+                           csr.ssc.get(), kappa, ib, ie, r0, r1, with_base ? 0 : (part_mode == 2 ? 2 : 1), raw.get(), status);
     MI_LAUNCH_CHECK();
     if (!shard) allgather_rows(raw.get());
 }
@@ -2964,10 +2968,8 @@ T engine<T>::QAf() const {
 template <typename T>
 void engine<T>::ctr_setup() {
     ctr_ok = false;
-    static const int mode = [] {
-        const char *v = std::getenv("PLSSVM_MI_CTR");
-        return v == nullptr ? 1 : std::atoi(v);
-    }();
+    const char *cv = std::getenv("PLSSVM_MI_CTR");  // read per setup: tests compare both finalizes in one process
+    const int mode = cv == nullptr ? 1 : std::atoi(cv);
     if (mode == 0 || !sparse || csr.dense_on || !csr.ex.on || csr.otf_on || (kernel != 1 && kernel != 2) || m <= 0) return;
     double nlast = 0;
     for (int64_t k = 0; k < d; ++k) nlast = std::fma((double) xlast_h[k], (double) xlast_h[k], nlast);

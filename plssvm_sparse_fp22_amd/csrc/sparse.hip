@@ -14,6 +14,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -724,10 +725,14 @@ template <typename T>
 void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void *val, int val_fmt, int64_t n_,
                           int64_t d_) {
     phase_timer pt;
+    host_check_csr<T>(rowptr, col, n_, d_);
+    if (!val && rowptr[n_] > 0) throw mi_error(-1, "CSR values missing");
+    if (val_fmt != PLSSVM_MI_VAL_REAL && val_fmt != PLSSVM_MI_VAL_FP22) throw mi_error(-1, "unknown value format");
+    if (val_fmt == PLSSVM_MI_VAL_FP22 && sizeof(T) != 4) throw mi_error(-5, "FP22 values need a float context");
     // HIP loads expand.hip's code object (11 MB of device code) at the first launch of one of its kernels, ~0.1 s into
-    // the expansion's build on the critical path of a process's first sparse setup: a host thread loads it now, beside
-    // the CSR check, the uploads and the CSC sort (sparse.hip kernels), and is joined before the expansion
-    // (PLSSVM_MI_EXP_PRELOAD=0: off)
+    // the expansion's build on the critical path of a process's first sparse setup: for the kernels that can use the
+    // expansion (poly, rbf) a host thread loads it now, once per process, beside the uploads and the CSC sort
+    // (sparse.hip kernels); it is joined before the expansion is built (and at the latest when setup_csr returns)
     struct loader_t {
         std::thread t;
         void join() {
@@ -736,10 +741,8 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
         ~loader_t() { join(); }
     } exp_loader;
     {
-        static bool loaded = false;  // once per process
-        const char *pe = std::getenv("PLSSVM_MI_EXP_PRELOAD");
-        if (!loaded && !(pe != nullptr && std::atoi(pe) == 0) && n_ > 1 && rowptr[n_ - 1] > 0) {
-            loaded = true;
+        static std::atomic<bool> loaded{ false };
+        if ((kernel == 1 || kernel == 2) && n_ > 1 && rowptr[n_ - 1] > 0 && !loaded.exchange(true)) {
             try {
                 const int dev = device;
                 exp_loader.t = std::thread([dev] {
@@ -749,10 +752,6 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
             }
         }
     }
-    host_check_csr<T>(rowptr, col, n_, d_);
-    if (!val && rowptr[n_] > 0) throw mi_error(-1, "CSR values missing");
-    if (val_fmt != PLSSVM_MI_VAL_REAL && val_fmt != PLSSVM_MI_VAL_FP22) throw mi_error(-1, "unknown value format");
-    if (val_fmt == PLSSVM_MI_VAL_FP22 && sizeof(T) != 4) throw mi_error(-5, "FP22 values need a float context");
     MI_HIP_CHECK(hipSetDevice(device));
     sparse = true;
     n = n_;
@@ -1151,6 +1150,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                         }
                         return plan_fail ? plan_fail : plan_fail2;
                     };
+                    exp_loader.join();  // expand.hip's code object is in place before its first kernel
                     try {
                         build_expansion(cpos_d.get(), max_inc, join_plans);
                     } catch (...) {
