@@ -273,8 +273,8 @@ typedef struct {
                            bound of expand.hip "H storage", else sizeof(real)) */
     int exp_layout;     /* kernel expansion: remainder stream layout — 1 = 4-slot chunks with a stored row index per
                            chunk, 2 = 4-slot chunks whose rows are numbered by row-start flags (no row index),
-                           3 = runs (no padding), 4 = row-start flags per slot pair (cells padded to 2 slots);
-                           0 = no expansion */
+                           4 = row-start flags per slot pair (cells padded to 2 slots); 0 = no expansion
+                           (3 was round 2's run layout, removed) */
     int exp_dot2;       /* kernel expansion, bfloat16 H: 1 = the remainder's chunk products run on the v_dot2_f32_bf16
                            kernel (built with EXP_DOT2 and selected: PLSSVM_MI_EXP_DOT2 != 0), 0 = the FMA chain */
     int centered;       /* kernel expansion: 1 = the finalize forms Q~'s rank-1 terms in the centered form

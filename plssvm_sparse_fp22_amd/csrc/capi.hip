@@ -400,7 +400,7 @@ int plssvm_mi_get_info(const plssvm_mi_ctx *cctx, plssvm_mi_info *info) {
         info->exp_waves = (int) (e.csr.ex.nblk * EXP_NWV_C);
         info->exp_chunks = e.csr.ex.nchunks;
         info->exp_hbytes = e.csr.ex.on ? (e.csr.ex.hbf16 ? 2 : (int) sizeof(e.gamma)) : 0;
-        info->exp_layout = !e.csr.ex.on ? 0 : e.csr.ex.runs ? 3 : e.csr.ex.rpairs ? 4 : e.csr.ex.rflags ? 2 : 1;
+        info->exp_layout = !e.csr.ex.on ? 0 : e.csr.ex.rpairs ? 4 : e.csr.ex.rflags ? 2 : 1;
         info->exp_dot2 = e.csr.ex.on && e.csr.ex.hbf16 && e.csr.ex.dot2 && sizeof(e.gamma) == 4 && plssvm_mi::exp_dot2_built() ? 1 : 0;
         info->centered = e.ctr_active() ? 1 : 0;
         info->exp_lt = e.csr.ex.on && e.csr.ex.lt ? 1 : 0;

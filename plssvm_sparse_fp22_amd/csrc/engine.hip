@@ -88,7 +88,6 @@ engine<T>::engine(int kernel_, int degree_, double gamma_, double coef0_, double
     sc.alloc(1, stream);
     red.alloc(2 * RED_BLOCKS, stream);
     wsp.alloc(2 * RED_BLOCKS, stream);
-    rbbar.alloc(RBB_WORDS, stream);  // zeroed (a stream capture may be the first to need it: no allocation there)
     cgp.alloc(6 * RED_BLOCKS, stream);
 }
 
@@ -592,18 +591,6 @@ void engine<T>::cg_iter(int reset) {
     // sharded: the partials the previous step gathered (slot 0: sum d / sum q d)
     const T *psum_in = gathered ? cgp_g.get() : psum;
     const int raw_only = (sim_world > 0 && sim_rank != 0 && !shard) ? 1 : 0;
-    // one GPU, factored sparse linear, not a reset iteration: the CSC pass, then the row-block CSR pass carrying the
-    // finalize, the x / r update and the direction update (spmv.hpp rb_cg_args; the same arithmetic as below)
-    if (!reset && sparse_stored() && factored() && world == 1 && sim_world == 0 && csr.rb_csr.nblk > 0 &&
-        rowblock_cg_usable()) {
-        spmv_pass_csc(dv.get(), st);
-        rb_cg_args<T> a;
-        a.xv = x.get(), a.rv = r.get(), a.dw = dv.get(), a.prr = prr, a.psum_out = psum, a.sc = sc.get();
-        a.trace = trace.get(), a.trace_cap = trace_cap, a.bar = rbbar.get();
-        launch_rowblock_cg<T>(csr.rb_csr, w.get(), d, q.get(), dv.get(), psum, QA_cost, cost_inv(), pdad, a, stream);
-        rb_cg_used = true;
-        return;
-    }
     // Ad = Q~ d (:111-113); alpha = delta / (d . Ad) (:116) in the next kernel
     const T *slabs = nullptr;
     int64_t P = 0;
@@ -651,28 +638,6 @@ void engine<T>::cg_iter(int reset) {
     w_pre = fw ? dv.get() : nullptr;
     if (gathered && comm != nullptr) psum_pending = true;  // gathered with the next K·p's first collective
     else gather_partials(psum, 0);
-}
-
-// the row-block CG pass needs every workgroup resident at once (grid barriers): one per CU with the whole LDS, so
-// the plan's blocks must not exceed the CUs (a partitioned device reports fewer). Off by default (PLSSVM_MI_RB_CG=1:
-// on): measured no faster than the three launches it replaces (profiles/r05_rowblock_cg_ab.json).
-template <typename T>
-bool engine<T>::rowblock_cg_usable() {
-    if (rb_cg_state < 0) {
-        rb_cg_state = 0;
-        const char *e = std::getenv("PLSSVM_MI_RB_CG");
-        if (e != nullptr && std::atoi(e) != 0) {
-            hipDeviceProp_t prop;
-            int per = 0;
-            const bool f22 = csr.rb_csr.val22.get() != nullptr;
-            const hipError_t oc = f22 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sell_rowblock_fin_kernel<T, true, true>, SELL_NT, 0)
-                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, sell_rowblock_fin_kernel<T, false, true>, SELL_NT, 0);
-            if (hipGetDeviceProperties(&prop, device) == hipSuccess && oc == hipSuccess && per >= 1 &&
-                csr.rb_csr.nblk <= (int64_t) prop.multiProcessorCount * per)
-                rb_cg_state = 1;
-        }
-    }
-    return rb_cg_state == 1;
 }
 
 // Iteration blocks of CG_RESET (the reset period) starting at a multiple of it are replayed from one
@@ -749,17 +714,7 @@ void engine<T>::cg_step(int64_t nsteps, bool &converged, int64_t &iters) {
     }
     cg_scalars<T> h{};
     MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));
-    unsigned bar_h = 0u;
-    if (rb_cg_used) MI_HIP_CHECK(hipMemcpyAsync(&bar_h, rbbar.get() + RBB_FLAG, sizeof(bar_h), hipMemcpyDeviceToHost, stream));
     MI_HIP_CHECK(hipStreamSynchronize(stream));
-    if (bar_h != 0u) {  // a grid barrier of the row-block CG pass timed out: never again on this engine
-        rb_cg_state = 0;
-        rb_cg_used = false;
-        MI_HIP_CHECK(hipMemsetAsync(rbbar.get(), 0, sizeof(unsigned) * RBB_WORDS, stream));
-        MI_HIP_CHECK(hipStreamSynchronize(stream));
-        throw mi_error(-2, "the row-block CG pass's grid barrier timed out (not all of its workgroups were resident); "
-                           "the pass is disabled for this context, solve again");
-    }
     polled = h;
     converged = h.converged != 0;
     iters = h.iters;

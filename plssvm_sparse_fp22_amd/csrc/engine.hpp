@@ -121,12 +121,6 @@ struct engine : engine_base {
     // (set after a carrying direction update of dv, cleared by any other w pass), graph_w_end = w_pre after a
     // captured iteration block
     dev_buf<T> wsp;
-    // one GPU, factored sparse linear: the row-block pass carrying the x / r and direction updates (spmv.hpp
-    // rb_cg_args); rbbar = its grid barrier [count, generation, timeout flag]; rb_cg_ok: co-residency checked
-    dev_buf<unsigned> rbbar;
-    int rb_cg_state = -1;  // -1 unchecked, 0 off, 1 on
-    bool rb_cg_used = false;
-    bool rowblock_cg_usable();
     const T *w_pre = nullptr, *graph_w_end = nullptr;
     bool dir_w_fill(dir_w_t<T> &o);
     dev_buf<T> cgp;  // fused CG partials: [0, 2R) sum d / sum q d, [2R, 4R) d.Ad, [4R, 6R) r.r

@@ -42,9 +42,6 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 // rbf with |u| = |2 g a| < 2^-7 (every pair of the BASELINE sets: u <= 2 g max x^2 ~ 1e-4): the Taylor
 // polynomial of degree 7, whose remainder u^8 / 8! is below 2^-54 |u| there — fp64 accuracy in 8 fma instead of
 // the library expm1's range reduction (the setup's remainder kernels evaluate phi once per wave step)
-#ifndef PLSSVM_MI_PHI_POLY
-#define PLSSVM_MI_PHI_POLY 1
-#endif
 struct phi_fn {
     int rbf = 0, deg = 0;
     double g2 = 0.0;                   // rbf: 2 g
@@ -52,7 +49,7 @@ struct phi_fn {
     __host__ __device__ double operator()(double a) const {
         if (rbf) {
             const double u = g2 * a;
-            if (PLSSVM_MI_PHI_POLY && fabs(u) < 0x1p-7) {
+            if (fabs(u) < 0x1p-7) {
                 double p = 1.0 / 5040.0;
                 p = fma(p, u, 1.0 / 720.0);
                 p = fma(p, u, 1.0 / 120.0);
@@ -1098,75 +1095,6 @@ __global__ __launch_bounds__(256) void exp_cell_scatter_flag_kernel(const int64_
     dummies(last + 1, nW);
 }
 
-// ---- run layout (option, PLSSVM_MI_EXP_RUNS): no padding, no per-chunk row index --------------------
-// Per (row, window) exactly max(count, 1) entries: the first entry of every row carries bit 15 of its
-// window-local j (so CW <= 32768), a row without partners in the window gets one flagged dummy (j = 0,
-// H = 0). A wave's stream of a window then lists its RPW rows in order and the row of an entry is the
-// number of flags up to it: neither the 4-slot padding nor the chunk rows of the chunk layout are stored.
-template <typename T>
-__global__ __launch_bounds__(256) void exp_run_count_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
-                                                            const int32_t *__restrict__ sj, const T *__restrict__ sv,
-                                                            int64_t R, int64_t nW, int64_t CW, int64_t RB,
-                                                            int64_t *__restrict__ cnt,
-                                                            unsigned long long *__restrict__ dummies) {
-    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= R) return;
-    for (int64_t W = 0; W < nW; ++W) cnt[exp_cidx(r, W, nW, RB)] = 1;  // the dummy, unless entries follow
-    int64_t Wc = -1, k = 0, filled = 0;
-    for (int64_t s = rbeg[r]; s < rend[r]; ++s) {
-        if (sv[s] == T(0)) continue;
-        const int64_t W = sj[s] / CW;
-        if (W != Wc) {
-            if (Wc >= 0) cnt[exp_cidx(r, Wc, nW, RB)] = k;
-            Wc = W;
-            k = 0;
-            ++filled;
-        }
-        ++k;
-    }
-    if (Wc >= 0) cnt[exp_cidx(r, Wc, nW, RB)] = k;
-    atomicAdd(dummies, (unsigned long long) (nW - filled));
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void exp_run_scatter_kernel(const int64_t *__restrict__ rbeg, const int64_t *__restrict__ rend,
-                                                              const int32_t *__restrict__ sj, const T *__restrict__ sv,
-                                                              int64_t R, int64_t nW, int64_t CW, int64_t RB,
-                                                              const int64_t *__restrict__ coff,
-                                                              uint16_t *__restrict__ hjl, T *__restrict__ hv) {
-    const int64_t r = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= R) return;
-    for (int64_t W = 0; W < nW; ++W) {  // dummies (overwritten where the row has entries in W)
-        const int64_t b = coff[exp_cidx(r, W, nW, RB)];
-        hjl[b] = (uint16_t) 0x8000u;
-        hv[b] = T(0);
-    }
-    int64_t Wc = -1, base = 0, k = 0;
-    for (int64_t s = rbeg[r]; s < rend[r]; ++s) {
-        const T h = sv[s];
-        if (h == T(0)) continue;
-        const int64_t W = sj[s] / CW;
-        if (W != Wc) {
-            Wc = W;
-            base = coff[exp_cidx(r, W, nW, RB)];
-            k = 0;
-        }
-        hjl[base + k] = (uint16_t) ((sj[s] - W * CW) | (k == 0 ? 0x8000 : 0));
-        hv[base + k] = h;
-        ++k;
-    }
-}
-
-// first entry of (block I, wave v, window W), W = 0..nW
-__global__ __launch_bounds__(256) void exp_run_woff_kernel(const int64_t *__restrict__ coff, int64_t nbv, int64_t nW,
-                                                           int64_t RB, int64_t *__restrict__ woff) {
-    const int64_t RPW = RB / EXP_NWV;
-    const int64_t t = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nbv * (nW + 1)) return;
-    const int64_t bv = t / (nW + 1), W = t % (nW + 1);
-    woff[t] = coff[(bv * nW + W) * RPW];
-}
-
 // first chunk of (block I, wave v, window W), W = 0..nW (W = nW: the end of the wave's stream)
 __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__restrict__ coff, int64_t nbv, int64_t nW,
                                                             int64_t RB, int64_t *__restrict__ woff) {
@@ -1197,6 +1125,21 @@ __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__res
 #define EXP_DOT2 0
 #endif
 #endif
+
+#ifndef EXP_LDS_ATOMIC
+#define EXP_LDS_ATOMIC 1
+#endif
+// v added to a row accumulator in LDS: one ds_add (no return value, so no wait for an LDS read) instead of a
+// read-add-write. Each wave owns its rows and issues its adds in program order, and no instruction adds to one row
+// twice: the same sums in the same order as the read-add-write, bit for bit
+template <typename T>
+__device__ __forceinline__ void racc_add(T *p, T v) {
+#if EXP_LDS_ATOMIC
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+    *p += v;
+#endif
+}
 
 // one step of a segmented inclusive lane scan keyed by k (keys non-decreasing in lane order): v += the DPP
 // source lane's v when that lane holds the same key. A lane without a source (or in a masked DPP row) reads
@@ -1375,10 +1318,10 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             const int row0 = carry + below + (f0 ? 1 : 0) - 1, row1 = row0 + (f1 ? 1 : 0);
             carry += __popcll(b0) + __popcll(b1);
             if (bh == 0ull) return;  // a group wholly past the window's end
-            if (f0 || f1) racc[f1 ? row1 : row0] += (f1 ? a23 : t) - P;  // tail: the row left open in this lane
-            if (f0 && f1) racc[row0] += a01;                             // a row inside this lane
-            if ((f0 || f1) && !(lane == 0 && f0)) racc[(f0 ? row0 : row1) - 1] += E + (f0 ? 0.f : a01);  // head
-            if (lane == 63) racc[row1] += P;                             // the row open at the group's end
+            if (f0 || f1) racc_add(&racc[f1 ? row1 : row0], (f1 ? a23 : t) - P);  // tail: the row left open in this lane
+            if (f0 && f1) racc_add(&racc[row0], a01);                             // a row inside this lane
+            if ((f0 || f1) && !(lane == 0 && f0)) racc_add(&racc[(f0 ? row0 : row1) - 1], E + (f0 ? 0.f : a01));  // head
+            if (lane == 63) racc_add(&racc[row1], P);                             // the row open at the group's end
             return;
         }
         int rl = have ? g.rl : -1;
@@ -1435,8 +1378,8 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             P += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(P), 0x143, 0xC, 0xF, true));  // row_bcast:31
             const int rnext = __builtin_amdgcn_update_dpp(-1, rl, 0x130, 0xF, 0xF, false);  // wave_shl:1 (lane 63: -1)
             const bool end = rl >= 0 && (lane == 63 || rnext != rl);
-            if (end) racc[rl] += (T) P;  // rows of this wave only
-            if (end && lane != 63 && rnext >= 0) racc[rnext] -= (T) P;
+            if (end) racc_add(&racc[rl], (T) P);  // rows of this wave only
+            if (end && lane != 63 && rnext >= 0) racc_add(&racc[rnext], -(T) P);
             return;
         }
         // segmented inclusive prefix sums over the lanes by DPP (rows are non-decreasing in lane order):
@@ -1450,7 +1393,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
         seg_step<0x142, 0xA>(sacc, rl);  // row_bcast:15 (rows 1, 3)
         seg_step<0x143, 0xC>(sacc, rl);  // row_bcast:31 (rows 2, 3)
         const int rnext = __builtin_amdgcn_update_dpp(0, rl, 0x130, 0xF, 0xF, true);  // wave_shl:1 (lane 63: tested apart)
-        if (rl >= 0 && (lane == 63 || rnext != rl)) racc[rl] += sacc;  // rows of this wave only
+        if (rl >= 0 && (lane == 63 || rnext != rl)) racc_add(&racc[rl], sacc);  // rows of this wave only
 #else
         // segmented suffix sums: rows are non-decreasing in lane order
         T sacc = acc;
@@ -1484,165 +1427,6 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             fetch((cb + STEP < c_end ? cb + STEP : c_end) + lane);
 #pragma unroll
             for (int hh = 0; hh < EXP_NH; ++hh) group(cur[hh], cb + 64 * hh + lane < c_end);  // groups in order
-        }
-        if (W + 1 < W1) {
-            __syncthreads();  // every wave is done with window W
-            store_win();
-        }
-        __syncthreads();
-    }
-    const int64_t rb0 = I * RB;
-    const int rows = (int) min<int64_t>(RB, R - rb0);
-    if (G == 1) {
-        for (int t = tid; t < rows; t += NT) hs[r0 + rb0 + t] = racc[t];
-    } else {
-        for (int t = tid; t < rows; t += NT) hslab[g * R + rb0 + t] = racc[t];
-    }
-}
-
-// hs[i] = sum_j H_ij w_j over the run layout. Same block / window / prefetch structure as exp_hcell_kernel;
-// each lane takes 4 consecutive entries per step (4-aligned steps of 256 entries; the entries outside the
-// window's range [wo[W], wo[W + 1]) are masked, so a step that straddles two windows is loaded for both).
-// Rows: carry (flags so far) + the flags of the lower lanes (ballots) + the lane's own. A lane's entries
-// span consecutive rows h..t: the rows strictly inside and row h (when h != t, completed with the
-// segmented scan value of the previous lane) end in this lane; row t is summed across lanes by a segmented
-// inclusive scan keyed by t and added where it ends. Each row is written once per step, by this wave only,
-// in a fixed order: bitwise reproducible.
-template <typename T, int RBB>
-__global__ __launch_bounds__(EXP_NWV * 64) void exp_hrun_kernel(const int64_t *__restrict__ woff,
-                                                                const uint16_t *__restrict__ hjl,
-                                                                const T *__restrict__ hv, const T *__restrict__ w,
-                                                                int64_t m, int64_t r0, int64_t R, int64_t nW,
-                                                                int64_t RB, int64_t nI, int G, T *__restrict__ hs,
-                                                                T *__restrict__ hslab,
-                                                                const cg_scalars<T> *__restrict__ status) {
-    constexpr int CW = exp_cw_run<T, RBB>(), RBC = exp_rb_of<T, RBB>(), NT = EXP_NWV * 64;
-    using WT = T;  // the run layout keeps the real type
-    const T *wsrc = w;
-    __shared__ __attribute__((aligned(16))) T wl[CW];
-    __shared__ T racc[RBC];
-    if (status != nullptr && status->converged) return;
-    const int64_t bx = xcd_remap(blockIdx.x, gridDim.x);
-    const int64_t I = bx % nI, g = bx / nI;
-    const int64_t W0 = g * nW / G, W1 = (g + 1) * nW / G;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int RPW = (int) (RB / EXP_NWV);
-    for (int t = tid; t < RB; t += NT) racc[t] = T(0);
-    T *ra = racc + wave * RPW;
-    // the window of w moves as 16-byte vectors: thread tid takes vectors tid, tid + NT, ... (PV of them)
-    constexpr int VE = 16 / (int) sizeof(WT), NV = CW / VE, PV = (NV + NT - 1) / NT;
-    using wvec = __attribute__((ext_vector_type(VE))) WT;
-    wvec reg[PV];
-    auto load_win = [&](int64_t W) {
-#pragma unroll
-        for (int q = 0; q < PV; ++q) {
-            const int v = q * NT + tid;
-            if (NV % NT == 0 || v < NV) {
-                const int64_t idx = W * CW + (int64_t) v * VE;
-                if (idx + VE <= m) {
-                    reg[q] = *reinterpret_cast<const wvec *>(wsrc + idx);
-                } else {
-#pragma unroll
-                    for (int e = 0; e < VE; ++e) reg[q][e] = idx + e < m ? wsrc[idx + e] : WT(0);
-                }
-            }
-        }
-    };
-    auto store_win = [&]() {
-#pragma unroll
-        for (int q = 0; q < PV; ++q) {
-            const int v = q * NT + tid;
-            if (NV % NT == 0 || v < NV) reinterpret_cast<wvec *>(wl)[v] = reg[q];
-        }
-    };
-    const int64_t *wo = woff + (I * EXP_NWV + wave) * (nW + 1);
-    u32x2 jj_n = { 0u, 0u };
-    T h_n[4] = { T(0), T(0), T(0), T(0) };
-    auto fetch = [&](int64_t sb) {  // sb: a multiple of 4 inside the (padded) stream
-        const int64_t e = sb + 4 * lane;
-        jj_n = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(hjl + e));
-        if constexpr (sizeof(T) == 4) {
-            const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(hv + e));
-            h_n[0] = v.x, h_n[1] = v.y, h_n[2] = v.z, h_n[3] = v.w;
-        } else {
-            const f64x2 v0 = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(hv + e));
-            const f64x2 v1 = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(hv + e + 2));
-            h_n[0] = v0.x, h_n[1] = v0.y, h_n[2] = v1.x, h_n[3] = v1.y;
-        }
-    };
-    if (W0 < W1) {
-        load_win(W0);
-        store_win();
-        fetch(wo[W0] & ~int64_t(3));
-    }
-    __syncthreads();
-    const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));  // lanes below this one
-    for (int64_t W = W0; W < W1; ++W) {
-        if (W + 1 < W1) load_win(W + 1);
-        const int64_t e0 = wo[W], e1 = wo[W + 1];
-        int carry = 0;  // flags (rows started) before this step in window W
-        for (int64_t sb = e0 & ~int64_t(3); sb < e1; sb += 256) {  // wave-uniform trip count
-            const u32x2 jj = jj_n;
-            const T hc[4] = { h_n[0], h_n[1], h_n[2], h_n[3] };
-            fetch(sb + 256 < e1 ? sb + 256 : (e1 & ~int64_t(3)));  // next step (the next window's first at the end)
-            const int64_t e = sb + 4 * lane;
-            const unsigned jr[4] = { jj.x & 0xFFFFu, jj.x >> 16, jj.y & 0xFFFFu, jj.y >> 16 };
-            T a[4];
-            int fl[4];
-            uint64_t nb = 0;  // flags in lower lanes
-            int tot = 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const bool v = e + u >= e0 && e + u < e1;
-                fl[u] = v && (jr[u] & 0x8000u) ? 1 : 0;
-                a[u] = v ? hc[u] * wl[jr[u] & 0x7FFFu] : T(0);
-                const uint64_t b = __ballot(fl[u]);
-                nb += (uint64_t) __popcll(b & lt);
-                tot += __popcll(b);
-            }
-            int r[4];
-            int cum = carry + (int) nb;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                cum += fl[u];
-                r[u] = cum - 1;  // -1: entries before the window's first (masked, a = 0)
-            }
-            carry += tot;
-            const int h = r[0], t = r[3];
-            T ts = T(0), hsum = T(0);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (r[u] == t) ts += a[u];
-                else if (r[u] == h) hsum += a[u];
-            }
-            // rows strictly between h and t end in this lane (at most two: 4 entries)
-            if (t - h >= 2 && h + 1 >= 0) {
-                T s1 = T(0);
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (r[u] == h + 1) s1 += a[u];
-                ra[h + 1] += s1;
-            }
-            if (t - h >= 3 && h + 2 >= 0) {
-                T s2 = T(0);
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (r[u] == h + 2) s2 += a[u];
-                ra[h + 2] += s2;
-            }
-            // segmented inclusive scan of the tail sums keyed by the tail row
-            T sc = ts;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const T so = __shfl_up(sc, off);
-                const int ko = __shfl_up(t, off);
-                if (lane >= off && ko == t) sc += so;
-            }
-            const T sprev = __shfl_up(sc, 1);
-            const int tprev = __shfl_up(t, 1);
-            const int hnext = __shfl_down(h, 1);
-            if (h != t && h >= 0) ra[h] += hsum + ((lane > 0 && tprev == h) ? sprev : T(0));
-            if (t >= 0 && (lane == 63 || hnext != t)) ra[t] += sc;
         }
         if (W + 1 < W1) {
             __syncthreads();  // every wave is done with window W
@@ -1859,12 +1643,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
                                             stream));
             MI_HIP_CHECK(hipStreamSynchronize(stream));
         }
-        // incidences per sub-block (≈ 80 B each in flight); PLSSVM_MI_EXP_CAPLOG = log2 (measurements)
-        const int64_t CAP = int64_t(1) << [] {
-            const char *e = std::getenv("PLSSVM_MI_EXP_CAPLOG");
-            const int v = e ? std::atoi(e) : 0;
-            return v >= 20 && v <= 31 ? v : 27;
-        }();
+        constexpr int64_t CAP = int64_t(1) << 27;  // incidences per sub-block (≈ 80 B each in flight)
         constexpr int64_t ROWS_MAX = 65536;            // rows per sub-block (one workgroup per row)
         std::vector<std::pair<int64_t, int64_t>> blocks;
         {
@@ -2448,11 +2227,8 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             ex.RBB = 32768;
             int64_t nI = ceil_div(Rr, cap_max);
             ex.G = (int) std::max<int64_t>(1, cus / nI);
-#ifndef PLSSVM_MI_EXP_FILLCU
-#define PLSSVM_MI_EXP_FILLCU 1
-#endif
             // as many row blocks as the G window groups leave CUs (3-RBF: 128 x 2 = 256 workgroups, not 123 x 2)
-            if (PLSSVM_MI_EXP_FILLCU) nI = std::max<int64_t>(nI, cus / ex.G);
+            nI = std::max<int64_t>(nI, cus / ex.G);
             ex.RB = (int) round_up(ceil_div(Rr, nI), (int64_t) EXP_NWV);
         }
         if (const char *e = std::getenv("PLSSVM_MI_EXP_RBB")) {
@@ -2479,47 +2255,7 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             MI_HIP_CHECK(hipMemcpyAsync(&ex.slots, coff.get() + ncnt, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
             MI_HIP_CHECK(hipStreamSynchronize(stream));
         };
-        // PLSSVM_MI_EXP_RUNS = 1: the run layout (when its dummies, rows without partners in a window, stay
-        // under 5 % of the entries; = 2 regardless). Off by default: 11-20 % fewer bytes (config 3-RBF 7.87 ->
-        // 6.99 GB, config 5 8.89 -> 7.10 GB) but 2.5x the VALU per 256-entry step (161 vs 64: row numbering,
-        // multi-row lanes, the segmented scan), measured 1.52 vs 1.42 ms (3-RBF) and 1.74 vs 1.67 ms (5)
-        // In a real group only the forced option (= 2, the same on every rank): the run layout keeps real H, so a
-        // per-rank choice would split the group's H storage again.
-        const char *re = std::getenv("PLSSVM_MI_EXP_RUNS");
-        int runs_opt = re != nullptr ? std::atoi(re) : 0;
-        if (in_group() && runs_opt != 2) runs_opt = 0;
-        ex.runs = false;
-        if (runs_opt != 0 && R > 0) {
-            ex.CW = exp_cw_run_host(ex.RBB, (int) sizeof(T));
-            ex.nW = ceil_div(std::max<int64_t>(m, 1), (int64_t) ex.CW);
-            const int64_t ncnt = ex.nblk * RB * ex.nW;
-            cnt.alloc(ncnt + 1, stream);
-            coff.alloc(ncnt + 1, stream, false);
-            dev_buf<unsigned long long> dum;
-            dum.alloc(1, stream);
-            hipLaunchKernelGGL(exp_run_count_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                               rbeg, rend, sj.get(), sv.get(), R, ex.nW, (int64_t) ex.CW, RB, cnt.get(), dum.get());
-            MI_LAUNCH_CHECK();
-            unsigned long long nd = 0;
-            MI_HIP_CHECK(hipMemcpyAsync(&nd, dum.get(), sizeof(nd), hipMemcpyDeviceToHost, stream));
-            scan(ncnt);
-            ex.runs = runs_opt == 2 || (double) nd <= 0.05 * (double) (ex.slots - (int64_t) nd);
-            if (ex.runs) {
-                ex.nchunks = 0;
-                ex.hjl.alloc(ex.slots + 512, stream);  // steps of 256 entries from 4-aligned starts
-                ex.hv.alloc(ex.slots + 512, stream);
-                ex.hrow.reset();
-                hipLaunchKernelGGL(exp_run_scatter_kernel<T>, dim3((unsigned) ceil_div(R, 256)), dim3(256), 0, stream,
-                                   rbeg, rend, sj.get(), sv.get(), R, ex.nW, (int64_t) ex.CW, RB, coff.get(),
-                                   ex.hjl.get(), ex.hv.get());
-                MI_LAUNCH_CHECK();
-                ex.woff.alloc(std::max<int64_t>(nbv * (ex.nW + 1), 1), stream);
-                hipLaunchKernelGGL(exp_run_woff_kernel, dim3((unsigned) ceil_div(nbv * (ex.nW + 1), 256)), dim3(256),
-                                   0, stream, coff.get(), nbv, ex.nW, RB, ex.woff.get());
-                MI_LAUNCH_CHECK();
-            }
-        }
-        if (!ex.runs) {
+        {
             // H storage (float contexts): bfloat16 H and bfloat16 windows of w when every stored |H_ij| is at most
             // 2^-16 of its pair's kernel value (row join's hratio). H_ij w_j is then formed from two values with
             // relative error <= 2^-9 each, so each pair's term moves by at most ~2^-8 |H_ij w_j| <= 2^-24 of
@@ -2660,19 +2396,7 @@ void engine<T>::expansion_dominant(const T *w, const cg_scalars<T> *status) {
                                ex.hrow.get(), ex.hjl.get(), ex.hv.get(), ex.hv16.get(), w, ex.wv16.get(), m, r0, r1 - r0, ex.nW,
                                (int64_t) ex.RB, ex.nblk, ex.G, ex.hs.get(), ex.hslab.get(), status, (exp_ablate() & 4) ? 1 : 0);
         };
-        auto launch_run = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3((unsigned) (ex.nblk * ex.G)), dim3(EXP_NWV * 64), 0, stream, ex.woff.get(),
-                               ex.hjl.get(), ex.hv.get(), w, m, r0, r1 - r0, ex.nW, (int64_t) ex.RB, ex.nblk, ex.G,
-                               ex.hs.get(), ex.hslab.get(), status);
-        };
-        if (ex.runs) {
-            switch (ex.RBB) {
-                case 4096: launch_run(exp_hrun_kernel<T, 4096>); break;
-                case 8192: launch_run(exp_hrun_kernel<T, 8192>); break;
-                case 32768: launch_run(exp_hrun_kernel<T, 32768>); break;
-                default: launch_run(exp_hrun_kernel<T, 16384>);
-            }
-        } else {
+        {
             auto pick = [&](auto hb, auto rf, auto d2) {
                 constexpr bool HB = decltype(hb)::value, D2 = decltype(d2)::value;
                 constexpr int RF = decltype(rf)::value;
@@ -2765,12 +2489,10 @@ void engine<T>::expansion_mscale(const cg_scalars<T> *status) {
 // The CG direction update carries the next K·p's w pass (round 5): with bfloat16 windows the K·p of d starts with
 // exp_wown_kernel over the rows the direction update has just written (w = e d, its bfloat16 copy, S partials); the
 // update forms them in its own element loop (cgk::w_elem, the same grid and order: the same bits) and the K·p skips
-// the launch. Sharded: the rank's rows, whose w the group then gathers as before. PLSSVM_MI_DIR_W=0: off.
+// the launch. Sharded: the rank's rows, whose w the group then gathers as before. (Measured neutral, round 5.)
 template <typename T>
 bool engine<T>::dir_w_fill(dir_w_t<T> &o) {
-    const char *env = std::getenv("PLSSVM_MI_DIR_W");
-    const bool on = env == nullptr || std::atoi(env) != 0;
-    if (!on || !sparse_stored() || factored() || csr.otf_on || !csr.ex.on || !csr.ex.hbf16) return false;
+    if (!sparse_stored() || factored() || csr.otf_on || !csr.ex.on || !csr.ex.hbf16) return false;
     if (shard) {  // expansion_kp_raw's g16 over [r0, r1)
         const bool rgrp = comm != nullptr && cstream != nullptr;
         if (d <= 0 || !(rgrp || sim_world > 0) || v0 != r0 || vn != r1 - r0) return false;

@@ -114,61 +114,21 @@ __constant__ double c_exp2_256[256] = {
     1.978456026387951, 1.9838201648502194, 1.9891988469672663, 1.9945921121709402
 };
 
-// 32-entry variant (PLSSVM_MI_EXP_TAB = 32, not the default): 2^(i/32) is one 256-B LDS bank row, so its
-// table read is conflict-free for any index pattern, at the price of a degree-5 (or 6) polynomial
-// (Chebyshev fit on [-1/2, 1/2]: worst relative error of the double Horner evaluation 2.5e-16 /
-// 1.1e-16). Measured on config 2: 39.36 / 39.57 ms vs 39.07 ms for the 256-entry
-// table — the table read costs its issue and latency, not bank conflicts.
-#ifndef PLSSVM_MI_EXP_TAB
-#define PLSSVM_MI_EXP_TAB 256
-#endif
-#ifndef PLSSVM_MI_EXP_DEG
-#define PLSSVM_MI_EXP_DEG 5
-#endif
-__constant__ double c_exp2_32[32] = {
-    1.0, 1.0218971486541166, 1.0442737824274138, 1.0671404006768237, 1.0905077326652577, 1.1143867425958924,
-    1.1387886347566916, 1.1637248587775775, 1.189207115002721, 1.215247359980469, 1.241857812073484,
-    1.2690509571917332, 1.2968395546510096, 1.3252366431597413, 1.3542555469368927, 1.383909881963832,
-    1.4142135623730951, 1.4451808069770467, 1.4768261459394993, 1.5091644275934228, 1.5422108254079407,
-    1.5759808451078865, 1.6104903319492543, 1.645755478153965, 1.681792830507429, 1.718619298122478,
-    1.7562521603732995, 1.7947090750031072, 1.8340080864093424, 1.8741676341103, 1.9152065613971474,
-    1.9571441241754002
-};
-constexpr int EXP_TAB = PLSSVM_MI_EXP_TAB;
-constexpr double KEXP = EXP_TAB == 32 ? 46.16624130844683 : 369.3299304675746;  // EXP_TAB / ln 2
+// (A 32-entry table — one 256-B LDS bank row, conflict-free for any index pattern — with a degree-5 / 6 Chebyshev
+// polynomial measured 39.36 / 39.57 ms against 39.07 ms for this 256-entry table on config 2, DESIGN.md §3.1: the
+// table read costs its issue and latency, not bank conflicts.)
+constexpr int EXP_TAB = 256;
+constexpr double KEXP = 369.3299304675746;  // EXP_TAB / ln 2
 
-#ifndef PLSSVM_MI_ABL_DENSE
-#define PLSSVM_MI_ABL_DENSE 0  // timing ablations only: 1 kv = y (no exp), 2 no table read, 3 no ldexp
-#endif
 __device__ __forceinline__ double exp_scaled_f64(double y, const double *tab) {
-    if constexpr (PLSSVM_MI_ABL_DENSE == 1) return y;
     const double jn = rint(y);
     const double r = y - jn;  // exact
-    double pr;
-    if constexpr (EXP_TAB == 32 && PLSSVM_MI_EXP_DEG == 6) {
-        double t = fma(1.4345708169159177e-13, r, 3.973729405781781e-11);
-        t = fma(t, r, 9.172562701758912e-09);
-        t = fma(t, r, 1.6938509724129055e-06);
-        t = fma(t, r, 0.0002345961982022468);
-        t = fma(t, r, 0.02166084939249829);
-        pr = fma(t, r, 1.0);
-    } else if constexpr (EXP_TAB == 32) {
-        double t = fma(3.9737266313166245e-11, r, 9.172616498159851e-09);
-        t = fma(t, r, 1.6938509724215757e-06);
-        t = fma(t, r, 0.0002345961981972034);
-        t = fma(t, r, 0.02166084939249829);
-        pr = fma(t, r, 1.0);
-    } else {
-        double t = fma(2.239395190875157e-12, r, 3.3083026805413713e-09);  // (ln2/256)^k / k!, k = 4..1
-        t = fma(t, r, 3.6655655969101062e-06);
-        t = fma(t, r, 0.0027076061740622863);
-        pr = fma(t, r, 1.0);
-    }
+    double t = fma(2.239395190875157e-12, r, 3.3083026805413713e-09);  // (ln2/256)^k / k!, k = 4..1
+    t = fma(t, r, 3.6655655969101062e-06);
+    t = fma(t, r, 0.0027076061740622863);
+    const double pr = fma(t, r, 1.0);
     const int j = (int) jn;  // saturates for huge |y|: the ldexp below then returns 0
-    constexpr int SH = EXP_TAB == 32 ? 5 : 8;
-    if constexpr (PLSSVM_MI_ABL_DENSE == 2) return ldexp(pr, j >> SH);
-    if constexpr (PLSSVM_MI_ABL_DENSE == 3) return tab[j & (EXP_TAB - 1)] * pr;
-    return ldexp(tab[j & (EXP_TAB - 1)] * pr, j >> SH);
+    return ldexp(tab[j & (EXP_TAB - 1)] * pr, j >> 8);
 }
 
 // 16 B per lane global -> LDS through a buffer descriptor on a wave-uniform base: the per-lane part is
@@ -290,7 +250,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
     smem[tid] = pin;
     smem[2 * KP_TILE + tid] = nin;
     if constexpr (FAST_EXP) {
-        if (tid < EXP_TAB) exp_tab[tid] = EXP_TAB == 32 ? c_exp2_32[tid] : c_exp2_256[tid];  // visible after the first K-loop barrier
+        if (tid < EXP_TAB) exp_tab[tid] = c_exp2_256[tid];  // visible after the first K-loop barrier
     }
 
     const int64_t nk = d_pad / BK;
@@ -393,35 +353,6 @@ __device__ __forceinline__ void kp_sb_values(const T *__restrict__ partial, int6
     }
 }
 
-// raw[i] = sum over the column blocks c = 0 .. nb-1 (in order) of row i's slab values: the whole
-// triangle on one rank. One thread per row; a wave's 64 rows share their row block, so the record
-// arithmetic is wave-uniform; a super-block's 8 records in flight per step
-template <typename T>
-__global__ __launch_bounds__(256) void kp_reduce_kernel(const T *__restrict__ partial, int64_t nb, int64_t m,
-                                                        const int32_t *__restrict__ wg_off, T *__restrict__ raw,
-                                                        const cg_scalars<T> *__restrict__ status) {
-    if (status != nullptr && status->converged) return;
-    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t Ib = __builtin_amdgcn_readfirstlane((int) (((int64_t) blockIdx.x * blockDim.x + (threadIdx.x & ~63)) / KP_TILE));
-    if (i >= m) return;
-    const int64_t q = i % KP_TILE, RS = Ib / KP_SUPER, ns = (nb + KP_SUPER - 1) / KP_SUPER;
-    T s = 0;
-    for (int64_t CS = 0; CS < ns; ++CS) {
-        const int64_t sb = RS >= CS ? tri_index(RS, CS) : tri_index(CS, RS);
-        const int64_t base = wg_off[sb];
-        const int cnt = (int) min<int64_t>(KP_SUPER, nb - CS * KP_SUPER);
-        T v[KP_SUPER];
-        if (cnt == KP_SUPER) {
-            kp_sb_values(partial, Ib, q, CS, nb, base, v, KP_SUPER);
-#pragma unroll
-            for (int u = 0; u < KP_SUPER; ++u) s += v[u];
-        } else {
-            kp_sb_values(partial, Ib, q, CS, nb, base, v, cnt);
-            for (int u = 0; u < cnt; ++u) s += v[u];
-        }
-    }
-    raw[i] = s;
-}
 
 // raw[i] = sum of the slab values of the super-blocks [s0, s1) (a rank's share, or the whole triangle): the
 // column super-blocks of a row are dealt to the 16 waves of a block (64 rows per block, lanes = rows:
@@ -501,23 +432,13 @@ void launch_kp_tiles(kfun<T> kf, const T *XT, const T *norms, const T *p, T *par
 
 // Both the whole triangle and a rank's share use the wave-split reduction (16 waves per 64 rows, each a
 // range of column super-blocks, partial sums added in wave order): one thread per row walking all nb
-// records (kp_reduce_kernel, PLSSVM_MI_KP_REDUCE=1) is latency-bound — 0.43 ms for config 2's 627 MB slab.
+// records (round 1's kp_reduce_kernel) was latency-bound — 0.43 ms for config 2's 627 MB slab.
 template <typename T>
 void launch_kp_reduce(const T *partial, int64_t nb, int64_t m, int64_t s0, int64_t s1, const int32_t *wg_off, T *raw,
                       const cg_scalars<T> *status, hipStream_t s) {
     if (m <= 0) return;
-    static const bool serial = [] {
-        const char *e = std::getenv("PLSSVM_MI_KP_REDUCE");
-        return e != nullptr && std::atoi(e) == 1;
-    }();
-    const int64_t ns = ceil_div(nb, KP_SUPER);
-    if (serial && s0 == 0 && s1 == ns * (ns + 1) / 2) {
-        hipLaunchKernelGGL(kp_reduce_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, s, partial, nb, m,
-                           wg_off, raw, status);
-    } else {
-        hipLaunchKernelGGL(kp_reduce_share_kernel<T>, dim3((unsigned) ceil_div(m, 64)), dim3(64 * KP_RED_G), 0, s,
-                           partial, nb, m, s0, s1, wg_off, raw, status);
-    }
+    hipLaunchKernelGGL(kp_reduce_share_kernel<T>, dim3((unsigned) ceil_div(m, 64)), dim3(64 * KP_RED_G), 0, s,
+                       partial, nb, m, s0, s1, wg_off, raw, status);
     MI_LAUNCH_CHECK();
 }
 

@@ -65,17 +65,12 @@ __global__ __launch_bounds__(256) void otf_pack_kernel(const T *__restrict__ p, 
     if (j < m) pne[j] = pne_t<T>{ p[j], norms[j], ev != nullptr ? ev[j] : T(1), T(0) };
 }
 
-// partner accumulators per wave: CWB bytes (4 / 8 / 16 / 32 KiB; PLSSVM_MI_OTF_CWB, default 8 KiB)
+// partner accumulators per wave: CWB bytes (8 KiB; 16 / 32 KiB measured 1.06x / 2.3x slower — fewer waves —, 4 KiB
+// 1.9x slower)
 template <typename T, int CWB>
 constexpr int otf_cw() { return CWB / (int) sizeof(T); }
-inline int otf_cwb() {
-    static const int v = [] {
-        const char *e = std::getenv("PLSSVM_MI_OTF_CWB");
-        const int b = e != nullptr ? std::atoi(e) : 8192;
-        return (b == 4096 || b == 16384 || b == 32768) ? b : 8192;
-    }();
-    return v;
-}
+constexpr int OTF_CWB = 8192;
+inline int otf_cwb() { return OTF_CWB; }
 
 // pair part c_ij = k_ij - kappa_ij for s_ij != 0 (the Gram pattern's forms, sparse.hip)
 template <typename T>
@@ -383,7 +378,6 @@ void engine<T>::setup_otf(int rbf_fact_ok) {
     MI_LAUNCH_CHECK();
     csr.pne.alloc(4 * std::max<int64_t>(m, 1), stream, false);
     csr.otf_part.alloc(std::max<int64_t>(m, 1), stream, false);
-    if (const char *e = std::getenv("PLSSVM_MI_OTF_WPL")) csr.otf_wpl = std::max<long long>(0, std::atoll(e));
     csr.cjv.alloc(2 * std::max<int64_t>(csr.nnz, 1), stream, false);
     if (csr.nnz > 0)
         hipLaunchKernelGGL(otf_jv_kernel<T>, dim3((unsigned) ceil_div(csr.nnz, 256)), dim3(256), 0, stream,
@@ -428,26 +422,15 @@ void engine<T>::otf_dominant(const T *p, const cg_scalars<T> *status) {
     hipLaunchKernelGGL(otf_pack_kernel<T>, dim3((unsigned) ceil_div(m, 256)), dim3(256), 0, stream, p, norms.get(),
                        kernel == 2 ? csr.e.get() : nullptr, m, pne, status);
     MI_LAUNCH_CHECK();
-    // windows per launch (PLSSVM_MI_OTF_WPL; default: all in one launch). Splitting the windows over
-    // launches keeps every wave of the GPU on the same partner window (its CSC segments shared through
-    // the L2s / Infinity Cache): measured no gain at 1 % density (1 / 4 / all windows per launch: 0.626 /
-    // 0.605 / 0.610 s), the segment walk is bound by its scattered L2 misses either way
-    const int64_t nW = csr.otf_nw, wpl = csr.otf_wpl > 0 ? csr.otf_wpl : nW;
-    auto launch = [&](auto kern) {
-        for (int64_t Wa = 0; Wa < nW; Wa += wpl) {
-            const int64_t Wb = std::min(nW, Wa + wpl);
-            hipLaunchKernelGGL(kern, dim3((unsigned) ceil_div(r1 - r0, OTF_NT / 64)), dim3(OTF_NT), 0, stream,
-                               csr.rowptr.get(), csr.col.get(), csr.val.get(), csr.ecb.get(),
-                               reinterpret_cast<const otf_jv<T> *>(csr.cjv.get()), csr.seg.get(), norms.get(),
-                               kernel == 2 ? csr.e.get() : nullptr, pne, m, nW, r0, r1, pf, Wa, Wb, csr.otf_part.get(),
-                               raw.get(), status);
-        }
-    };
-    const int cwb = csr.otf_cw * (int) sizeof(T);
-    if (cwb == 32768) launch(otf_kp_kernel<T, 32768>);
-    else if (cwb == 16384) launch(otf_kp_kernel<T, 16384>);
-    else if (cwb == 4096) launch(otf_kp_kernel<T, 4096>);
-    else launch(otf_kp_kernel<T, 8192>);
+    // all partner windows in one launch (round 3: splitting them over launches, so that every wave of the GPU works on
+    // one window whose CSC segments are shared in the L2s / Infinity Cache, measured no gain at 1 % density — 1 / 4 /
+    // all windows per launch 0.626 / 0.605 / 0.610 s: the segment walk is bound by its scattered L2 misses either way)
+    const int64_t nW = csr.otf_nw;
+    hipLaunchKernelGGL((otf_kp_kernel<T, OTF_CWB>), dim3((unsigned) ceil_div(r1 - r0, OTF_NT / 64)), dim3(OTF_NT), 0, stream,
+                       csr.rowptr.get(), csr.col.get(), csr.val.get(), csr.ecb.get(),
+                       reinterpret_cast<const otf_jv<T> *>(csr.cjv.get()), csr.seg.get(), norms.get(),
+                       kernel == 2 ? csr.e.get() : nullptr, pne, m, nW, r0, r1, pf, (int64_t) 0, nW, csr.otf_part.get(),
+                       raw.get(), status);
     MI_LAUNCH_CHECK();
 }
 

@@ -668,14 +668,9 @@ void host_check_csr(const int64_t *rowptr, const int32_t *col, int64_t n, int64_
 
 }  // namespace
 
-// FP22 input: the SELL streams hold the packed values (PLSSVM_MI_SELL_F22=1) or their exact fp32 decoding
-inline bool sell_fp22_stream() {
-    static const bool on = [] {
-        const char *e = std::getenv("PLSSVM_MI_SELL_F22");
-        return e == nullptr || std::atoi(e) != 0;
-    }();
-    return on;
-}
+// FP22 input: the SELL streams hold the packed values (2.75 B per value; their exact fp32 decoding, 4 B, measured
+// equal to 1 % slower on config 5, round 4)
+inline bool sell_fp22_stream() { return true; }
 
 // ---- engine members ----------------------------------------------------------------------------------
 // the CSC of rows 0..m-1 from the device CSR (0 < nnz < 2^31): entries sorted by column with a stable radix sort
@@ -761,7 +756,6 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
     n_pad = std::max<int64_t>(nb, 1) * KP_TILE;
     d_pad = d;
     csr = csr_data<T>{};
-    rb_cg_state = -1;  // the row-block CG pass is checked again for the new plan
     csr.val_fmt = val_fmt;
     const int64_t nnz = rowptr[m];  // rows 0..m-1
     csr.nnz = nnz;
@@ -955,7 +949,7 @@ void engine<T>::setup_csr(const int64_t *rowptr, const int32_t *col, const void 
                 MI_HIP_CHECK(hipSetDevice(device));
                 MI_HIP_CHECK(hipStreamCreateWithFlags(&rs, hipStreamNonBlocking));
                 build_spmv_plan<T>(csr.spmv_csr, r1 - r0, d, rowptr[r1] - rowptr[r0], f22, csr_gen(r0), blocks, rs);
-                if (world == 1 && sim_world == 0 && rowblock_fused_enabled())  // CG: CSR pass + finalize in one launch
+                if (world == 1 && sim_world == 0)  // CG: CSR pass + finalize in one launch
                     build_rowblock_plan<T>(csr.rb_csr, m, d, f22, csr_gen(0), blocks, rs);
                 MI_HIP_CHECK(hipStreamSynchronize(rs));
             } catch (...) {

@@ -50,10 +50,6 @@ inline int exp_cw_host(int rbb, int es) { return (EXP_LDS - rbb) / es / 1024 * 1
 template <int RBB>
 constexpr int exp_cw16_of() { return (EXP_LDS - RBB) / 2 / 1024 * 1024 < 65536 ? (EXP_LDS - RBB) / 2 / 1024 * 1024 : 65536; }
 inline int exp_cw16_host(int rbb) { return std::min((EXP_LDS - rbb) / 2 / 1024 * 1024, 65536); }
-// the run layout keeps a flag in bit 15 of the window-local j: windows of at most 32768 partners
-template <typename T, int RBB>
-constexpr int exp_cw_run() { return exp_cw_of<T, RBB>() < 32768 ? exp_cw_of<T, RBB>() : 32768; }
-inline int exp_cw_run_host(int rbb, int es) { return exp_cw_host(rbb, es) < 32768 ? exp_cw_host(rbb, es) : 32768; }
 
 // phi's polynomial coefficients (kernel argument of the moment / Horner kernels)
 struct coefs {
@@ -79,7 +75,6 @@ struct exp_data {
     int64_t slots = 0, nchunks = 0, nblk = 0, nW = 0;
     int RBB = 16384, RB = 0, CW = 0;  // geometry (see above): accumulator bytes, rows per block, window
     int G = 1;                         // window groups per row block (G > 1: row sums via hslab)
-    bool runs = false;                 // run layout (exp_hrun_kernel): no padding / chunk rows, see expand.hip
     dev_buf<T> hslab;                  // [G][rows] partial row sums of the window groups
     dev_buf<uint16_t> hjl;            // [slots] j - W * CW
     dev_buf<T> hv;                    // [slots] H_ij (the real type)
@@ -144,7 +139,6 @@ struct csr_data {
     bool otf_on = false;
     int otf_cw = 0;
     int64_t otf_nw = 0;
-    int64_t otf_wpl = 0;    // partner windows per launch (0: all; PLSSVM_MI_OTF_WPL at setup)
     dev_buf<int2> seg;      // [d][otf_nw]
     dev_buf<int64_t> ecb;   // [nnz]: colptr[col[k]] per CSR entry
     dev_buf<T> pne;         // [m][4]: p_j, |x_j|^2, e_j, 0 of the current K·p

@@ -39,59 +39,29 @@ namespace plssvm_mi {
 
 constexpr int SELL_NT = 1024;  // 16 waves per workgroup
 constexpr int SELL_WAVES = SELL_NT / 64;
-#ifndef PLSSVM_MI_SELL_XBYTES
-#define PLSSVM_MI_SELL_XBYTES 163840
-#endif
-constexpr int SELL_XBYTES = PLSSVM_MI_SELL_XBYTES;  // LDS panel of the gathered vector (all of a CU's LDS)
-constexpr int SELL_SIGMA = 4096;    // sorting window (segments)
+constexpr int SELL_XBYTES = 163840;  // LDS panel of the gathered vector (all of a CU's LDS)
+constexpr int SELL_SIGMA = 4096;     // sorting window (segments)
 // entries per lane in flight per step: the passes are bound by the bytes in flight per CU (one 1024-thread
 // workgroup per CU, every step's loads issued together). Measured on one box (round 3, CG it/s): real-typed
 // values 4 / 6 / 8 entries: config 3 6 777 / 7 011 / 7 203, 3-RBF 958 / 961 / 969; packed FP22 (8-byte loads
 // per value) config 5 778 / 771 / 761 — so 8 for real values, 4 for FP22 (round 2, before the row-block pass
 // and the 16-bit pair loads, measured 4 best for both)
-#ifndef PLSSVM_MI_SELL_UNROLL
-#define PLSSVM_MI_SELL_UNROLL 8
-#endif
-#ifndef PLSSVM_MI_SELL_UNROLL_F22
-#define PLSSVM_MI_SELL_UNROLL_F22 4
-#endif
 template <bool F22>
-constexpr int sell_unroll() { return F22 ? PLSSVM_MI_SELL_UNROLL_F22 : PLSSVM_MI_SELL_UNROLL; }
-constexpr int SELL_UNROLL = PLSSVM_MI_SELL_UNROLL;
-// IDX2: the 16-bit panel indices of entries 2t, 2t+1 of a slot are adjacent, so one 32-bit load per lane
-// (256 B per wave-instruction) fetches two; chunk widths are padded to even
-#ifndef PLSSVM_MI_SELL_IDX2
-#define PLSSVM_MI_SELL_IDX2 1
+#ifndef SELL_SU_F22
+#define SELL_SU_F22 4
 #endif
-constexpr bool SELL_IDX2 = PLSSVM_MI_SELL_IDX2 != 0;
-// VAL2 (with IDX2): the values are stored in the same pair-interleaved order (one 8 / 16-byte load per
-// lane fetches two real values; FP22 streams keep per-entry decoding at the remapped positions)
-#ifndef PLSSVM_MI_SELL_VAL2
-#define PLSSVM_MI_SELL_VAL2 0
-#endif
-constexpr bool SELL_VAL2 = SELL_IDX2 && PLSSVM_MI_SELL_VAL2 != 0;
-// F22PAIR (with IDX2, FP22 streams of the panelled passes only): entries 2t, 2t+1 of a slot adjacent in the packed
-// stream as well, so one 12-byte load per lane (3 words at 4-byte alignment) decodes two values instead of two
-// overlapping 8-byte loads
-#ifndef PLSSVM_MI_SELL_F22PAIR
-#define PLSSVM_MI_SELL_F22PAIR 1
-#endif
-constexpr bool SELL_F22PAIR = SELL_IDX2 && PLSSVM_MI_SELL_F22PAIR != 0;
+constexpr int sell_unroll() { return F22 ? SELL_SU_F22 : 8; }
+// LDS-panel passes: the 16-bit panel indices of entries 2t, 2t+1 of a slot are adjacent, so one 32-bit load per lane
+// (256 B per wave-instruction) fetches two (chunk widths padded to even); packed FP22 values likewise, one 12-byte
+// load per lane (3 words at 4-byte alignment) decodes two. (Pairing real values too measured no gain, round 2.)
 // storage position of the entry at value position t = off + 64 j + l (off % 128 == 0 when paired)
 inline int64_t sell_pair_pos(int64_t t) { return (t & ~int64_t(127)) + 2 * (t & 63) + ((t >> 6) & 1); }
-static_assert(!SELL_IDX2 || (sell_unroll<false>() % 2 == 0 && sell_unroll<true>() % 2 == 0), "paired indices need an even step");
+static_assert(sell_unroll<false>() % 2 == 0 && sell_unroll<true>() % 2 == 0, "paired indices need an even step");
 template <typename T>
 constexpr int sell_width() { return SELL_XBYTES / (int) sizeof(T); }
-// workgroups per pass: equal-cost chunk ranges, a multiple of the 256 CUs (one resident workgroup per
-// CU with a full-LDS panel); PLSSVM_MI_SELL_BLOCKS overrides (measurements)
-inline int64_t sell_target_blocks() {
-    static const int64_t nb = [] {
-        const char *e = std::getenv("PLSSVM_MI_SELL_BLOCKS");
-        const long v = e ? std::atol(e) : 0;
-        return v > 0 ? (int64_t) v : (int64_t) 256;
-    }();
-    return nb;
-}
+// workgroups per pass: equal-cost chunk ranges, one per CU (one resident workgroup per CU with a full-LDS panel;
+// 512 / 768 / 1024 measured 8 / 14 / 18 % slower on config 3, round 4)
+inline int64_t sell_target_blocks() { return 256; }
 
 struct sell_chunk {
     int64_t off;    // first entry (entry j of slot l at off + 64 j + l)
@@ -189,10 +159,7 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
         const int ce = min(c1, (q + 1) * nchp);  // chunks of panel q are [q nchp, (q + 1) nchp)
         T *o = out + (int64_t) q * nseg * OC;
         const T *xg = x + (int64_t) q * W * XC;  // LDSX: panel q gathers x[q W + local]; otherwise W = 0
-#ifndef PLSSVM_MI_ABL_SELL
-#define PLSSVM_MI_ABL_SELL 0  // timing ablation only: 1 = skip the panel fill (wrong results)
-#endif
-        if constexpr (LDSX && PLSSVM_MI_ABL_SELL != 1) {
+        if constexpr (LDSX) {
             if (cb != c0) __syncthreads();
             const int xl = (int) min((int64_t) W, xn - (int64_t) q * W) * XC;
             // 16-byte loads and LDS stores (XW is a multiple of 16 B per thread); a misaligned panel
@@ -232,17 +199,10 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
 #pragma unroll
                 for (int u = 0; u < SU; ++u) {
                     const int64_t k = base + (int64_t) min(j + u, last) * 64;
-                    if constexpr (!(LDSX && SELL_IDX2)) ci[u] = __builtin_nontemporal_load(idx + k);
-                    if constexpr (LDSX && F22 && SELL_F22PAIR && !SELL_VAL2) {
-                        // paired below
-                    } else if constexpr (!(LDSX && SELL_VAL2)) {
-                        vi[u] = sell_val<T, F22>(val, k);
-                    } else if constexpr (F22) {
-                        const int jj = min(j + u, last);
-                        vi[u] = sell_val<T, F22>(val, ch.off + 128 * (int64_t) (jj >> 1) + 2 * lane + (jj & 1));
-                    }
+                    if constexpr (!LDSX) ci[u] = __builtin_nontemporal_load(idx + k);
+                    if constexpr (!(LDSX && F22)) vi[u] = sell_val<T, F22>(val, k);
                 }
-                if constexpr (LDSX && F22 && SELL_F22PAIR && !SELL_VAL2) {
+                if constexpr (LDSX && F22) {
                     // entries jj, jj + 1 (jj even) of this slot at stream positions p, p + 1, p = off + 128 (jj / 2) + 2 lane:
                     // bits 22 p .. 22 p + 43 lie in the 3 words from (22 p) / 32 (shift 22 p % 32 <= 28)
                     const int lastp = max((ch.width >> 1) - 1, 0);
@@ -261,18 +221,7 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
                         vi[2 * u2 + 1] = (T) fp22_decode(c1);
                     }
                 }
-                if constexpr (LDSX && SELL_VAL2 && !F22) {
-                    using V2 = __attribute__((ext_vector_type(2))) T;
-                    const V2 *vp = reinterpret_cast<const V2 *>(val.v) + (ch.off >> 1) + lane;
-                    const int lastp = max((ch.width >> 1) - 1, 0);
-#pragma unroll
-                    for (int u2 = 0; u2 < SU / 2; ++u2) {
-                        const V2 pr = __builtin_nontemporal_load(vp + (int64_t) min((j >> 1) + u2, lastp) * 64);
-                        vi[2 * u2] = pr.x;
-                        vi[2 * u2 + 1] = pr.y;
-                    }
-                }
-                if constexpr (LDSX && SELL_IDX2) {
+                if constexpr (LDSX) {
                     const uint32_t *ip = reinterpret_cast<const uint32_t *>(idx) + (ch.off >> 1) + lane;
                     const int lastp = max((ch.width >> 1) - 1, 0);
 #pragma unroll
@@ -306,232 +255,6 @@ __global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__
             if (seg >= 0) {
 #pragma unroll
                 for (int k = 0; k < OC; ++k) o[(int64_t) k * nseg + seg] = acc[k];
-            }
-        }
-        cb = ce;
-    }
-}
-
-// ---- software-pipelined walk (round 5, PLSSVM_MI_SELL_PIPE) ------------------------------------------------
-// The same chunks, entries, products and summation order as sell_spmv_kernel (LDS panels, paired 16-bit indices,
-// real values or paired FP22 words) — bit for bit its results — but a wave issues the loads of its next step (the
-// chunk's next SU entries, or the first SU entries of its next chunk) before it consumes the current one, so its
-// loads stay in flight through the gathers, the products and the chunk switch. Two register sets (A, B) alternate
-// (the loop body is written twice: no copies between them, so no wait for the next loads at the loop's end); the
-// chunk descriptors and slot maps of the next chunk are vector loads issued a chunk ahead (a scalar load would share
-// the LDS counter and stall the gathers). A finished wave's last prefetch re-reads its own chunk (cached, discarded).
-// Measured (round 5, one box, profiles/r05_sell_pipe_ab.json): bitwise the plain walk's results, and no faster —
-// config 3 7 159 vs 7 216 CG it/s, 3-RBF 1 055 vs 1 059, config 5 845 vs 846 (the ISA shows the next step's loads in
-// flight through the consume for the real-valued passes): the passes are not bound by a wave's load latency. Off by
-// default; kept as the measured alternative.
-#ifndef PLSSVM_MI_SELL_PIPE
-#define PLSSVM_MI_SELL_PIPE 0
-#endif
-template <typename T, bool F22>
-struct sell_pipe_regs {
-    static constexpr int SU = sell_unroll<F22>(), SU2 = SU / 2;
-    uint32_t ip[SU2];                                  // paired 16-bit panel indices
-    u32x3_a4 vw[F22 ? SU2 : 1];                        // FP22: the 3 words holding an entry pair
-    T v[F22 ? 1 : SU];                                 // real values
-    int seg;                                           // the step's chunk's slot map (loaded with its entries)
-};
-
-template <typename T, bool F22, int KC = 1, int MODE = 0>
-__global__ __launch_bounds__(SELL_NT) void sell_spmv_pipe_kernel(const sell_chunk *__restrict__ chunks,
-                                                                 const int32_t *__restrict__ perm,
-                                                                 const uint16_t *__restrict__ idx, vals_t<T> val,
-                                                                 const int32_t *__restrict__ bchunk,
-                                                                 const T *__restrict__ x, int64_t xn, int64_t W,
-                                                                 int64_t nseg, int nchp, T *__restrict__ out,
-                                                                 const cg_scalars<T> *__restrict__ status) {
-    static_assert(SELL_IDX2 && !SELL_VAL2 && (!F22 || SELL_F22PAIR), "the pipelined walk covers the default layouts");
-    constexpr int XC = MODE == 2 ? KC : 1;
-    constexpr int OC = MODE == 1 ? KC : 1;
-    constexpr int XW = sell_width<T>();
-    constexpr int SU = sell_unroll<F22>(), SU2 = SU / 2;
-    using R = sell_pipe_regs<T, F22>;
-    __shared__ T xs[XW];
-    if (status != nullptr && status->converged) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int blk = (int) xcd_remap(blockIdx.x, gridDim.x);
-    const int c0 = bchunk[blk], c1 = bchunk[blk + 1];
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t *ip32 = reinterpret_cast<const uint32_t *>(idx);
-    // a chunk descriptor through the vector memory path (in order with the step loads; see above)
-    auto desc = [&](int c) -> sell_chunk {
-        int cv = c;
-        asm volatile("" : "+v"(cv));
-        return chunks[cv];
-    };
-    // the streams through buffer descriptors (host-checked: < 2^31 bytes each): every per-step offset is a scalar
-    // (soffset), the lanes' offsets constants — no per-load vector address arithmetic. Paired FP22 chunks start at
-    // multiples of 128 entries, so entry pair p = off + 128 pj + 2 lane starts at bit 22 (off + 128 pj) (a word
-    // boundary) + 44 lane: word 11 (off + 128 pj) / 16 + (44 lane) / 32, shift (44 lane) % 32, per-lane constants
-    const __amdgpu_buffer_rsrc_t rs_ip = __builtin_amdgcn_make_buffer_rsrc((void *) ip32, (short) 0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc(
-        F22 ? (void *) val.v22 : (void *) val.v, (short) 0, 0x7FFFFFFF, 0x00020000);
-    const int vo_ip = 4 * lane, vo_v = F22 ? 4 * ((44 * lane) >> 5) : (int) sizeof(T) * lane;
-    const int sh0 = (44 * lane) & 31;
-    auto load = [&](R &r, int64_t off, int width, int j) {
-        const int lastp = max((width >> 1) - 1, 0);
-#pragma unroll
-        for (int u2 = 0; u2 < SU2; ++u2) {
-            const int64_t pj = min((j >> 1) + u2, lastp);
-            r.ip[u2] = __builtin_amdgcn_raw_buffer_load_b32(rs_ip, vo_ip, (int) (4 * ((off >> 1) + pj * 64)), 2);
-            if constexpr (F22) {
-                const auto w3 = __builtin_amdgcn_raw_buffer_load_b96(rs_v, vo_v, (int) (4 * (11 * (off + 128 * pj) / 16)), 2);
-                r.vw[u2] = u32x3_a4{ w3[0], w3[1], w3[2] };
-            }
-        }
-        if constexpr (!F22) {
-            const int last = max(width - 1, 0);
-#pragma unroll
-            for (int u = 0; u < SU; ++u) {
-                const int so = (int) (sizeof(T) * (off + (int64_t) min(j + u, last) * 64));
-                if constexpr (sizeof(T) == 4) {
-                    r.v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, vo_v, so, 2));
-                } else {
-                    const auto d2 = __builtin_amdgcn_raw_buffer_load_b64(rs_v, vo_v, so, 2);
-                    r.v[u] = __longlong_as_double((long long) (((uint64_t) d2[1] << 32) | d2[0]));
-                }
-            }
-        }
-    };
-    for (int cb = c0; cb < c1;) {
-        const int q = chunks[cb].q;
-        const int ce = min(c1, (q + 1) * nchp);
-        T *o = out + (int64_t) q * nseg * OC;
-        {
-            if (cb != c0) __syncthreads();
-            const T *xg = x + (int64_t) q * W * XC;
-            const int xl = (int) min((int64_t) W, xn - (int64_t) q * W) * XC;
-            using V = __attribute__((ext_vector_type(4))) float;
-            constexpr int EV = 16 / (int) sizeof(T);
-            constexpr int VPER = XW / EV / SELL_NT;
-            static_assert(VPER * EV * SELL_NT == XW, "panel width must be a multiple of 16 B per thread");
-            if (xl == XW && (reinterpret_cast<uintptr_t>(xg) & 15) == 0) {
-                V t[VPER];
-#pragma unroll
-                for (int u = 0; u < VPER; ++u) t[u] = reinterpret_cast<const V *>(xg)[tid + u * SELL_NT];
-#pragma unroll
-                for (int u = 0; u < VPER; ++u) reinterpret_cast<V *>(xs)[tid + u * SELL_NT] = t[u];
-            } else {
-                constexpr int XPER = XW / SELL_NT;
-                for (int u = 0; u < XPER; ++u) {
-                    const int k = tid + u * SELL_NT;
-                    xs[k] = k < xl ? xg[k] : T(0);
-                }
-            }
-            __syncthreads();
-        }
-        const int cw0 = cb + wave;
-        const int nk = cw0 < ce ? (ce - cw0 + SELL_WAVES - 1) / SELL_WAVES : 0;  // this wave's chunks of the panel
-        if (nk > 0) {
-            // the wave's chunk descriptors, lane l holding its chunk l (+ 64 b): read with v_readlane at a chunk switch,
-            // so the walk issues no descriptor load (a wave with more than 64 chunks reloads them, rarely)
-            int64_t dl_off = 0;
-            int dl_w = 0;
-            auto batch = [&](int b) {
-                const int k = b * 64 + lane;
-                const sell_chunk d = k < nk ? chunks[cw0 + SELL_WAVES * k] : sell_chunk{ 0, 0, 0 };
-                dl_off = d.off;
-                dl_w = d.width;
-            };
-            auto rl64 = [](int64_t v, int l) -> int64_t {
-                const uint32_t lo = __builtin_amdgcn_readlane((uint32_t) v, l);
-                const uint32_t hi = __builtin_amdgcn_readlane((uint32_t) ((uint64_t) v >> 32), l);
-                return (int64_t) (((uint64_t) hi << 32) | lo);
-            };
-            batch(0);
-            int k = 0;  // the current chunk: cw0 + 16 k
-            int64_t ch_off = rl64(dl_off, 0);
-            int ch_w = __builtin_amdgcn_readlane(dl_w, 0);
-            int64_t nx_off = ch_off;  // the next chunk (itself when there is none; its step re-reads are discarded)
-            int nx_w = ch_w;
-            if (nk > 1) {
-                nx_off = rl64(dl_off, 1);
-                nx_w = __builtin_amdgcn_readlane(dl_w, 1);
-            }
-            R ra, rb;
-            ra.seg = perm[(int64_t) cw0 * 64 + lane];
-            load(ra, ch_off, ch_w, 0);
-            int j = 0;
-            T acc[OC];
-#pragma unroll
-            for (int kk = 0; kk < OC; ++kk) acc[kk] = T(0);
-            auto step = [&](const R &cur, R &nxt) -> bool {
-                const int w = ch_w;
-                const bool last = j + SU >= w;
-                // every step issues the same loads (no merge of load paths, so the compiler's wait counts stay exact):
-                // the next step's entries (selected position) and its chunk's slot map
-                const int kn = last && k + 1 < nk ? k + 1 : k;
-                nxt.seg = perm[(int64_t) (cw0 + SELL_WAVES * kn) * 64 + lane];
-                load(nxt, last ? nx_off : ch_off, last ? nx_w : w, last ? 0 : j + SU);
-                // consume the current step (sell_spmv_kernel's arithmetic and order)
-#pragma unroll
-                for (int u2 = 0; u2 < SU2; ++u2) {
-                    T vv[2];
-                    if constexpr (F22) {
-                        const int sh = sh0;
-                        const u32x3_a4 ww = cur.vw[u2];
-                        const uint64_t lo = ((uint64_t) ww.y << 32) | ww.x;
-                        const uint32_t k0 = (uint32_t) (lo >> sh) & 0x3FFFFFu;
-                        const int sh1 = sh + 22;
-                        const uint64_t hi = ((uint64_t) ww.z << 32) | ww.y;
-                        const uint32_t k1 = (uint32_t) (sh1 >= 32 ? hi >> (sh1 - 32) : lo >> sh1) & 0x3FFFFFu;
-                        vv[0] = (T) fp22_decode(k0);
-                        vv[1] = (T) fp22_decode(k1);
-                    } else {
-                        vv[0] = cur.v[2 * u2];
-                        vv[1] = cur.v[2 * u2 + 1];
-                    }
-                    const uint32_t pr = cur.ip[u2];
-#pragma unroll
-                    for (int t = 0; t < 2; ++t) {
-                        const int u = 2 * u2 + t;
-                        const int64_t ci = t == 0 ? (int64_t) (pr & 0xFFFFu) : (int64_t) (pr >> 16);
-                        const T v = j + u < w ? vv[t] : T(0);
-                        if constexpr (MODE == 0) {
-                            acc[0] = fma(v, xs[ci], acc[0]);
-                        } else if constexpr (MODE == 1) {
-                            T tt = v * xs[ci];
-#pragma unroll
-                            for (int k = 0; k < KC; ++k) {
-                                acc[k] += tt;
-                                tt *= v;
-                            }
-                        } else {
-                            const int64_t cx = ci * KC;
-                            T h = xs[cx + KC - 1];
-#pragma unroll
-                            for (int k = KC - 2; k >= 0; --k) h = fma(h, v, xs[cx + k]);
-                            acc[0] = fma(h, v, acc[0]);
-                        }
-                    }
-                }
-                if (!last) {
-                    j += SU;
-                    return true;
-                }
-                if (cur.seg >= 0) {
-#pragma unroll
-                    for (int kk = 0; kk < OC; ++kk) o[(int64_t) kk * nseg + cur.seg] = acc[kk];
-                }
-#pragma unroll
-                for (int kk = 0; kk < OC; ++kk) acc[kk] = T(0);
-                if (k + 1 >= nk) return false;
-                ++k;
-                j = 0;
-                ch_off = nx_off;
-                ch_w = nx_w;
-                if (k + 1 < nk) {
-                    if (((k + 1) & 63) == 0) batch((k + 1) >> 6);
-                    nx_off = rl64(dl_off, (k + 1) & 63);
-                    nx_w = __builtin_amdgcn_readlane(dl_w, (k + 1) & 63);
-                }
-                return true;
-            };
-            while (step(ra, rb) && step(rb, ra)) {
             }
         }
         cb = ce;
@@ -582,17 +305,7 @@ inline void launch_panel_spmv_t(const spmv_plan<T> &pl, const T *x, int64_t xn, 
     const bool f22 = pl.val22.get() != nullptr;
     T *dst = pl.P > 1 ? pl.partial.get() : out;
     const dim3 grid((unsigned) pl.nblocks), block(SELL_NT);
-    bool done = false;
-    if constexpr (PLSSVM_MI_SELL_PIPE != 0) {
-        if (pl.ldsx) {
-            auto k = f22 ? sell_spmv_pipe_kernel<T, true, KC, MODE> : sell_spmv_pipe_kernel<T, false, KC, MODE>;
-            hipLaunchKernelGGL(k, grid, block, 0, stream, pl.chunks.get(), pl.perm.get(), pl.idx16.get(), pl.vals(),
-                               pl.bchunk.get(), x, xn, pl.W, pl.nseg, (int) pl.nchp, dst, status);
-            done = true;
-        }
-    }
-    if (done) {
-    } else if (pl.ldsx) {
+    if (pl.ldsx) {
         auto k = f22 ? sell_spmv_kernel<T, true, true, KC, MODE> : sell_spmv_kernel<T, true, false, KC, MODE>;
         hipLaunchKernelGGL(k, grid, block, 0, stream, pl.chunks.get(), pl.perm.get(), pl.idx16.get(), pl.vals(),
                            pl.bchunk.get(), x, xn, pl.W, pl.nseg, (int) pl.nchp, dst, status);
@@ -714,7 +427,7 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
                 const int32_t sgm = perm[(size_t) (q * slots_per_panel + c * 64 + l)];
                 if (sgm >= 0) width = std::max(width, lq[sgm]);
             }
-            if (SELL_IDX2 && ldsx) width = (width + 1) & ~1;  // paired indices: even widths, off % 128 == 0
+            if (ldsx) width = (width + 1) & ~1;  // paired indices: even widths, off % 128 == 0
             chunks[(size_t) (q * nch_per_panel + c)] = sell_chunk{ off, width, (int32_t) q };
             for (int l = 0; l < 64; ++l) {
                 const int32_t sgm = perm[(size_t) (q * slots_per_panel + c * 64 + l)];
@@ -745,11 +458,10 @@ void build_spmv_plan(spmv_plan<T> &pl, int64_t nseg, int64_t xn, int64_t nnz, bo
             if (ldsx) {
                 // IDX2: entry j of slot l (value position t = off + 64 j + l) keeps its index at
                 // off + 128 (j >> 1) + 2 l + (j & 1)
-                const int64_t ti = SELL_IDX2 ? sell_pair_pos(t) : t;
-                i16[ti] = (uint16_t) (g - q * W);
+                i16[sell_pair_pos(t)] = (uint16_t) (g - q * W);
             }
             else i32[t] = (int32_t) g;
-            const int64_t tv = ((SELL_VAL2 || (fp22 && SELL_F22PAIR)) && ldsx) ? sell_pair_pos(t) : t;  // value position
+            const int64_t tv = (fp22 && ldsx) ? sell_pair_pos(t) : t;  // value position
             if (fp22) vf[tv] = (float) v;
             else vr[tv] = (T) v;
         }, s0, s1);
@@ -807,15 +519,6 @@ constexpr int rb_rows() { return 16384 / (int) sizeof(T); }  // row accumulator:
 template <typename T>
 constexpr int rb_width() { return (163840 - 16384) / (int) sizeof(T) / 1024 * 1024; }  // panel: the rest
 
-// PLSSVM_MI_ROWBLOCK=0 disables the fused row-block pass (measurements)
-inline bool rowblock_fused_enabled() {
-    static const bool on = [] {
-        const char *e = std::getenv("PLSSVM_MI_ROWBLOCK");
-        return e == nullptr || std::atoi(e) != 0;
-    }();
-    return on;
-}
-
 template <typename T>
 struct rb_plan {
     int64_t P = 0, W = 0, RBK = 0, nblk = 0, nrows = 0, entries = 0;
@@ -835,96 +538,15 @@ struct rb_plan {
     }
 };
 
-// The rest of a CG iteration carried by the row-block pass (round 5, one GPU, non-reset iterations): after the
-// finalize, a grid barrier, then every block sums the d.Ad partials (dot_final's order), forms alpha and updates x, r
-// of its own rows (Ad and d still in registers: no Ad round trip), a second barrier, then every block sums the r.r
-// partials, takes the stop test / beta and updates d of its rows with the sum d / sum q d partials — cg_upd_rr and
-// cg_dir_sums_kernel's arithmetic (products rounded before the adds), two launches and 20 MB of vector traffic fewer.
-// The blocks are all resident (one per CU, grid <= the CUs, checked on the host); each barrier's wait is bounded:
-// past ~0.2 s a block sets the timeout flag and leaves (the host then reports the failure instead of hanging).
-// Measured (round 5, config 3, one box, profiles/r05_rowblock_cg_ab.json): with this light barrier 0.139 ms per CG
-// iteration, equal to the three launches (fenced two-level barrier 0.156 ms, one-level 0.176 ms) — the 20 MB saved pay
-// for the two barriers and no more; results within the CG-trace tests' bars. Off by default (PLSSVM_MI_RB_CG=1).
-template <typename T>
-struct rb_cg_args {
-    T *xv = nullptr, *rv = nullptr, *dw = nullptr;  // x, r, d (d written by the direction update)
-    T *prr = nullptr, *psum_out = nullptr;           // r.r partials, sum d / sum q d partials (RED_BLOCKS layout)
-    cg_scalars<T> *sc = nullptr;
-    double *trace = nullptr;
-    int64_t trace_cap = 0;
-    unsigned *bar = nullptr;  // RBB_WORDS: group counters, root counter, generation, timeout flag
-};
-
-// grid barrier of nb resident blocks, two levels: blocks arrive on one of RBB_G group counters (block b on b % RBB_G,
-// each counter on its own 64-byte line), the last of a group on the root counter, the last of all bumps the
-// generation — one same-address atomic chain of 256 device-scope adds measured ~20 us per barrier, 16 + 16 far less.
-// False when the wait timed out (bar[RBB_FLAG] set).
-constexpr int RBB_G = 16, RBB_STRIDE = 16, RBB_ROOT = RBB_G * RBB_STRIDE, RBB_GEN = RBB_ROOT + RBB_STRIDE,
-              RBB_FLAG = RBB_GEN + RBB_STRIDE, RBB_WORDS = RBB_FLAG + RBB_STRIDE;
-// Light form (no L2 write-back / invalidate): everything one block hands to another inside the kernel — the d.Ad and
-// r.r partials — is written and read with agent-scope atomic stores / loads (sc1: at the coherence point, past every
-// XCD's L2), every wave waits for its stores before the barrier, and the counters are agent-scope atomics; the
-// vectors each block reads and writes are its own rows (kernel boundaries order them for the next launch).
-template <typename T>
-__device__ __forceinline__ void rb_st(T *p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ T rb_ld(const T *p) {
-    return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename S>
-__device__ __forceinline__ bool rb_grid_sync(unsigned *bar, unsigned nb, S *ok_s) {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's partial stores have reached the coherence point
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int ok = 1;
-        const unsigned ng = nb < (unsigned) RBB_G ? nb : (unsigned) RBB_G;
-        const unsigned gi = blockIdx.x % ng, gsize = (nb - gi + ng - 1) / ng;
-        const unsigned g = __hip_atomic_load(bar + RBB_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        bool last = false;
-        if (__hip_atomic_fetch_add(bar + gi * RBB_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
-            __hip_atomic_store(bar + gi * RBB_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            __builtin_amdgcn_s_waitcnt(0);
-            if (__hip_atomic_fetch_add(bar + RBB_ROOT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
-                __hip_atomic_store(bar + RBB_ROOT, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                __builtin_amdgcn_s_waitcnt(0);  // the counters are reset before anyone can arrive again
-                __hip_atomic_fetch_add(bar + RBB_GEN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                last = true;
-            }
-        }
-        if (!last) {
-            const uint64_t t0 = wall_clock64();  // constant rate (100 MHz on MI355X)
-            while (__hip_atomic_load(bar + RBB_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-                __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - t0 > 20000000ull) {
-                    ok = 0;
-                    __hip_atomic_store(bar + RBB_FLAG, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-            }
-        }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        *ok_s = S(ok);
-    }
-    __syncthreads();
-    return *ok_s != S(0);
-}
-
-template <typename T, bool F22, bool CG = false>
+template <typename T, bool F22>
 __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
     const sell_chunk *__restrict__ chunks, const int32_t *__restrict__ perm, const uint16_t *__restrict__ idx,
     vals_t<T> val, const int32_t *__restrict__ bpc, int64_t P, int64_t W, int64_t RBK, const T *__restrict__ x,
     int64_t xn, int64_t nrows, const T *__restrict__ q, const T *__restrict__ d, const T *__restrict__ psum,
-    T QA_cost, T cost_inv, T *__restrict__ Ad, T *__restrict__ pdad, const cg_scalars<T> *__restrict__ status,
-    rb_cg_args<T> cg = {}) {
+    T QA_cost, T cost_inv, T *__restrict__ Ad, T *__restrict__ pdad, const cg_scalars<T> *__restrict__ status) {
     constexpr int XW = rb_width<T>(), RB = rb_rows<T>();
     constexpr int SU = sell_unroll<F22>();
-    constexpr int RPT = (RB + SELL_NT - 1) / SELL_NT;  // rows per thread (CG: kept in registers)
+    constexpr int RPT = (RB + SELL_NT - 1) / SELL_NT;  // rows per thread
     __shared__ T xs[XW];
     __shared__ T racc[RB];
     T *red = racc, *bc = racc + SELL_WAVES;  // block-reduction scratch (before / after the accumulator's use)
@@ -1012,7 +634,6 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
     }
     __syncthreads();
     T s1 = 0;
-    T avr[CG ? RPT : 1], dvr[CG ? RPT : 1], qvr[CG ? RPT : 1];
 #pragma unroll
     for (int u = 0; u < RPT; ++u) {
         const int t = tid + u * SELL_NT;
@@ -1025,11 +646,7 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
             v = rw + (QA_cost - qi) * sp - sqp + cost_inv * di;
             v = T(0) + T(1) * v;
         }
-        if constexpr (CG) {
-            avr[u] = v, dvr[u] = di, qvr[u] = qi;
-        } else {
-            Ad[i] = v;
-        }
+        Ad[i] = v;
         s1 += di * v;
     }
 #pragma unroll
@@ -1040,93 +657,11 @@ __global__ __launch_bounds__(SELL_NT) void sell_rowblock_fin_kernel(
     if (tid == 0) {
         T t = 0;
         for (int w2 = 0; w2 < SELL_WAVES; ++w2) t += red[w2];
-        if constexpr (CG) {
-            rb_st(pdad + blk, t);
-            pdad[RED_BLOCKS + blk] = T(0);
-        } else {
-            pdad[blk] = t;
-        }
+        pdad[blk] = t;
     }
     // the consumer sums RED_BLOCKS partials: the slots past this launch's blocks are zero
     if (blk == 0)
-        for (int b = (int) gridDim.x + tid; b < RED_BLOCKS; b += SELL_NT) {
-            if constexpr (CG) {
-                rb_st(pdad + b, T(0));
-                pdad[RED_BLOCKS + b] = T(0);
-            } else {
-                pdad[b] = T(0);
-            }
-        }
-    if constexpr (CG) {
-#pragma clang fp contract(off)  // cg_upd_rr / cg_dir_sums: products rounded before the adds
-        const unsigned nb = gridDim.x;
-        T *red2 = racc + 2 * SELL_WAVES, *bc2 = racc + 3 * SELL_WAVES, *ok_s = racc + 4 * SELL_WAVES;  // scratch
-        auto total = [&](const T *parts) {  // partials_total1: the RED_BLOCKS partials in dot_final's order
-            T a = 0;
-            for (int i2 = tid; i2 < RED_BLOCKS; i2 += SELL_NT) a += rb_ld(parts + i2);
-            return cgk::block_sum_all(a, red2, bc2);
-        };
-        if (!rb_grid_sync(cg.bar, nb, ok_s)) return;
-        // cg_upd_rr_kernel: alpha = delta / d.Ad; x += alpha d; r -= alpha Ad; r.r partials
-        const T dAd = total(pdad);
-        const T delta = cg.sc->delta;
-        const T alpha = delta / dAd;
-        if (blk == 0 && tid == 0) cg.sc->dAd = dAd, cg.sc->alpha = alpha, cg.sc->delta_prev = delta;
-        T rnr[RPT];
-        T srr = 0;
-#pragma unroll
-        for (int u = 0; u < RPT; ++u) {
-            const int t = tid + u * SELL_NT;
-            if (t >= rows) break;
-            const int64_t i = row0 + t;
-            const T xi = cg.xv[i], ri = cg.rv[i];
-            const T tx = alpha * dvr[u];
-            cg.xv[i] = xi + tx;
-            const T ua = alpha * avr[u];
-            const T rn = ri - ua;
-            cg.rv[i] = rn;
-            rnr[u] = rn;
-            srr += rn * rn;
-        }
-        {
-            const T b1 = cgk::block_sum(srr, red2);
-            if (tid == 0) rb_st(cg.prr + blk, b1), cg.prr[RED_BLOCKS + blk] = T(0);
-            if (blk == 0)
-                for (int b = (int) nb + tid; b < RED_BLOCKS; b += SELL_NT) rb_st(cg.prr + b, T(0)), cg.prr[RED_BLOCKS + b] = T(0);
-        }
-        if (!rb_grid_sync(cg.bar, nb, ok_s)) return;
-        // cg_dir_sums_kernel: delta = r.r, stop test, beta; d = beta d + r; sum d / sum q d partials
-        const T rr = total(cg.prr);
-        const bool conv = rr <= cg.sc->eps2delta0;
-        const T beta = rr / delta;  // = sc->delta_prev (written by block 0 above)
-        if (blk == 0 && tid == 0) {
-            const int64_t run = cg.sc->iters;
-            cg.sc->delta = rr;
-            cg.sc->iters = run + 1;
-            if (cg.trace && run + 1 < cg.trace_cap) cg.trace[run + 1] = (double) rr;
-            if (conv) cg.sc->converged = 1;
-            else cg.sc->beta = beta;
-        }
-        if (conv) return;  // the same decision in every block
-        T sd = 0, sqd = 0;
-#pragma unroll
-        for (int u = 0; u < RPT; ++u) {
-            const int t = tid + u * SELL_NT;
-            if (t >= rows) break;
-            const int64_t i = row0 + t;
-            const T tb = beta * dvr[u];
-            const T dn = tb + rnr[u];
-            cg.dw[i] = dn;
-            sd += dn;
-            sqd += qvr[u] * dn;
-        }
-        const T b1 = cgk::block_sum(sd, red2);
-        __syncthreads();
-        const T b2 = cgk::block_sum(sqd, red2);
-        if (tid == 0) cg.psum_out[blk] = b1, cg.psum_out[RED_BLOCKS + blk] = b2;
-        if (blk == 0)
-            for (int b = (int) nb + tid; b < RED_BLOCKS; b += SELL_NT) cg.psum_out[b] = T(0), cg.psum_out[RED_BLOCKS + b] = T(0);
-    }
+        for (int b = (int) gridDim.x + tid; b < RED_BLOCKS; b += SELL_NT) pdad[b] = T(0);
 }
 
 template <typename T>
@@ -1137,19 +672,7 @@ inline void launch_rowblock_fin(const rb_plan<T> &pl, const T *w, int64_t xn, co
     auto k = pl.val22.get() ? sell_rowblock_fin_kernel<T, true> : sell_rowblock_fin_kernel<T, false>;
     hipLaunchKernelGGL(k, dim3((unsigned) pl.nblk), dim3(SELL_NT), 0, stream, pl.chunks.get(), pl.perm.get(),
                        pl.idx16.get(), pl.vals(), pl.bpc.get(), pl.P, pl.W, pl.RBK, w, xn, pl.nrows, q, d, psum,
-                       QA_cost, cost_inv, Ad, pdad, status, rb_cg_args<T>{});
-    MI_LAUNCH_CHECK();
-}
-
-// the row-block pass carrying the iteration's x / r and direction updates (sell_rowblock_fin_kernel<..., true>)
-template <typename T>
-inline void launch_rowblock_cg(const rb_plan<T> &pl, const T *w, int64_t xn, const T *q, const T *d, const T *psum,
-                               T QA_cost, T cost_inv, T *pdad, const rb_cg_args<T> &cg, hipStream_t stream) {
-    if (pl.nblk <= 0) return;
-    auto k = pl.val22.get() ? sell_rowblock_fin_kernel<T, true, true> : sell_rowblock_fin_kernel<T, false, true>;
-    hipLaunchKernelGGL(k, dim3((unsigned) pl.nblk), dim3(SELL_NT), 0, stream, pl.chunks.get(), pl.perm.get(),
-                       pl.idx16.get(), pl.vals(), pl.bpc.get(), pl.P, pl.W, pl.RBK, w, xn, pl.nrows, q, d, psum,
-                       QA_cost, cost_inv, (T *) nullptr, pdad, cg.sc, cg);
+                       QA_cost, cost_inv, Ad, pdad, status);
     MI_LAUNCH_CHECK();
 }
 

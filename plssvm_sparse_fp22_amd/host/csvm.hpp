@@ -8,14 +8,17 @@
 // writes the LIBSVM model format of csvm.cpp:60-204.
 #pragma once
 
+#include <algorithm>
 #include <charconv>
 #include <cmath>
 #include <cstdio>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "../../include/plssvm_mi355x.h"
+#include "../../include/plssvm_mi355x_group.hpp"
 #include "csvm_interface.hpp"
 #include "parameter.hpp"
 
@@ -34,32 +37,66 @@ class csvm : public csvm_interface<T> {
     using real_type = T;
     using base::learn;  // learn() (imax = num_features) and learn(imax)
 
-    explicit csvm(const parameter<T> &params, int device = 0) : base(params) {
-        const int rc = plssvm_mi_create((int) sizeof(T), (int) this->kernel_, this->degree_, (double) this->gamma_,
-                                        (double) this->coef0_, (double) this->cost_, device, &ctx_);
-        if (rc != PLSSVM_MI_OK) throw backend_exception(rc, plssvm_mi_last_error(nullptr));
+    // hip::csvm<T>(params) (src/plssvm/backends/HIP/csvm.hip.cpp:38-81): every visible GPU of the node, one host
+    // thread and one context per GPU in a row-block group (RCCL), at most one GPU per row of the m = N - 1 rows
+    explicit csvm(const parameter<T> &params) : csvm(params, all_devices(params)) {}
+    // one GPU (plssvm-train --device N)
+    csvm(const parameter<T> &params, int device) : csvm(params, std::vector<int>{ device }) {}
+    // an explicit device list; a device listed twice forms the group over the in-process host exchange
+    // (device_group: two contexts on one GPU, which RCCL refuses — the multi-rank path's test transport)
+    csvm(const parameter<T> &params, const std::vector<int> &devices,
+         device_group::transport tr = device_group::transport::automatic) :
+        base(params) {
+        try {
+            grp_ = std::make_unique<device_group>(devices, (int) sizeof(T), (int) this->kernel_, this->degree_,
+                                                  (double) this->gamma_, (double) this->coef0_, (double) this->cost_, tr);
+        } catch (const group_error &e) {
+            throw backend_exception(e.code, e.what());
+        }
     }
-    ~csvm() override { plssvm_mi_destroy(ctx_); }
 
-    // one process per GPU: join a row-block group before setup (rank 0 creates the id)
-    void join_group(int rank, int world, const void *unique_id) { check(plssvm_mi_comm_init(ctx_, rank, world, unique_id)); }
+    // the visible GPUs the default constructor takes: min(#GPUs, m), like the reference's min(#GPUs, #features)
+    // feature split (csvm.hip.cpp:53-55), here over rows
+    static std::vector<int> all_devices(const parameter<T> &params) {
+        const int n = plssvm_mi_device_count();
+        if (n <= 0) throw backend_exception(PLSSVM_MI_ERR_NODEV, "HIP backend selected but no HIP devices were found!");
+        const int64_t m = std::max<int64_t>(params.num_data_points - 1, 1);
+        std::vector<int> d((size_t) std::min<int64_t>(n, m));
+        for (size_t k = 0; k < d.size(); ++k) d[k] = (int) k;
+        return d;
+    }
+    int num_devices() const { return grp_->size(); }
+    const std::vector<int> &devices() const { return grp_->devices(); }
+
+    // one process per GPU instead (MPI / torch launchers): a one-device csvm joins a row-block group before setup
+    // (rank 0 creates the id)
+    void join_group(int rank, int world, const void *unique_id) {
+        if (grp_->size() != 1) throw exception{ "join_group needs a one-device csvm" };
+        on_all([&](int, plssvm_mi_ctx *c) { return plssvm_mi_comm_init(c, rank, world, unique_id); });
+    }
 
     // ---- the reference's pure virtuals (csvm.hpp:188-214), public here like mock_hip_csvm's hooks ----
+    // every call runs on all ranks at once (their collectives meet inside the library); outputs come from rank 0
     void setup_data_on_device() override {
         const auto &p = this->params_;
-        if (p.sparse) {
-            const bool f22 = !p.val22.empty() && sizeof(T) == 4;  // packed FP22 input stays packed
-            check(plssvm_mi_setup_csr(ctx_, p.rowptr.data(), p.col.data(), f22 ? (const void *) p.val22.data() : p.val.data(),
-                                      f22 ? PLSSVM_MI_VAL_FP22 : PLSSVM_MI_VAL_REAL, p.num_data_points, p.num_features));
-        } else {
-            check(plssvm_mi_setup_dense(ctx_, p.dense.data(), p.num_data_points, p.num_features));
-        }
+        on_all([&](int, plssvm_mi_ctx *c) {
+            if (p.sparse) {
+                const bool f22 = !p.val22.empty() && sizeof(T) == 4;  // packed FP22 input stays packed
+                return plssvm_mi_setup_csr(c, p.rowptr.data(), p.col.data(), f22 ? (const void *) p.val22.data() : p.val.data(),
+                                           f22 ? PLSSVM_MI_VAL_FP22 : PLSSVM_MI_VAL_REAL, p.num_data_points, p.num_features);
+            }
+            return plssvm_mi_setup_dense(c, p.dense.data(), p.num_data_points, p.num_features);
+        });
         on_device_ = true;
     }
     [[nodiscard]] std::vector<T> generate_q() override {
-        std::vector<T> q(std::max<std::size_t>(this->num_data_points_ - 1, 1));
-        double qa = 0;
-        check(plssvm_mi_generate_q(ctx_, q.data(), &qa));
+        const size_t len = std::max<std::size_t>(this->num_data_points_ - 1, 1);
+        std::vector<T> q(len);
+        auto sc = scratch(len);
+        on_all([&](int r, plssvm_mi_ctx *c) {
+            double qa = 0;
+            return plssvm_mi_generate_q(c, r == 0 ? q.data() : sc[(size_t) r].data(), &qa);
+        });
         q.resize(this->num_data_points_ - 1);
         return q;
     }
@@ -68,16 +105,27 @@ class csvm : public csvm_interface<T> {
     // "Done in" time of an iteration is its batch's wall time / iterations (the device runs a batch
     // without host round trips), truncated to ms like the reference's duration_cast
     std::vector<T> solver_CG(const std::vector<T> &b, std::size_t imax, T eps, const std::vector<T> &q) override {
-        check(plssvm_mi_set_qa_cost(ctx_, (double) this->QA_cost_));  // learn() computed it on the host
-        std::vector<T> x(std::max<std::size_t>(b.size(), 1));
-        trace_.assign(imax + 1, 0.0);
-        int64_t it = 0;
+        const size_t len = std::max<std::size_t>(b.size(), 1);
+        std::vector<T> x(len);
+        auto sc = scratch(len);
+        std::vector<std::vector<double>> tr((size_t) grp_->size(), std::vector<double>(imax + 1, 0.0));
+        std::vector<int64_t> its((size_t) grp_->size(), 0);
         progress_state ps{ (int64_t) imax, 0.0, 0.0, 0 };
-        if (this->print_info_) check(plssvm_mi_set_progress(ctx_, &csvm::print_progress, &ps));
-        const int rc = plssvm_mi_solve_cg(ctx_, b.data(), q.data(), (int64_t) imax, (double) eps, x.data(), trace_.data(), &it);
-        if (this->print_info_) (void) plssvm_mi_set_progress(ctx_, nullptr, nullptr);
-        check(rc);
+        on_all([&](int r, plssvm_mi_ctx *c) {
+            int rc = plssvm_mi_set_qa_cost(c, (double) this->QA_cost_);  // learn() computed it on the host
+            if (rc != PLSSVM_MI_OK) return rc;
+            if (this->print_info_ && r == 0) {
+                rc = plssvm_mi_set_progress(c, &csvm::print_progress, &ps);
+                if (rc != PLSSVM_MI_OK) return rc;
+            }
+            rc = plssvm_mi_solve_cg(c, b.data(), q.data(), (int64_t) imax, (double) eps, r == 0 ? x.data() : sc[(size_t) r].data(),
+                                    tr[(size_t) r].data(), &its[(size_t) r]);
+            if (this->print_info_ && r == 0) (void) plssvm_mi_set_progress(c, nullptr, nullptr);
+            return rc;
+        });
+        const int64_t it = its[0];
         iterations_ = it;
+        trace_ = std::move(tr[0]);
         trace_.resize((std::size_t) it + 1);
         x.resize(b.size());
         if (this->print_info_) {
@@ -92,8 +140,13 @@ class csvm : public csvm_interface<T> {
     // gpu_csvm::update_w (gpu_csvm.cpp:327-350): w_ = sum_i alpha_i x_i (linear model vector)
     void update_w() override {
         need_model();
-        this->w_.assign(std::max<std::size_t>(this->num_features_, 1), T(0));
-        check(plssvm_mi_update_w(ctx_, this->alpha_ptr_->data(), this->w_.data()));
+        const size_t len = std::max<std::size_t>(this->num_features_, 1);
+        this->w_.assign(len, T(0));
+        auto sc = scratch(len);
+        const T *alpha = this->alpha_ptr_->data();
+        on_all([&](int r, plssvm_mi_ctx *c) {
+            return plssvm_mi_update_w(c, alpha, r == 0 ? this->w_.data() : sc[(size_t) r].data());
+        });
         this->w_.resize(this->num_features_);
     }
     // gpu_csvm::predict (gpu_csvm.cpp:52-127): decision values bias + sum_i alpha_i k(x_i, z) of dense points
@@ -107,21 +160,28 @@ class csvm : public csvm_interface<T> {
             Z.insert(Z.end(), z.begin(), z.end());
         }
         std::vector<T> out(points.size());
-        check(plssvm_mi_predict_dense(ctx_, this->alpha_ptr_->data(), (double) this->bias_, Z.data(), (int64_t) points.size(),
-                                      (int64_t) points[0].size(), out.data()));
+        auto sc = scratch(points.size());
+        const T *alpha = this->alpha_ptr_->data();
+        on_all([&](int r, plssvm_mi_ctx *c) {
+            return plssvm_mi_predict_dense(c, alpha, (double) this->bias_, Z.data(), (int64_t) points.size(),
+                                           (int64_t) points[0].size(), r == 0 ? out.data() : sc[(size_t) r].data());
+        });
         return out;
     }
 
     // ---- run_device_kernel + the mock_hip_csvm setters (tests/backends/HIP/mock_hip_csvm.hpp:24-51) ----
     void run_device_kernel(const std::vector<T> &q, std::vector<T> &ret, const std::vector<T> &d, T add) {
-        check(plssvm_mi_kp(ctx_, q.data(), d.data(), ret.data(), (double) add));
+        std::vector<std::vector<T>> rets((size_t) grp_->size(), ret);  // every rank adds into its own copy
+        on_all([&](int r, plssvm_mi_ctx *c) {
+            return plssvm_mi_kp(c, q.data(), d.data(), r == 0 ? ret.data() : rets[(size_t) r].data(), (double) add);
+        });
     }
     void set_cost(T c) {
-        check(plssvm_mi_set_cost(ctx_, (double) c));
+        on_all([&](int, plssvm_mi_ctx *x) { return plssvm_mi_set_cost(x, (double) c); });
         this->cost_ = c;
     }
     void set_QA_cost(T qa) {
-        check(plssvm_mi_set_qa_cost(ctx_, (double) qa));
+        on_all([&](int, plssvm_mi_ctx *x) { return plssvm_mi_set_qa_cost(x, (double) qa); });
         this->QA_cost_ = qa;
     }
 
@@ -181,15 +241,19 @@ class csvm : public csvm_interface<T> {
     // decision values bias + sum_i alpha_i k(sv_i, z) of the points held by `points` (dense or CSR)
     std::vector<T> predict(const parameter<T> &points) {
         need_model();
-        std::vector<T> out((std::size_t) std::max<int64_t>(points.num_data_points, 1));
+        const size_t len = (std::size_t) std::max<int64_t>(points.num_data_points, 1);
+        std::vector<T> out(len);
+        auto sc = scratch(len);
         const T *alpha = this->alpha_ptr_->data();
-        if (points.sparse)
-            check(plssvm_mi_predict_csr(ctx_, alpha, (double) this->bias_, points.rowptr.data(), points.col.data(),
-                                        points.val.data(), PLSSVM_MI_VAL_REAL, points.num_data_points,
-                                        points.num_features, out.data()));
-        else
-            check(plssvm_mi_predict_dense(ctx_, alpha, (double) this->bias_, points.dense.data(), points.num_data_points,
-                                          points.num_features, out.data()));
+        on_all([&](int r, plssvm_mi_ctx *c) {
+            T *o = r == 0 ? out.data() : sc[(size_t) r].data();
+            if (points.sparse)
+                return plssvm_mi_predict_csr(c, alpha, (double) this->bias_, points.rowptr.data(), points.col.data(),
+                                             points.val.data(), PLSSVM_MI_VAL_REAL, points.num_data_points,
+                                             points.num_features, o);
+            return plssvm_mi_predict_dense(c, alpha, (double) this->bias_, points.dense.data(), points.num_data_points,
+                                           points.num_features, o);
+        });
         out.resize((std::size_t) points.num_data_points);
         return out;
     }
@@ -247,10 +311,22 @@ class csvm : public csvm_interface<T> {
         if (this->alpha_ptr_ == nullptr) throw exception{ "No alphas provided for prediction!" };
         if (!on_device_) setup_data_on_device();
     }
-    void check(int rc) const {
-        if (rc != PLSSVM_MI_OK) throw backend_exception(rc, plssvm_mi_last_error(ctx_));
+    // f(rank, ctx) -> PLSSVM_MI_* code on every rank at once; the first failing rank's message is thrown
+    template <typename F>
+    void on_all(F &&f) {
+        try {
+            grp_->run([&](int r, plssvm_mi_ctx *&c) { return f(r, c); });
+        } catch (const group_error &e) {
+            throw backend_exception(e.code, e.what());
+        }
     }
-    plssvm_mi_ctx *ctx_ = nullptr;
+    // host output buffers of the ranks other than 0 (their results equal rank 0's)
+    std::vector<std::vector<T>> scratch(size_t len) const {
+        std::vector<std::vector<T>> v((size_t) grp_->size());
+        for (size_t r = 1; r < v.size(); ++r) v[r].assign(len, T(0));
+        return v;
+    }
+    std::unique_ptr<device_group> grp_;
     std::vector<double> trace_;
     int64_t iterations_ = 0;
     bool on_device_ = false;

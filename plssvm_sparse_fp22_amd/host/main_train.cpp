@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <iostream>
 #include <map>
 #include <string>
@@ -39,7 +40,9 @@ const char *kHelp =
     "      --sparse               keep the data as CSR on the device (MI355X backend addition)\n"
     "      --max_iter arg         maximum CG iterations (default: num_features)\n"
     "      --single               train in single precision (float)\n"
-    "      --device arg           HIP device ordinal (default: 0)\n";
+    "      --device arg           train on this one HIP device (default: every visible device)\n"
+    "      --devices arg          comma-separated device list, one rank per entry (a device listed twice:\n"
+    "                             in-process host exchange instead of RCCL)\n";
 
 template <typename T>
 int train(const cli &c) {
@@ -92,10 +95,29 @@ int train(const cli &c) {
         std::printf("cost: %s\nepsilon: %s\ninput file (data set): '%s'\noutput file (model): '%s'\n\n",
                     csvm<T>::shortest(params.cost).c_str(), csvm<T>::shortest(params.epsilon).c_str(),
                     params.input_filename.c_str(), params.model_filename.c_str());
-        std::printf("Using HIP (MI355X, gfx950) as backend.\n\n");
+        std::printf("Using HIP (MI355X, gfx950) as backend.\n");
     }
-    const int device = c.opt.count("device") ? std::stoi(c.opt.at("device")) : 0;
-    csvm<T> svm(params, device);
+    // hip::csvm<T>(params) takes every visible device (csvm.hip.cpp:53-55): here one rank of a row-block group per
+    // device; --device keeps one, --devices lists them
+    std::vector<int> devs;
+    if (c.opt.count("devices")) {
+        const std::string &l = c.opt.at("devices");
+        for (size_t a = 0; a <= l.size();) {
+            const size_t b = std::min(l.find(',', a), l.size());
+            devs.push_back(std::stoi(l.substr(a, b - a)));
+            a = b + 1;
+        }
+    } else if (c.opt.count("device")) {
+        devs.push_back(std::stoi(c.opt.at("device")));
+    } else {
+        devs = csvm<T>::all_devices(params);
+    }
+    csvm<T> svm(params, devs);
+    if (params.print_info) {
+        std::printf("Found %d HIP device(s):\n", svm.num_devices());
+        for (const int d : svm.devices()) std::printf("  [%d, gfx950]\n", d);
+        std::printf("\n");
+    }
     // learn() prints the reference's setup line, one line per CG iteration and the solve summary
     // (csvm.cpp:226-266, OpenMP/csvm.cpp:115-117,161-166)
     if (c.opt.count("max_iter")) svm.learn((std::size_t) std::stoll(c.opt.at("max_iter")));

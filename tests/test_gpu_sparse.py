@@ -138,22 +138,6 @@ def test_sparse_onthefly_ragged_and_linear_pairwise(oracle):
     check_sparse_kp(oracle, csr, "linear", np.float64, mode="pairwise", algo="onthefly")
 
 
-def test_sparse_onthefly_windows_over_launches(monkeypatch):
-    """PLSSVM_MI_OTF_WPL: the partner windows split over several launches (row sums carried in fp64 between
-    them) give the one-launch K·p to rounding"""
-    csr, _ = datagen.sparse_csr(9000, 3000, 25, seed=13, dtype=np.float64)
-    m = csr[3] - 1
-    x = np.linspace(1, 2, m)
-    outs = []
-    for wpl in ("0", "3"):
-        monkeypatch.setenv("PLSSVM_MI_OTF_WPL", wpl)
-        svm = sparse_svm(csr, "rbf", np.float64, algo="onthefly")
-        svm.setup_data_on_device()
-        outs.append(svm.kp_part(x, "kernel"))
-        svm.close()
-    np.testing.assert_allclose(outs[1], outs[0], rtol=1e-13, atol=1e-13 * np.abs(outs[0]).max())
-
-
 @pytest.mark.parametrize("world", [2, 3])
 def test_sparse_onthefly_simulated_ranks(world):
     """rank shares (rows split) sum to the single-rank K·p"""
@@ -274,17 +258,14 @@ def test_sparse_densified_learn_and_fp22(oracle):
     assert info["sparse_algo"] == pm._abi.SPARSE_DENSE
 
 
-@pytest.mark.parametrize("runs", ["0", "1"])
 @pytest.mark.parametrize("rbb,groups", [("4096", "1"), ("8192", "1"), ("32768", "1"), ("4096", "2"), ("8192", "3")])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_sparse_expansion_stream_geometries(oracle, rbb, groups, dtype, runs, monkeypatch):
+def test_sparse_expansion_stream_geometries(oracle, rbb, groups, dtype, monkeypatch):
     """every remainder-stream geometry (rows per block / window width, PLSSVM_MI_EXP_RBB; window groups
-    with partial row sums, PLSSVM_MI_EXP_G) in both layouts (PLSSVM_MI_EXP_RUNS: 4-slot chunks with a row
-    per chunk / flagged runs with dummies for rows without partners in a window) against the oracle, on
-    data whose multi-feature pairs span several windows and blocks"""
+    with partial row sums, PLSSVM_MI_EXP_G) against the oracle, on data whose multi-feature pairs span
+    several windows and blocks"""
     monkeypatch.setenv("PLSSVM_MI_EXP_RBB", rbb)
     monkeypatch.setenv("PLSSVM_MI_EXP_G", groups)
-    monkeypatch.setenv("PLSSVM_MI_EXP_RUNS", "2" if runs == "1" else "0")
     csr, _ = datagen.sparse_csr(42000, 600, 10, seed=21, dtype=dtype)
     info = check_sparse_kp(oracle, csr, "rbf", dtype, gamma=0.1)
     assert info["sparse_algo"] == pm._abi.SPARSE_EXPANSION and info["pairs"] > 0
@@ -746,49 +727,3 @@ def test_expansion_float_h_equals_fp64_h(shape, monkeypatch):
     mag = np.abs(out["1"][4]) + 2.0 ** -10 * np.abs(out["1"][4]).max()
     dev = np.abs(out["0"][3] - out["1"][3])
     assert np.all(dev <= 2.0 ** -20 * mag + 2.0 ** -22 * np.abs(out["1"][3])), dev.max()
-
-
-def test_cg_direction_update_carrying_w_is_bitwise(monkeypatch):
-    """Round 5: the CG direction update forms the next K·p's w pass (w = e d, its bfloat16 copy, the S partials) in its
-    own element loop (PLSSVM_MI_DIR_W, default on) — the same grid, element order and block reduction as
-    exp_wown_kernel, so a whole learn() (a graph-captured 50-iteration block, the run-49 reset, ten iterations after
-    it) gives the same bits with and without it. (The sharded RCCL form is covered by the one-rank RCCL group tests,
-    bitwise against no group.)"""
-    csr, y = datagen.sparse_csr(6000, 1500, 12, seed=31, dtype=np.float32)
-    out = {}
-    for on in ("1", "0"):
-        monkeypatch.setenv("PLSSVM_MI_DIR_W", on)
-        with sparse_svm(csr, "rbf", np.float32, algo="expansion", y=y, cost=1e4) as svm:
-            svm.params.epsilon = 1e-30
-            svm.setup_data_on_device()
-            assert svm.info()["exp_hbytes"] == 2
-            svm.learn(imax=60)
-            out[on] = (np.asarray(svm.trace, np.float64), svm.alpha.copy(), svm.iters)
-    assert out["1"][2] == out["0"][2] == 60
-    np.testing.assert_array_equal(out["1"][0], out["0"][0])
-    np.testing.assert_array_equal(out["1"][1], out["0"][1])
-
-
-def test_rowblock_cg_pass_matches_default(monkeypatch):
-    """The row-block CSR pass carrying the CG x / r and direction updates behind two grid barriers (PLSSVM_MI_RB_CG=1,
-    off by default: measured slower, spmv.hpp) against the default three launches, on the long-trace sparse linear set
-    (tests/long_trace_cases.py: the oracle reproduces itself to 1e-9 over 71 iterations): the same recurrence with the
-    r.r and sum d partials per row block, so the 61 residuals (the run-49 reset runs the default kernels in both) agree
-    to 1e-9 and the alphas after 70 iterations to 1e-9 of their largest."""
-    import long_trace_cases as lc
-
-    s = lc.load("linear_f64_sparse")
-    out = {}
-    for on in ("0", "1"):
-        monkeypatch.setenv("PLSSVM_MI_RB_CG", on)
-        p = pm.Parameter("linear", gamma=float(s["gamma"]), coef0=float(s["coef0"]), cost=s["cost"], epsilon=s["eps"],
-                         real_type=np.float64)
-        p.csr = s["csr"]
-        p.labels = s["y"]
-        with pm.CSVM(p, kp_mode="factored") as svm:
-            svm.learn(imax=lc.IMAX)
-            out[on] = (np.asarray(svm.trace, np.float64), svm.alpha.astype(np.float64), svm.iters)
-    assert out["0"][2] == out["1"][2] == lc.IMAX
-    dev = np.abs(out["1"][0][:61] / out["0"][0][:61] - 1)
-    assert np.all(dev <= 1e-9), dev.max()
-    assert np.abs(out["1"][1] - out["0"][1]).max() <= 1e-9 * np.abs(out["0"][1]).max()
