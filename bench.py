@@ -116,7 +116,8 @@ def run_config(name, args, rank, world, dist, uid, steps, warmup, want_cpu, cpu_
     ndev = pm.device_count()
     device = int(os.environ.get("LOCAL_RANK", str(rank))) % ndev if ndev > 0 else 0
     svm = pm.CSVM(p, device=device, rank=rank, world_size=world, uid=uid, sim_rank=sim,
-                  sparse_algo=getattr(args, "sparse_algo", "auto") if layout != "dense" else "auto")
+                  sparse_algo=getattr(args, "sparse_algo", "auto") if layout != "dense" else "auto",
+                  cg_variant=getattr(args, "cg_variant", None))
     share = sim[1] if sim else world  # the work split divides the implicit matrix by this
     t0 = time.time()
     svm.setup_data_on_device()
@@ -232,6 +233,8 @@ def main():
     ap.add_argument("--sim-rank", default=None, metavar="R/W",
                     help="one GPU computes rank R's share of a W-GPU job (no collective): measures one rank of a "
                          "multi-GPU configuration that does not fit one GPU (e.g. configs[4])")
+    ap.add_argument("--cg-variant", default=None, choices=["reference", "one_reduction", "auto"],
+                    help="CG recurrence (default: the library's auto: one-reduction in a sharded group of several ranks)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--sparse-algo", default="auto", choices=["auto", "pattern", "expansion", "dense", "onthefly"],
                     help="sparse poly/rbf K·p algorithm (PLSSVM_MI_OPT_SPARSE_ALGO; ablations / time-to-solution studies)")

@@ -93,6 +93,19 @@ extern "C" {
 #define PLSSVM_MI_SPARSE_DENSE 3 /* densified on the device, MFMA pairwise tiles (every pair recomputed per K·p) */
 #define PLSSVM_MI_SPARSE_ONTHEFLY 4 /* s_ij re-formed from the CSR / CSC per K·p, nothing stored per pair */
 
+/* CG recurrence of plssvm_mi_solve_cg / plssvm_mi_learn:
+ *   0 = the reference's (OpenMP/csvm.cpp:82-170): two dependent inner products per iteration (d.Ad, r.r), i.e. two
+ *       exposed collectives in a sharded group;
+ *   1 = one-reduction CG (Chronopoulos & Gear): the same iterates in exact arithmetic, the product Q~r instead of Q~d
+ *       with s = Q~d carried by a recurrence, r.r and r.Q~r summed together after ONE collective per iteration; the
+ *       stop test, trace and every-50th explicit residual keep the reference's meaning (tests/test_gpu_cg1.py compares
+ *       its residual curves with the oracle's over 61 iterations);
+ *   2 = auto: 1 in a sharded group of several ranks, else 0. */
+#define PLSSVM_MI_OPT_CG_VARIANT 5
+#define PLSSVM_MI_CG_REFERENCE 0
+#define PLSSVM_MI_CG_ONE_REDUCTION 1
+#define PLSSVM_MI_CG_AUTO 2
+
 typedef struct plssvm_mi_ctx plssvm_mi_ctx;
 
 /* Number of visible HIP devices (>= 0), or a negative error code. */

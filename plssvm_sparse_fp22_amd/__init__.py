@@ -158,7 +158,7 @@ class CSVM:
     """One MI355X context (one GPU, one HIP stream). ``world_size > 1`` joins a row-block group."""
 
     def __init__(self, params: Parameter, device=0, rank=0, world_size=1, uid=None, kp_mode="auto",
-                 sim_rank=None, rbf_form=0, exchange=None, sparse_algo="auto"):
+                 sim_rank=None, rbf_form=0, exchange=None, sparse_algo="auto", cg_variant=None):
         if params.data is None and params.csr is None and params.coo is None:
             raise ValueError("No data points provided!")
         if params.data is not None:
@@ -184,6 +184,9 @@ class CSVM:
                 "dense": _abi.SPARSE_DENSE, "onthefly": _abi.SPARSE_ONTHEFLY}[sparse_algo]
         if algo != _abi.SPARSE_AUTO:  # sparse poly/rbf K·p algorithm, see PLSSVM_MI_OPT_SPARSE_ALGO
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_SPARSE_ALGO, algo))
+        if cg_variant is not None:  # "reference" | "one_reduction" | "auto", see PLSSVM_MI_OPT_CG_VARIANT
+            v = {"reference": 0, "one_reduction": 1, "auto": 2}[cg_variant]
+            self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_CG_VARIANT, v))
         if sim_rank is not None:  # (rank, world): single-GPU test hook, see PLSSVM_MI_OPT_SIM_RANK
             self._check(L.plssvm_mi_set_option(self._ctx, _abi.OPT_SIM_RANK, sim_rank[0] | (sim_rank[1] << 16)))
         if exchange is not None:  # host-staged group: fn(numpy buffer, op) combines in place (torch_exchange)

@@ -36,6 +36,7 @@ EXPORTS = (
 OPT_SIM_RANK = 2
 OPT_RBF_FORM = 3
 OPT_SPARSE_ALGO = 4
+OPT_CG_VARIANT = 5
 SPARSE_AUTO, SPARSE_PATTERN, SPARSE_EXPANSION, SPARSE_DENSE, SPARSE_ONTHEFLY = 0, 1, 2, 3, 4
 PART_KERNEL, PART_OVERLAP, PART_REMAINDER = 0, 1, 2
 XCHG_ALLREDUCE, XCHG_ALLGATHER = 0, 1

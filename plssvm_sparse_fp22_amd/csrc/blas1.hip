@@ -185,7 +185,7 @@ __global__ __launch_bounds__(CG_NT) void cg_fin_dad_kernel(const T *__restrict__
         if (i < m) one(i, rw[e], qv[e], dv[e]);
     }
     for (int64_t i = i0 + CG_PRE * st; i < m; i += st) one(i, load_raw(i), q[i], d[i]);
-    store_partial1(s1, red, pdad);
+    store_partial_first(s1, red, pdad);  // (consumers read the first partial of the pair only)
 }
 
 template <typename T>
@@ -295,7 +295,193 @@ __global__ __launch_bounds__(CG_NT) void cg_dir_sums_kernel(T *__restrict__ d, c
     }
 }
 
+// ---- one-reduction CG (Chronopoulos & Gear 1989; a sharded group's option, plssvm_mi OPT_CG_VARIANT) ------------------
+// The same iterates as openmp::csvm::solver_CG in exact arithmetic (OpenMP/csvm.cpp:82-170), with the matrix product of
+// r instead of d and s = Q~d carried by a recurrence, so an iteration's inner products are summed together after one
+// gather of their partials — one exposed collective per iteration instead of the reference's two (d.Ad before the
+// x / r update, r.r before the direction update):
+//   u_k = Q~ r_k;  gamma_k = r_k.r_k;  beta_k = gamma_k / gamma_{k-1};  d_k = r_k + beta_k d_{k-1};  s_k = u_k + beta_k s_{k-1}
+//   d_k.s_k = r_k.u_k + 2 beta_k r_k.s_{k-1} + beta_k^2 d_{k-1}.s_{k-1};  alpha_k = gamma_k / d_k.s_k
+//   x_{k+1} = x_k + alpha_k d_k;  r_{k+1} = r_k - alpha_k s_k   (every 50th iteration r_{k+1} = b - Q~x_{k+1} instead)
+// d.s is expanded with the measured r_k.s_{k-1} (formed by the update that forms r_k, at no extra pass) rather than
+// Chronopoulos-Gear's -gamma_k / alpha_{k-1}, which assumes r_k orthogonal to d_{k-1}: in fp32 the assumed form left
+// the oracle's curve by up to 1.6e-3 on the long-trace expansion sets, the measured one stays with it.
+// Partial sets (4 RED_BLOCKS per rank, by iteration parity): [r.u | r.r | r.s_prev | 0]; the finalize writes the first,
+// the update of the previous iteration the second and third.
+// The stop test delta <= eps^2 delta0 and the trace (r.r before each iteration) keep the reference's meaning; the r.r of
+// r_k is known when the update of iteration k runs, so the test of r_k is made there (after u_k = Q~r_k, one matrix
+// product that a converged solve does not use) or, at the end of a batch, by cg1_delta_kernel.
+constexpr int CG1_SET = 4 * RED_BLOCKS;
+
+// the first three sums of a gathered [.. | .. | .. | 0] set (G ranks, rank order in each element)
+template <typename T>
+__device__ __forceinline__ void cg1_totals(const T *__restrict__ pset, int G, T *red, T *bc, T &a, T &b, T &c) {
+    T s1 = 0, s2 = 0, s3 = 0;
+    for (int i = threadIdx.x; i < RED_BLOCKS; i += blockDim.x) {
+        T x1 = pset[i], x2 = pset[RED_BLOCKS + i], x3 = pset[2 * RED_BLOCKS + i];
+        for (int g = 1; g < G; ++g) {
+            x1 += pset[g * CG1_SET + i];
+            x2 += pset[g * CG1_SET + RED_BLOCKS + i];
+            x3 += pset[g * CG1_SET + 2 * RED_BLOCKS + i];
+        }
+        s1 += x1;
+        s2 += x2;
+        s3 += x3;
+    }
+    a = block_sum_all(s1, red, bc);
+    b = block_sum_all(s2, red, bc);
+    c = block_sum_all(s3, red, bc);
+}
+
+template <typename T, bool W>
+__global__ __launch_bounds__(CG_NT) void cg1_update_kernel(T *__restrict__ x, T *__restrict__ r, T *__restrict__ d,
+                                                         T *__restrict__ s, const T *__restrict__ u, const T *__restrict__ b,
+                                                         const T *__restrict__ q, int reset, const T *__restrict__ pset,
+                                                         int G, double *trace, int64_t trace_cap, int64_t m, int par,
+                                                         T *__restrict__ pnext, T *__restrict__ psum, cg_scalars<T> *sc,
+                                                         dir_w_t<T> wo) {
+    if (sc->converged) return;
+    __shared__ T red[CG_NT / 64], bc[1];
+    const int64_t i0 = (int64_t) blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t) gridDim.x * blockDim.x;
+    T ru, rr, rs;
+    cg1_totals(pset, G, red, bc, ru, rr, rs);  // r.u, r.r, r.s_prev, ranks in order
+    const bool conv = rr <= sc->eps2delta0;
+    const T gprev = sc->g1[par ^ 1], dsprev = sc->d1[par ^ 1];  // +inf / 0 before the first iteration: beta = 0
+    const T beta = rr / gprev;
+    const T t1 = beta * rs, bb = beta * beta;
+    const T t3 = bb * dsprev;
+    const T ds = (ru + (t1 + t1)) + t3;
+    const T alpha = rr / ds;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const int64_t run = sc->iters;  // the iteration index lives on the device (captured blocks are position-free)
+        sc->delta = rr;
+        if (trace && run < trace_cap) trace[run] = (double) rr;
+        if (conv) {
+            sc->converged = 1;
+        } else {
+            sc->g1[par] = rr, sc->a1[par] = alpha, sc->d1[par] = ds;
+            sc->alpha = alpha, sc->beta = beta, sc->dAd = ds, sc->delta_prev = rr;
+            sc->iters = run + 1;
+        }
+    }
+    if (conv) return;  // the same decision in every block
+    T s1 = 0, s2 = 0, s3 = 0, srr = 0, srs = 0;
+    for (int64_t i = i0; i < m; i += st) {
+        const T ri = r[i];
+        const T tb = beta * d[i];
+        const T dn = ri + tb;
+        d[i] = dn;
+        const T ts = beta * s[i];
+        const T sn = u[i] + ts;
+        s[i] = sn;
+        const T tx = alpha * dn;
+        x[i] = x[i] + tx;
+        if (reset) {
+            r[i] = b[i];  // r = b - Q~x follows (engine: the matrix product of x, then cg1_rsums_kernel)
+        } else {
+            const T ua = alpha * sn;
+            const T rn = ri - ua;
+            r[i] = rn;
+            srr += rn * rn;
+            srs += rn * sn;
+            s1 += rn;
+            s2 += q[i] * rn;
+            if constexpr (W) w_elem(i, rn, wo.e != nullptr ? wo.e[i] : T(1), wo.cw != nullptr ? wo.cw[i] : T(0), wo.e, wo.cw,
+                                    wo.w, wo.w16, s3);
+        }
+    }
+    if (reset) return;
+    store_partial_second(srr, red, pnext);                  // r.r of r_{k+1}
+    __syncthreads();
+    store_partial_first(srs, red, pnext + 2 * RED_BLOCKS);  // r_{k+1}.s_k
+    __syncthreads();
+    store_partials(s1, s2, red, psum);  // sum r / sum q r: the rank-1 terms of the next product
+    if constexpr (W) {
+        __syncthreads();
+        store_partial1(s3, red, wo.spart);
+    }
+}
+
+// r.r, sum r, sum q r (and the expansion's w pass) of a residual formed by a matrix product (x0 = 1, every 50th
+// iteration): the partials cg1_update_kernel leaves for a recurrence-formed r
+template <typename T, bool W>
+__global__ __launch_bounds__(CG_NT) void cg1_rsums_kernel(const T *__restrict__ r, const T *__restrict__ sv,
+                                                        const T *__restrict__ q, int64_t m, T *__restrict__ pnext,
+                                                        T *__restrict__ psum, const cg_scalars<T> *sc, dir_w_t<T> wo) {
+    if (sc->converged) return;
+    __shared__ T red[CG_NT / 64];
+    const int64_t i0 = (int64_t) blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t) gridDim.x * blockDim.x;
+    T s1 = 0, s2 = 0, s3 = 0, srr = 0, srs = 0;
+    for (int64_t i = i0; i < m; i += st) {
+        const T ri = r[i];
+        srr += ri * ri;
+        srs += ri * sv[i];
+        s1 += ri;
+        s2 += q[i] * ri;
+        if constexpr (W) w_elem(i, ri, wo.e != nullptr ? wo.e[i] : T(1), wo.cw != nullptr ? wo.cw[i] : T(0), wo.e, wo.cw, wo.w,
+                                wo.w16, s3);
+    }
+    store_partial_second(srr, red, pnext);
+    __syncthreads();
+    store_partial_first(srs, red, pnext + 2 * RED_BLOCKS);
+    __syncthreads();
+    store_partials(s1, s2, red, psum);
+    if constexpr (W) {
+        __syncthreads();
+        store_partial1(s3, red, wo.spart);
+    }
+}
+
+// the end of a batch: r.r of the current r (the second partials of pset, summed as cg1_update_kernel sums them — the
+// same bits), its trace entry and the stop test, so the host's poll sees the reference's residual after each iteration
+template <typename T>
+__global__ __launch_bounds__(CG_NT) void cg1_delta_kernel(const T *__restrict__ pset, int G, double *trace,
+                                                        int64_t trace_cap, cg_scalars<T> *sc) {
+    if (sc->converged) return;
+    __shared__ T red[CG_NT / 64], bc[1];
+    T ru, rr, rs;
+    cg1_totals(pset, G, red, bc, ru, rr, rs);
+    (void) ru, (void) rs;
+    if (threadIdx.x == 0) {
+        const int64_t run = sc->iters;
+        sc->delta = rr;
+        if (trace && run < trace_cap) trace[run] = (double) rr;
+        if (rr <= sc->eps2delta0) sc->converged = 1;
+    }
+}
+
 }  // namespace
+
+template <typename T>
+void launch_cg1_update(T *x, T *r, T *d, T *s, const T *u, const T *b, const T *q, int reset, const T *pset, int G,
+                       double *trace, int64_t trace_cap, int64_t m, int par, T *pnext, T *psum, cg_scalars<T> *sc,
+                       hipStream_t st, const dir_w_t<T> *wout) {
+    if (wout != nullptr && !reset)
+        hipLaunchKernelGGL((cg1_update_kernel<T, true>), dim3(RED_BLOCKS), dim3(CG_NT), 0, st, x, r, d, s, u, b, q, reset,
+                           pset, G, trace, trace_cap, m, par, pnext, psum, sc, *wout);
+    else
+        hipLaunchKernelGGL((cg1_update_kernel<T, false>), dim3(RED_BLOCKS), dim3(CG_NT), 0, st, x, r, d, s, u, b, q, reset,
+                           pset, G, trace, trace_cap, m, par, pnext, psum, sc, dir_w_t<T>{});
+    MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_cg1_rsums(const T *r, const T *s, const T *q, int64_t m, T *pnext, T *psum, cg_scalars<T> *sc, hipStream_t st,
+                      const dir_w_t<T> *wout) {
+    if (wout != nullptr)
+        hipLaunchKernelGGL((cg1_rsums_kernel<T, true>), dim3(RED_BLOCKS), dim3(CG_NT), 0, st, r, s, q, m, pnext, psum, sc,
+                           *wout);
+    else
+        hipLaunchKernelGGL((cg1_rsums_kernel<T, false>), dim3(RED_BLOCKS), dim3(CG_NT), 0, st, r, s, q, m, pnext, psum, sc,
+                           dir_w_t<T>{});
+    MI_LAUNCH_CHECK();
+}
+
+template <typename T>
+void launch_cg1_delta(const T *pset, int G, double *trace, int64_t trace_cap, cg_scalars<T> *sc, hipStream_t st) {
+    hipLaunchKernelGGL(cg1_delta_kernel<T>, dim3(1), dim3(CG_NT), 0, st, pset, G, trace, trace_cap, sc);
+    MI_LAUNCH_CHECK();
+}
 
 template <typename T>
 void launch_cg_fin_dad(const T *raw, const T *slabs, int64_t P, int64_t sstride, const T *q, const T *d, const T *psum,
@@ -386,7 +572,13 @@ void launch_cg_direction(T *d, const T *r, int64_t m, const cg_scalars<T> *sc, h
     template void launch_cg_upd_rr<T>(T *, T *, const T *, const T *, const T *, int, const T *, int, int64_t, T *, \
                                       cg_scalars<T> *, hipStream_t);                                                \
     template void launch_cg_dir_sums<T>(T *, const T *, const T *, const T *, int, int, double *, int64_t, int64_t, \
-                                        T *, cg_scalars<T> *, hipStream_t, const dir_w_t<T> *);
+                                        T *, cg_scalars<T> *, hipStream_t, const dir_w_t<T> *);                     \
+    template void launch_cg1_update<T>(T *, T *, T *, T *, const T *, const T *, const T *, int, const T *, int,     \
+                                       double *, int64_t, int64_t, int, T *, T *, cg_scalars<T> *, hipStream_t,      \
+                                       const dir_w_t<T> *);                                                         \
+    template void launch_cg1_rsums<T>(const T *, const T *, const T *, int64_t, T *, T *, cg_scalars<T> *, hipStream_t, \
+                                      const dir_w_t<T> *);                                                          \
+    template void launch_cg1_delta<T>(const T *, int, double *, int64_t, cg_scalars<T> *, hipStream_t);
 INST(float)
 INST(double)
 #undef INST

@@ -111,6 +111,8 @@ int plssvm_mi_set_option(plssvm_mi_ctx *ctx, int key, int64_t value) {
             e.rbf_form = (int) value;
         } else if (key == PLSSVM_MI_OPT_SPARSE_ALGO && value >= 0 && value <= 4) {
             e.sparse_algo = (int) value;
+        } else if (key == PLSSVM_MI_OPT_CG_VARIANT && value >= 0 && value <= 2) {
+            e.cg_variant = (int) value;
         } else {
             throw mi_error(PLSSVM_MI_ERR_ARG, "bad option");
         }

@@ -77,6 +77,21 @@ __device__ __forceinline__ void store_partial1(T v1, T *red, T *__restrict__ par
     }
 }
 
+// the first partial of the pair only: the second slot keeps what another kernel put there (the one-reduction CG keeps
+// its r.r partials beside the r.u partials of the finalize, so that one collective gathers both)
+template <typename T>
+__device__ __forceinline__ void store_partial_first(T v1, T *red, T *__restrict__ partials) {
+    const T r1 = block_sum(v1, red);
+    if (threadIdx.x == 0) partials[blockIdx.x] = r1;
+}
+
+// the second partial of the pair only
+template <typename T>
+__device__ __forceinline__ void store_partial_second(T v2, T *red, T *__restrict__ partials) {
+    const T r2 = block_sum(v2, red);
+    if (threadIdx.x == 0) partials[RED_BLOCKS + blockIdx.x] = r2;
+}
+
 template <typename T>
 __device__ __forceinline__ void store_partials(T v1, T v2, T *red, T *__restrict__ partials) {
     const T r1 = block_sum(v1, red);

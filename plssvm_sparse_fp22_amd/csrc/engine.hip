@@ -8,6 +8,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <limits>
+
 #include "engine.hpp"
 
 namespace plssvm_mi {
@@ -211,10 +213,9 @@ void engine<T>::allreduce(T *buf, int64_t count) {
 // sharded CG: the 2 x RED_BLOCKS partials of every rank (rank-major, into slot `slot` of cgp_g); the
 // consumers sum them in rank order. Unsharded or a single rank: the local partials.
 template <typename T>
-const T *engine<T>::gather_partials(T *local, int slot) {
+const T *engine<T>::gather_partials(T *local, int slot, int64_t K) {
     if (!gathered) return local;
-    const int64_t K = 2 * RED_BLOCKS;
-    T *out = cgp_g.get() + (int64_t) slot * G * K;
+    T *out = cgp_g.get() + (int64_t) slot * G * 2 * RED_BLOCKS;  // K = 4 R: slots slot and slot + 1
     if (comm != nullptr) {
         MI_NCCL_CHECK(ncclAllGather(local, out, (size_t) K, nccl_type<T>(), comm, stream));
     } else {
@@ -551,6 +552,8 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
     cg_scalars<T> init{};
     init.eps2delta0 = eps * eps;
     init.force = force ? 1 : 0;
+    cg1 = cg1_wanted();
+    init.g1[0] = init.g1[1] = init.a1[0] = init.a1[1] = std::numeric_limits<T>::infinity();
     MI_HIP_CHECK(hipMemcpyAsync(sc.get(), &init, sizeof(init), hipMemcpyHostToDevice, stream));
     trace_cap = std::max<int64_t>(trace_len, 1);
     if (trace.size() < trace_cap) trace.alloc(trace_cap, stream);
@@ -562,12 +565,22 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
     // delta = r.r ; delta0 ; d = r   (:92-97)   (sharded: this rank's rows, the ranks' partials gathered)
     launch_dot2<T>(r.get() + v0, r.get() + v0, nullptr, nullptr, vn, red.get(), nullptr, stream);
     launch_dot_final<T>(gather_partials(red.get(), 3), sc.get(), FIN_DELTA0, 0, trace.get(), trace_cap, nullptr, stream, G);
-    // d = r, with sum d / sum q d for the first Q~d
     dir_w_t<T> wo{};
     const bool fw = dir_w_fill(wo);
-    launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, qf() + v0, nullptr, 1, 1, nullptr, 0, vn, cgp.get(), sc.get(),
-                          stream, fw ? &wo : nullptr);
-    w_pre = fw ? dv.get() : nullptr;
+    if (cg1) {
+        // one-reduction CG: d = s = 0, the r.r / sum r / sum q r partials of r0 (set 0) for the first product Q~r
+        if (sv.size() < q.size()) sv.alloc(q.size(), stream);
+        if (cg1p.size() < 8 * RED_BLOCKS) cg1p.alloc(8 * RED_BLOCKS, stream);  // two [r.u | r.r | r.s | 0] sets
+        MI_HIP_CHECK(hipMemsetAsync(dv.get(), 0, sizeof(T) * (size_t) q.size(), stream));
+        MI_HIP_CHECK(hipMemsetAsync(sv.get(), 0, sizeof(T) * (size_t) q.size(), stream));
+        launch_cg1_rsums<T>(r.get() + v0, sv.get() + v0, qf() + v0, vn, cg1p.get(), cgp.get(), sc.get(), stream, fw ? &wo : nullptr);
+        w_pre = fw ? r.get() : nullptr;
+    } else {
+        // d = r, with sum d / sum q d for the first Q~d
+        launch_cg_dir_sums<T>(dv.get() + v0, r.get() + v0, qf() + v0, nullptr, 1, 1, nullptr, 0, vn, cgp.get(), sc.get(),
+                              stream, fw ? &wo : nullptr);
+        w_pre = fw ? dv.get() : nullptr;
+    }
     if (gathered && comm != nullptr) psum_pending = true;  // gathered with the first K·p's collective
     else gather_partials(cgp.get(), 0);
     run = 0;
@@ -584,8 +597,72 @@ void engine<T>::cg_begin(const T *b_host, const T *q_host, T eps, bool force, do
 }
 
 // one CG iteration (reset: the every-50th recomputation r = b - Q~x), all launches on the engine stream
+// the one-reduction recurrence: forced (PLSSVM_MI_CG_ONE_REDUCTION), or auto for a sharded group of several ranks
+template <typename T>
+bool engine<T>::cg1_wanted() const {
+    return cg_variant == 1 || (cg_variant == 2 && gathered && G > 1);
+}
+
+// one iteration of the one-reduction CG (blas1.hip cg1_update_kernel): u = Q~r with the finalize forming the r.u
+// partials beside the r.r ones of set `par`, ONE gather of that set, then d, s, x, r and the next partials in one kernel
+template <typename T>
+void engine<T>::cg1_iter(int reset) {
+    const cg_scalars<T> *st = sc.get();
+    T *psum = cgp.get();
+    T *cur = cg1p.get() + (int64_t) cg_par * 4 * RED_BLOCKS, *nxt = cg1p.get() + (int64_t) (cg_par ^ 1) * 4 * RED_BLOCKS;
+    const T *psum_in = gathered ? cgp_g.get() : psum;
+    const int raw_only = (sim_world > 0 && sim_rank != 0 && !shard) ? 1 : 0;
+    const T *slabs = nullptr;
+    int64_t P = 0;
+    bool fin = false;
+    if (sparse_stored() && factored() && world == 1 && sim_world == 0 && csr.rb_csr.nblk > 0) {
+        spmv_pass_csc(r.get(), st);
+        launch_rowblock_fin<T>(csr.rb_csr, w.get(), d, q.get(), r.get(), psum, QA_cost, cost_inv(), Ad.get(), cur, st, stream);
+        fin = true;
+    } else if (sparse && factored() && world == 1 && sim_world == 0 && csr.spmv_csr.P > 1) {
+        spmv_pass_csc(r.get(), st);
+        launch_panel_spmv<T>(csr.spmv_csr, w.get(), d, raw.get(), st, stream, 1, 0, false);
+        slabs = csr.spmv_csr.partial.get();
+        P = csr.spmv_csr.P;
+    } else {
+        const kp_fin_t f{ qf(), r.get(), psum_in, G, QAf(), cost_inv(), Ad.get(), cur };
+        kp_fin_req = raw_only ? nullptr : &f;
+        kp_fin_done = false;
+        ctr_now = ctr_active();
+        kp_raw(r.get(), st);
+        ctr_now = false;
+        kp_fin_req = nullptr;
+        fin = kp_fin_done;
+        kp_fin_done = false;
+    }
+    flush_psum();
+    if (!fin)
+        launch_cg_fin_dad<T>(raw.get() + v0, slabs, P, m, qf() + v0, r.get() + v0, psum_in, G, QAf(), cost_inv(), raw_only, vn,
+                             Ad.get() + v0, cur, sc.get(), stream);
+    // the one collective of the iteration: [r.u | r.r] partials of every rank
+    const T *pset = gather_partials(cur, 1, 4 * RED_BLOCKS);
+    dir_w_t<T> wo{};
+    const bool fw = !reset && dir_w_fill(wo);
+    launch_cg1_update<T>(x.get() + v0, r.get() + v0, dv.get() + v0, sv.get() + v0, Ad.get() + v0, b.get() + v0, qf() + v0,
+                         reset, pset, G, trace.get(), trace_cap, vn, cg_par, nxt, psum, sc.get(), stream, fw ? &wo : nullptr);
+    w_pre = fw ? r.get() : nullptr;
+    if (reset) {  // r = b - Q~x, then its partials (csvm.cpp:119-132)
+        kp_device(x.get(), r.get(), T(-1), false, st);
+        dir_w_t<T> wr{};
+        const bool fr = dir_w_fill(wr);
+        launch_cg1_rsums<T>(r.get() + v0, sv.get() + v0, qf() + v0, vn, nxt, psum, sc.get(), stream, fr ? &wr : nullptr);
+        w_pre = fr ? r.get() : nullptr;
+    }
+    if (gathered && comm != nullptr) psum_pending = true;  // gathered with the next product's first collective
+    else gather_partials(psum, 0);
+}
+
 template <typename T>
 void engine<T>::cg_iter(int reset) {
+    if (cg1) {
+        cg1_iter(reset);
+        return;
+    }
     const cg_scalars<T> *st = sc.get();
     T *psum = cgp.get(), *pdad = psum + 2 * RED_BLOCKS, *prr = psum + 4 * RED_BLOCKS;
     // sharded: the partials the previous step gathered (slot 0: sum d / sum q d)
@@ -673,7 +750,10 @@ void engine<T>::graph_capture() {
         w_pre = nullptr;
         MI_HIP_CHECK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
         try {
-            for (int k = 0; k < CG_RESET; ++k) cg_iter(k == CG_RESET - 1 ? 1 : 0);
+            for (int k = 0; k < CG_RESET; ++k) {
+                cg_par = k & 1;  // blocks start at multiples of CG_RESET (even)
+                cg_iter(k == CG_RESET - 1 ? 1 : 0);
+            }
         } catch (...) {
             (void) hipStreamEndCapture(stream, &g);
             if (g) (void) hipGraphDestroy(g);
@@ -707,10 +787,16 @@ void engine<T>::cg_step(int64_t nsteps, bool &converged, int64_t &iters) {
             s += CG_RESET;
             run += CG_RESET;
         } else {
+            cg_par = (int) (run & 1);
             cg_iter(run % CG_RESET == CG_RESET - 1 ? 1 : 0);
             ++s;
             ++run;
         }
+    }
+    if (cg1 && nsteps > 0) {  // the residual after the batch's last iteration: trace, stop test (cg1_delta_kernel)
+        const T *cur = cg1p.get() + (int64_t) (run & 1) * 4 * RED_BLOCKS;
+        flush_psum();
+        launch_cg1_delta<T>(gather_partials(const_cast<T *>(cur), 1, 4 * RED_BLOCKS), G, trace.get(), trace_cap, sc.get(), stream);
     }
     cg_scalars<T> h{};
     MI_HIP_CHECK(hipMemcpyAsync(&h, sc.get(), sizeof(h), hipMemcpyDeviceToHost, stream));

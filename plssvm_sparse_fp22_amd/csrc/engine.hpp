@@ -101,7 +101,7 @@ struct engine : engine_base {
     int G = 1;
     dev_buf<T> cgp_g;      // gathered partials, slots [5][G][2 RED_BLOCKS]: sum d / sum q d, d.Ad, r.r, kp sums, S
     std::vector<T> xpart;  // host staging of the host exchange's partial gathers
-    const T *gather_partials(T *local, int slot);
+    const T *gather_partials(T *local, int slot, int64_t K = 2 * RED_BLOCKS);  // K values per rank
     // RCCL group: the sum d / sum q d partials of a CG step ride with the next collective of the K·p
     // (one launch, one latency) instead of a collective of their own
     bool psum_pending = false;
@@ -124,6 +124,14 @@ struct engine : engine_base {
     const T *w_pre = nullptr, *graph_w_end = nullptr;
     bool dir_w_fill(dir_w_t<T> &o);
     dev_buf<T> cgp;  // fused CG partials: [0, 2R) sum d / sum q d, [2R, 4R) d.Ad, [4R, 6R) r.r
+    // one-reduction CG (blas1.hip cg1_*; PLSSVM_MI_OPT_CG_VARIANT): s = Q~d by recurrence (sv), u = Q~r in Ad, and two
+    // partial sets [r.u | r.r] by iteration parity (cg1p), gathered by one collective per iteration
+    int cg_variant = 2;  // PLSSVM_MI_CG_REFERENCE / _ONE_REDUCTION / _AUTO (default: one-reduction in sharded groups)
+    bool cg1 = false;    // the running solve uses it (cg_begin)
+    int cg_par = 0;      // parity of the iteration cg_iter forms
+    dev_buf<T> sv, cg1p;
+    bool cg1_wanted() const;
+    void cg1_iter(int reset);
     dev_buf<cg_scalars<T>> sc;
     dev_buf<double> trace;
     int64_t trace_cap = 0;

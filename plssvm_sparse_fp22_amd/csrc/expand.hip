@@ -1126,19 +1126,11 @@ __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__res
 #endif
 #endif
 
-#ifndef EXP_LDS_ATOMIC
-#define EXP_LDS_ATOMIC 1
-#endif
-// v added to a row accumulator in LDS: one ds_add (no return value, so no wait for an LDS read) instead of a
-// read-add-write. Each wave owns its rows and issues its adds in program order, and no instruction adds to one row
-// twice: the same sums in the same order as the read-add-write, bit for bit
+// v added to a row accumulator in LDS (read-add-write; each wave owns its rows). LDS float atomics (ds_add_f32, no
+// wait for the read) measured slower in round 6: config 5's pair-flag stream 0.842 -> 1.045 ms, 3-RBF unchanged
 template <typename T>
 __device__ __forceinline__ void racc_add(T *p, T v) {
-#if EXP_LDS_ATOMIC
-    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
     *p += v;
-#endif
 }
 
 // one step of a segmented inclusive lane scan keyed by k (keys non-decreasing in lane order): v += the DPP
@@ -1530,7 +1522,7 @@ __global__ __launch_bounds__(cgk::CG_NT) void exp_combine_fin_kernel(
         Ad[i] = v;
         s1 = cgk::cg_acc(s1, di, v);
     }
-    cgk::store_partial1(s1, red, pdad);
+    cgk::store_partial_first(s1, red, pdad);  // (consumers read the first partial of the pair only)
 }
 
 template <typename T>

@@ -21,6 +21,7 @@ template <typename T>
 struct cg_scalars {
     T delta, delta0, alpha, beta, sp, sqp, eps2delta0, dAd;
     T delta_prev;  // delta of the previous iteration (fused CG kernels: read while delta is rewritten)
+    T g1[2], a1[2], d1[2];  // one-reduction CG, by iteration parity: r.r (+inf before the first), alpha, d.Q~d (0)
     int converged;
     int force;  // bench mode: never converge (same work per iteration)
     int64_t iters;
@@ -138,6 +139,17 @@ struct dir_w_t {
     const T *cw;
     T *spart;
 };
+// one-reduction CG (Chronopoulos-Gear, blas1.hip): the update of iteration k from the gathered [r.u | r.r] partials
+// (pset, G sets), the residual sums of a new r, the r.r of a batch's last r (poll)
+template <typename T>
+void launch_cg1_update(T *x, T *r, T *d, T *s, const T *u, const T *b, const T *q, int reset, const T *pset, int G,
+                       double *trace, int64_t trace_cap, int64_t m, int par, T *pnext, T *psum, cg_scalars<T> *sc,
+                       hipStream_t st, const dir_w_t<T> *wout);
+template <typename T>
+void launch_cg1_rsums(const T *r, const T *s, const T *q, int64_t m, T *pnext, T *psum, cg_scalars<T> *sc, hipStream_t st,
+                      const dir_w_t<T> *wout);
+template <typename T>
+void launch_cg1_delta(const T *pset, int G, double *trace, int64_t trace_cap, cg_scalars<T> *sc, hipStream_t st);
 template <typename T>
 void launch_cg_dir_sums(T *d, const T *r, const T *q, const T *prr, int G, int init, double *trace, int64_t trace_cap,
                         int64_t m, T *psum, cg_scalars<T> *sc, hipStream_t s, const dir_w_t<T> *wout = nullptr);

@@ -47,10 +47,7 @@ constexpr int SELL_SIGMA = 4096;     // sorting window (segments)
 // per value) config 5 778 / 771 / 761 — so 8 for real values, 4 for FP22 (round 2, before the row-block pass
 // and the 16-bit pair loads, measured 4 best for both)
 template <bool F22>
-#ifndef SELL_SU_F22
-#define SELL_SU_F22 4
-#endif
-constexpr int sell_unroll() { return F22 ? SELL_SU_F22 : 8; }
+constexpr int sell_unroll() { return F22 ? 4 : 8; }
 // LDS-panel passes: the 16-bit panel indices of entries 2t, 2t+1 of a slot are adjacent, so one 32-bit load per lane
 // (256 B per wave-instruction) fetches two (chunk widths padded to even); packed FP22 values likewise, one 12-byte
 // load per lane (3 words at 4-byte alignment) decodes two. (Pairing real values too measured no gain, round 2.)

@@ -16,10 +16,10 @@ def share(ms, layout="fp22", kp_mode="pairwise", launch_ms=0.1, h="bfloat16 (pre
             "roofline": {"kernel": "exp_hcell_kernel", "launch_ms": launch_ms, "h_storage": h}}
 
 
-def run_predict(tmp_path, rows, one_ms, *extra):
+def run_predict(tmp_path, rows, one_ms, *extra, flags=()):
     f = tmp_path / "shares.jsonl"
     f.write_text("".join(json.dumps(r) + "\n" for r in rows))
-    out = subprocess.run([sys.executable, os.path.join(TOOLS, "predict_scaling.py"), str(f), str(one_ms), *extra],
+    out = subprocess.run([sys.executable, os.path.join(TOOLS, "predict_scaling.py"), *flags, str(f), str(one_ms), *extra],
                          check=True, capture_output=True, text=True).stdout
     return json.loads(out)
 
@@ -43,6 +43,20 @@ def test_predict_scaling_collective_model(tmp_path):
     # slower interconnect assumptions can only predict less
     sp = [out["predictions"][k]["speedup"] for k in ("fast", "mid", "slow")]
     assert sp[0] >= sp[1] >= sp[2]
+
+
+def test_predict_scaling_one_reduction_cg(tmp_path):
+    """--cg1 (the one-reduction CG of a sharded group): the iteration's dot partials travel in one all-gather of
+    4 x 512 partials per rank instead of two of 2 x 512 — one latency fewer"""
+    rows = [share(0.22 + 0.001 * r) for r in range(8)]
+    ref = run_predict(tmp_path, rows, 1.3, "2", "0")
+    one = run_predict(tmp_path, rows, 1.3, "2", "0", flags=("--cg1",))
+    G, alpha, beta = 8, 8e-6, 200e9
+    tiny = 2 * 512 * 4 * G
+    saved = 2 * (alpha + (G - 1) / G * tiny / beta) - (alpha + (G - 1) / G * 2 * tiny / beta)
+    got = (ref["predictions"]["fast"]["iteration_ms"] - one["predictions"]["fast"]["iteration_ms"]) * 1e-3
+    assert one["cg"] == "one-reduction" and ref["cg"] == "reference"
+    assert abs(got - saved) < 1e-7, (got, saved)
 
 
 def test_predict_scaling_dense_allreduce(tmp_path):

@@ -21,12 +21,18 @@ t_stream is the share's exp_hcell_kernel launch (roofline.launch_ms of the share
 column-moment pass of one share (optional argument, microseconds, from the share's kernel stats; 0 = no
 credit).
 
-usage: tools/predict_scaling.py <shares.jsonl> <one-GPU ms per iteration> [KM] [t_moments_us]
+With --cg1 (shares measured with bench.py --cg-variant one_reduction, the default of a sharded group since round 6)
+the iteration's inner products travel in ONE all-gather of 4 x 512 partials per rank instead of two of 2 x 512.
+
+usage: tools/predict_scaling.py [--cg1] <shares.jsonl> <one-GPU ms per iteration> [KM] [t_moments_us]
 """
 import json
 import sys
 
 MODELS = [("fast", 8e-6, 200e9), ("mid", 12e-6, 150e9), ("slow", 20e-6, 100e9)]
+
+
+CG1 = False
 
 
 def collectives(rec, G, km):
@@ -38,12 +44,12 @@ def collectives(rec, G, km):
     if cfg["layout"] == "dense" and cfg["kp_mode"] == "pairwise":
         return [("allreduce", m * s, None)]
     if cfg["kp_mode"] == "factored":
-        return [("allreduce", d * s, None)] + [("allgather", tiny, None)] * 2
+        return [("allreduce", d * s, None)] + ([("allgather", 2 * tiny, None)] if CG1 else [("allgather", tiny, None)] * 2)
     # bfloat16 windows: the group gathers w as bfloat16 plus the ranks' S partials
     ws = 2 if "bfloat16" in str(rec["roofline"].get("h_storage", "")) else s
     extra = tiny if ws == 2 else 0
-    return [("allgather", m * ws + tiny + extra, "moments"), ("allreduce", d * km * s, "stream")] + \
-        [("allgather", tiny, None)] * 2
+    dots = [("allgather", 2 * tiny, None)] if CG1 else [("allgather", tiny, None)] * 2
+    return [("allgather", m * ws + tiny + extra, "moments"), ("allreduce", d * km * s, "stream")] + dots
 
 
 def t_coll(kind, total, G, alpha, beta):
@@ -52,14 +58,18 @@ def t_coll(kind, total, G, alpha, beta):
 
 
 def main():
-    rows = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")]
-    one = float(sys.argv[2])
-    km = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-    t_mom = float(sys.argv[4]) * 1e-6 if len(sys.argv) > 4 else 0.0
+    global CG1
+    argv = sys.argv[1:]
+    if argv and argv[0] == "--cg1":
+        CG1, argv = True, argv[1:]
+    rows = [json.loads(l) for l in open(argv[0]) if l.startswith("{")]
+    one = float(argv[1])
+    km = int(argv[2]) if len(argv) > 2 else 2
+    t_mom = float(argv[3]) * 1e-6 if len(argv) > 3 else 0.0
     G = len(rows)
     ms = [r["ms_per_step"] for r in rows]
     out = {"config": rows[0]["config"]["workload"], "W": G, "ms_per_step_by_rank": ms, "max_share_ms": max(ms),
-           "one_gpu_ms": one, "predictions": {}}
+           "one_gpu_ms": one, "cg": "one-reduction" if CG1 else "reference", "predictions": {}}
     for name, alpha, beta in MODELS:
         c = 0.0
         for r in rows:  # the slowest rank's share + its exposed collective time
