@@ -724,10 +724,8 @@ void engine<T>::cg_iter(int reset) {
 // PLSSVM_MI_GRAPH=2 (the collectives then run as graph nodes); PLSSVM_MI_GRAPH=0 disables graphs.
 template <typename T>
 bool engine<T>::graph_usable() const {
-    static const int mode = [] {
-        const char *e = std::getenv("PLSSVM_MI_GRAPH");
-        return e == nullptr ? 1 : std::atoi(e);
-    }();
+    const char *ge = std::getenv("PLSSVM_MI_GRAPH");  // read per call (tests compare graphs off / on in one process)
+    const int mode = ge == nullptr ? 1 : std::atoi(ge);
     if (mode == 0 || xchg != nullptr || m <= 0) return false;
     return comm == nullptr || mode == 2;
 }

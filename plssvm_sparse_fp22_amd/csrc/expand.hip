@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     constexpr int VE = 16 / (int) sizeof(WT), NV = CW / VE, PV = (NV + NT - 1) / NT;
     using wvec = __attribute__((ext_vector_type(VE))) WT;
     wvec reg[PV];
-    auto load_win = [&](int64_t W) {
+    auto load_win = [&](int64_t W) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < PV; ++q) {
             const int v = q * NT + tid;
@@ -1214,11 +1214,11 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             }
         }
     };
-    auto wat = [&](uint32_t j) -> T {  // w_j from the staged window
+    auto wat = [&](uint32_t j) __attribute__((always_inline)) -> T {  // w_j from the staged window
         if constexpr (HB) return (T) __uint_as_float((uint32_t) wl[j] << 16);
         else return wl[j];
     };
-    auto store_win = [&]() {
+    auto store_win = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < PV; ++q) {
             const int v = q * NT + tid;
@@ -1237,7 +1237,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     };
     group_regs nx[EXP_NH];
     const bool empty = s_end == wo[W0];
-    auto fetch = [&](int64_t c) {
+    auto fetch = [&](int64_t c) __attribute__((always_inline)) {
         if (empty) return;  // empty stream (wave-uniform)
 #pragma unroll
         for (int hh = 0; hh < EXP_NH; ++hh) {
@@ -1266,7 +1266,7 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     // one group of 64 chunks: the 4 slots times w from the window, then the rows' sums into racc
     // RF: the rows of a window's chunks from their row-start flags (carry = the row before the step's first chunk + 1)
     int carry = 0;
-    auto group = [&](const group_regs &g, bool have) {
+    auto group = [&](const group_regs &g, bool have) __attribute__((always_inline)) {
         if constexpr (RF == 2) {
             static_assert(HB && EXP_JH && sizeof(T) == 4, "pair flags: bfloat16 H, side-by-side chunks");
             // pair flags: bit 14 of the chunk's H0 / H2 marks a row starting at slot 0 / 2. A lane's two pairs give
@@ -1312,7 +1312,9 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
             if (bh == 0ull) return;  // a group wholly past the window's end
             if (f0 || f1) racc_add(&racc[f1 ? row1 : row0], (f1 ? a23 : t) - P);  // tail: the row left open in this lane
             if (f0 && f1) racc_add(&racc[row0], a01);                             // a row inside this lane
-            if ((f0 || f1) && !(lane == 0 && f0)) racc_add(&racc[(f0 ? row0 : row1) - 1], E + (f0 ? 0.f : a01));  // head
+            // head: not for a row that starts at the group's first valid lane (its predecessor is no row of this pass)
+            const int lead = __builtin_ctzll(bh);
+            if ((f0 || f1) && !(lane == lead && f0)) racc_add(&racc[(f0 ? row0 : row1) - 1], E + (f0 ? 0.f : a01));
             if (lane == 63) racc_add(&racc[row1], P);                             // the row open at the group's end
             return;
         }
@@ -1406,24 +1408,68 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     }
     __syncthreads();
     constexpr int STEP = 64 * EXP_NH;
-    for (int64_t W = W0; W < W1; ++W) {
+    if constexpr (RF == 2) {
+        // pair flags: steps restart at every window (the part of a window's last step past its end is loaded again as
+        // the next window's first step). The contiguous walk below measured 4.5 % slower here (config 5: 0.861 vs
+        // 0.824 ms, round 6 — 127 VGPRs and a spill for the straddling step's registers), 1.8 % faster with chunk flags.
+        for (int64_t W = W0; W < W1; ++W) {
+            if (W + 1 < W1) load_win(W + 1);  // lands in registers while this window is processed
+            const int64_t c_end = wo[W + 1];
+            carry = wave * (int) (RB / EXP_NWV);  // the wave's first row starts every window
+            for (int64_t cb = wo[W]; cb < c_end; cb += STEP) {  // wave-uniform trip count
+                group_regs cur[EXP_NH];
+#pragma unroll
+                for (int hh = 0; hh < EXP_NH; ++hh) cur[hh] = nx[hh];
+                fetch((cb + STEP < c_end ? cb + STEP : c_end) + lane);
+#pragma unroll
+                for (int hh = 0; hh < EXP_NH; ++hh) group(cur[hh], cb + 64 * hh + lane < c_end);  // groups in order
+            }
+            if (W + 1 < W1) {
+                __syncthreads();  // every wave is done with window W
+                store_win();
+            }
+            __syncthreads();
+        }
+    } else if (W0 < W1) {
+        // The wave's stream is one contiguous range over its windows, walked in steps of STEP chunks that ignore the
+        // window boundaries: a step that straddles the end of window W is processed for W (the chunks below the end),
+        // then — after the block's window switch — for W + 1 (the chunks from there), so no chunk is loaded twice (the
+        // restarted steps load the part of a window's last step past its end again as the next window's first step:
+        // 3-RBF 0.782 -> 0.768 ms, round 6). Every wave switches windows W1 - W0 - 1 times (the block's barriers match).
+        int64_t W = W0, c_lo = wo[W0], c_hi = wo[W0 + 1];
+        const int base_row = wave * (int) (RB / EXP_NWV);  // RF: the wave's first row starts every window
+        carry = base_row;
         if (W + 1 < W1) load_win(W + 1);  // lands in registers while this window is processed
-        const int64_t c_end = wo[W + 1];
-        carry = wave * (int) (RB / EXP_NWV);  // RF: the wave's first row starts every window
-        for (int64_t cb = wo[W]; cb < c_end; cb += STEP) {  // wave-uniform trip count
+        auto next_window = [&]() __attribute__((always_inline)) {
+            __syncthreads();  // every wave is done with window W
+            store_win();
+            __syncthreads();
+            ++W;
+            if (W + 1 < W1) load_win(W + 1);
+            c_lo = c_hi;
+            c_hi = wo[W + 1];
+            carry = base_row;
+        };
+        for (int64_t cb = wo[W0]; cb < s_end; cb += STEP) {  // wave-uniform trip count
             group_regs cur[EXP_NH];
 #pragma unroll
             for (int hh = 0; hh < EXP_NH; ++hh) cur[hh] = nx[hh];
-            // next step (next window's first at c_end; groups past a window's end are loaded, masked, and
-            // loaded again as the next window's)
-            fetch((cb + STEP < c_end ? cb + STEP : c_end) + lane);
+            fetch((cb + STEP < s_end ? cb + STEP : s_end) + lane);  // the next step, one ahead (unconditional: a
+            // conditional load would wait for it at the merge)
+            for (;;) {
 #pragma unroll
-            for (int hh = 0; hh < EXP_NH; ++hh) group(cur[hh], cb + 64 * hh + lane < c_end);  // groups in order
+                for (int hh = 0; hh < EXP_NH; ++hh) {  // groups in order, the chunks of window W
+                    const int64_t pos = cb + 64 * hh + lane;
+                    group(cur[hh], pos >= c_lo && pos < c_hi);
+                }
+                if (c_hi > cb + STEP || W + 1 >= W1) break;  // window W goes on in the next step (or is the last)
+                next_window();
+                if (c_lo >= cb + STEP) break;  // the new window starts with the next step
+            }
         }
-        if (W + 1 < W1) {
-            __syncthreads();  // every wave is done with window W
-            store_win();
-        }
+        while (W + 1 < W1) next_window();  // a wave whose stream is empty still takes part in every switch
+        __syncthreads();
+    } else {
         __syncthreads();
     }
     const int64_t rb0 = I * RB;

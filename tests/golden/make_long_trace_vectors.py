@@ -63,6 +63,9 @@ def vectors(name):
         meta["rep_1e6"] = reproducible(a["trace"], b["trace"], 1e-6)
         n = min(61, len(r1["trace"]), len(a["trace"]))
         meta["f32_oracle_dev"] = float(np.abs(r1["trace"][:n] / a["trace"][:n] - 1).max())
+        # the curve the fp32 GPU runs are compared with: the fp64 oracle's (delta_ratio_last is the fp32 oracle's own)
+        meta["delta_ratio_last64"] = float(a["trace"][-1] / a["trace"][0])
+        meta["delta_ratio_60_64"] = float(a["trace"][min(60, len(a["trace"]) - 1)] / a["trace"][0])
     else:
         meta["rep_1e9"] = reproducible(r1["trace"], r8["trace"])
         meta["ld_dev"] = float(np.abs(r1["trace"] / arrays["trace_ld"][:len(r1["trace"])] - 1).max())

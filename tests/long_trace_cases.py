@@ -105,6 +105,12 @@ CASES = {
                              {"PLSSVM_MI_EXP_ROWS": "flags"}, {"exp_hbytes": 2, "exp_layout": 2, "centered": 1}),
     "rbf_f32_bf16_flags_c": ("rbf", np.float32, ("group", 300, 10, 17, 1e3), ("dist", 0.001), 0.0, 1e6, "expansion",
                              {"PLSSVM_MI_EXP_ROWS": "flags"}, {"exp_hbytes": 2, "exp_layout": 2, "centered": 1}),
+    # round 6: fp32 bfloat16 cases whose fp64 curve DESCENDS by 2-3 orders over the window (C = 3e5;
+    # the C = 1e6 cases above descend by less than one, non-monotonically) while the oracle still reproduces itself
+    "rbf_f32_bf16_desc": ("rbf", np.float32, ("group", 300, 10, 18, 1e3), ("dist", 0.001), 0.0, 3e5, "expansion",
+                          {"PLSSVM_MI_EXP_ROWS": "flags"}, {"exp_hbytes": 2, "exp_layout": 2, "centered": 1}),
+    "rbf_f32_bf16_desc_pairs": ("rbf", np.float32, ("group", 300, 3, 19, 1e3), ("x2", 4e-3), 0.0, 3e5, "expansion",
+                                {"PLSSVM_MI_EXP_ROWS": "pairs"}, {"exp_hbytes": 2, "exp_layout": 4, "centered": 1}),
 }
 
 

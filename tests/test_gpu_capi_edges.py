@@ -102,3 +102,33 @@ def test_centered_learn_equals_plain(oracle, kernel, monkeypatch):
     scale = np.abs(ref["alpha"]).max()
     for ctr in ("1", "0"):
         assert np.abs(got[ctr] - ref["alpha"]).max() <= 2e-2 * scale, (kernel, ctr)
+
+
+@pytest.mark.parametrize("kernel", ["rbf", "linear"])
+def test_graph_replay_off_equals_on(kernel, monkeypatch):
+    """PLSSVM_MI_GRAPH=0 launches every CG iteration instead of replaying captured 50-iteration blocks: the same
+    kernels in the same order, so learn() gives the same bits (imax = 120 crosses two captured blocks)."""
+    csr, y = datagen.sparse_csr(3000, 1500, 10, seed=23, dtype=np.float64)
+    out = {}
+    for g in ("1", "0"):
+        monkeypatch.setenv("PLSSVM_MI_GRAPH", g)
+        rowptr, col, val, n, d = csr
+        p = pm.Parameter(kernel, gamma=1.0 / d, real_type=np.float64, epsilon=1e-30, cost=1e3)
+        p.csr = csr
+        p.labels = y
+        with pm.CSVM(p) as svm:
+            svm.learn(imax=120)
+            out[g] = (np.asarray(svm.trace).copy(), svm.alpha.copy(), svm.iters)
+    assert out["1"][2] == out["0"][2]
+    np.testing.assert_array_equal(out["1"][0], out["0"][0])
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
+
+
+def test_setup_timing_lines(capfd, monkeypatch):
+    """PLSSVM_MI_TIMING=1 prints the setup's phase times to stderr ("[plssvm_mi] <phase> <seconds>")."""
+    monkeypatch.setenv("PLSSVM_MI_TIMING", "1")
+    csr, y = datagen.sparse_csr(3000, 1500, 10, seed=24, dtype=np.float32)
+    with _svm(csr, "rbf", np.float32) as svm:
+        svm.setup_data_on_device()
+    err = capfd.readouterr().err
+    assert "[plssvm_mi]" in err and "expansion" in err, err[-2000:]
