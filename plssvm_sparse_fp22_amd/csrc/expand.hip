@@ -1408,68 +1408,28 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     }
     __syncthreads();
     constexpr int STEP = 64 * EXP_NH;
-    if constexpr (RF == 2) {
-        // pair flags: steps restart at every window (the part of a window's last step past its end is loaded again as
-        // the next window's first step). The contiguous walk below measured 4.5 % slower here (config 5: 0.861 vs
-        // 0.824 ms, round 6 — 127 VGPRs and a spill for the straddling step's registers), 1.8 % faster with chunk flags.
-        for (int64_t W = W0; W < W1; ++W) {
-            if (W + 1 < W1) load_win(W + 1);  // lands in registers while this window is processed
-            const int64_t c_end = wo[W + 1];
-            carry = wave * (int) (RB / EXP_NWV);  // the wave's first row starts every window
-            for (int64_t cb = wo[W]; cb < c_end; cb += STEP) {  // wave-uniform trip count
-                group_regs cur[EXP_NH];
-#pragma unroll
-                for (int hh = 0; hh < EXP_NH; ++hh) cur[hh] = nx[hh];
-                fetch((cb + STEP < c_end ? cb + STEP : c_end) + lane);
-#pragma unroll
-                for (int hh = 0; hh < EXP_NH; ++hh) group(cur[hh], cb + 64 * hh + lane < c_end);  // groups in order
-            }
-            if (W + 1 < W1) {
-                __syncthreads();  // every wave is done with window W
-                store_win();
-            }
-            __syncthreads();
-        }
-    } else if (W0 < W1) {
-        // The wave's stream is one contiguous range over its windows, walked in steps of STEP chunks that ignore the
-        // window boundaries: a step that straddles the end of window W is processed for W (the chunks below the end),
-        // then — after the block's window switch — for W + 1 (the chunks from there), so no chunk is loaded twice (the
-        // restarted steps load the part of a window's last step past its end again as the next window's first step:
-        // 3-RBF 0.782 -> 0.768 ms, round 6). Every wave switches windows W1 - W0 - 1 times (the block's barriers match).
-        int64_t W = W0, c_lo = wo[W0], c_hi = wo[W0 + 1];
-        const int base_row = wave * (int) (RB / EXP_NWV);  // RF: the wave's first row starts every window
-        carry = base_row;
+    // Steps restart at every window: the part of a window's last step past its end is masked and loaded again as the
+    // next window's first step (mostly from L2). Round 6 measured a walk that ignores the window boundaries (a
+    // straddling step processed for both windows, nothing loaded twice): 3-RBF 0.766 vs 0.770 ms over three same-box
+    // pairs and FETCH 4.915 vs 4.93 GB — nothing to show for it; with pair flags 4.5 % slower (registers, a spill).
+    for (int64_t W = W0; W < W1; ++W) {
         if (W + 1 < W1) load_win(W + 1);  // lands in registers while this window is processed
-        auto next_window = [&]() __attribute__((always_inline)) {
-            __syncthreads();  // every wave is done with window W
-            store_win();
-            __syncthreads();
-            ++W;
-            if (W + 1 < W1) load_win(W + 1);
-            c_lo = c_hi;
-            c_hi = wo[W + 1];
-            carry = base_row;
-        };
-        for (int64_t cb = wo[W0]; cb < s_end; cb += STEP) {  // wave-uniform trip count
+        const int64_t c_end = wo[W + 1];
+        carry = wave * (int) (RB / EXP_NWV);  // RF: the wave's first row starts every window
+        for (int64_t cb = wo[W]; cb < c_end; cb += STEP) {  // wave-uniform trip count
             group_regs cur[EXP_NH];
 #pragma unroll
             for (int hh = 0; hh < EXP_NH; ++hh) cur[hh] = nx[hh];
-            fetch((cb + STEP < s_end ? cb + STEP : s_end) + lane);  // the next step, one ahead (unconditional: a
-            // conditional load would wait for it at the merge)
-            for (;;) {
+            // next step (next window's first at c_end; groups past a window's end are loaded, masked, and
+            // loaded again as the next window's)
+            fetch((cb + STEP < c_end ? cb + STEP : c_end) + lane);
 #pragma unroll
-                for (int hh = 0; hh < EXP_NH; ++hh) {  // groups in order, the chunks of window W
-                    const int64_t pos = cb + 64 * hh + lane;
-                    group(cur[hh], pos >= c_lo && pos < c_hi);
-                }
-                if (c_hi > cb + STEP || W + 1 >= W1) break;  // window W goes on in the next step (or is the last)
-                next_window();
-                if (c_lo >= cb + STEP) break;  // the new window starts with the next step
-            }
+            for (int hh = 0; hh < EXP_NH; ++hh) group(cur[hh], cb + 64 * hh + lane < c_end);  // groups in order
         }
-        while (W + 1 < W1) next_window();  // a wave whose stream is empty still takes part in every switch
-        __syncthreads();
-    } else {
+        if (W + 1 < W1) {
+            __syncthreads();  // every wave is done with window W
+            store_win();
+        }
         __syncthreads();
     }
     const int64_t rb0 = I * RB;
