@@ -1114,6 +1114,13 @@ __global__ __launch_bounds__(256) void exp_cell_woff_kernel(const int64_t *__res
 #ifndef EXP_PSCAN
 #define EXP_PSCAN 1  // bfloat16 remainder: row sums as differences of one unsegmented lane prefix (0: segmented scan)
 #endif
+#ifndef EXP_COLPROBE
+// cost probe of the one-triangle stream (built only as a variant, -DEXP_COLPROBE=1): every bfloat16
+// slot also adds H_ij times a stand-in for w_i into an LDS float at its partner's index with ds_add_f32 — the column
+// scatter that design needs — into the row accumulator's LDS (the window already takes the rest), so the results
+// are wrong by construction; the timing bounds the design from below
+#define EXP_COLPROBE 0
+#endif
 #ifndef EXP_DOT2
 // bfloat16 remainder: a chunk's 4 products as two v_dot2_f32_bf16 (the stream is VALU-bound). The instruction
 // pair is inline assembly whose hazard padding (the s_nop in exp_hcell_kernel) was verified on the GPU with the
@@ -1266,6 +1273,17 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
     // one group of 64 chunks: the 4 slots times w from the window, then the rows' sums into racc
     // RF: the rows of a window's chunks from their row-start flags (carry = the row before the step's first chunk + 1)
     int carry = 0;
+#if EXP_COLPROBE
+    auto col_probe = [&](u32x2 jj, uint32_t hx, uint32_t hy, float wi) __attribute__((always_inline)) {
+        if constexpr (HB && sizeof(T) == 4) {
+            constexpr uint32_t MSK = (uint32_t) RBC - 1u;  // RBC: a power of two
+            atomicAdd(&racc[(jj.x & 0xFFFFu) & MSK], __uint_as_float(hx << 16) * wi);
+            atomicAdd(&racc[(jj.x >> 16) & MSK], __uint_as_float(hx & 0xFFFF0000u) * wi);
+            atomicAdd(&racc[(jj.y & 0xFFFFu) & MSK], __uint_as_float(hy << 16) * wi);
+            atomicAdd(&racc[(jj.y >> 16) & MSK], __uint_as_float(hy & 0xFFFF0000u) * wi);
+        }
+    };
+#endif
     auto group = [&](const group_regs &g, bool have) __attribute__((always_inline)) {
         if constexpr (RF == 2) {
             static_assert(HB && EXP_JH && sizeof(T) == 4, "pair flags: bfloat16 H, side-by-side chunks");
@@ -1294,6 +1312,9 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
                     a23 = __uint_as_float(hy << 16) * __uint_as_float(w23 << 16);
                     a23 = fmaf(__uint_as_float(hy & 0xFFFF0000u), __uint_as_float(w23 & 0xFFFF0000u), a23);
                 }
+#if EXP_COLPROBE
+                col_probe(jj, hx, hy, a01);
+#endif
             }
             const float t = a01 + a23;
             float P = t;
@@ -1349,6 +1370,9 @@ __global__ __launch_bounds__(EXP_NWV * 64) void exp_hcell_kernel(const int64_t *
                 asm("v_dot2_f32_bf16 %0, %1, %2, 0\n\tv_dot2_f32_bf16 %0, %3, %4, %0\n\ts_nop 1"
                     : "=&v"(acc)
                     : "v"(hx), "v"(w01), "v"(g.hb.y), "v"(w23));
+#if EXP_COLPROBE
+                col_probe(jj, hx, g.hb.y, acc);
+#endif
             }
         } else if (have) {
             acc = h0 * wat(jj.x & 0xFFFFu);
@@ -1999,6 +2023,11 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             MI_HIP_CHECK(hipMemcpyAsync(&NL, loff.get() + R, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
             MI_HIP_CHECK(hipStreamSynchronize(stream));
             if (NL >= (int64_t) INT32_MAX) return false;
+            // the transpose's peak: the packed pairs, their sorted copy and the symmetric rows (both
+            // triangles) live together once the slot pool is freed — gated on the same room as the pool
+            const double tr_b = (double) NL * (double) (2 * (sizeof(uint32_t) + sizeof(lt_val<T>)) + 2 * (4 + sizeof(T))) +
+                                4.0 * 8.0 * (double) (R + 1);
+            if (tr_b > room) return false;
             const int64_t NLa = std::max<int64_t>(NL, 1);
             dev_buf<uint32_t> lk, ks;
             dev_buf<lt_val<T>> lvv, vs;
@@ -2055,7 +2084,12 @@ void engine<T>::build_expansion(const int64_t *cpos, int64_t /*max_inc*/,
             return false;
         }
     };
-    if (lt_join()) ex.lt = true;
+    if (lt_join()) {
+        ex.lt = true;
+    } else {  // the full join recounts the pairs and the H bound; nothing the lower join read may survive it
+        ex.pairs = 0;
+        ex.hratio = -1.0;
+    }
     if (row_join && R > 0 && rbeg == nullptr) {
         const char *rj = std::getenv("PLSSVM_MI_EXP_RJ");
         const bool want = !(rj != nullptr && std::strcmp(rj, "twopass") == 0);

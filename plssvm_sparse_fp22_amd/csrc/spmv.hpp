@@ -39,7 +39,12 @@ namespace plssvm_mi {
 
 constexpr int SELL_NT = 1024;  // 16 waves per workgroup
 constexpr int SELL_WAVES = SELL_NT / 64;
-constexpr int SELL_XBYTES = 163840;  // LDS panel of the gathered vector (all of a CU's LDS)
+#ifndef SELL_LDS_KB
+#define SELL_LDS_KB 160  // LDS panel of the gathered vector (KiB); variants only (tools/variants.sh): 80 = two workgroups per CU
+#endif
+constexpr int SELL_XBYTES = SELL_LDS_KB * 1024;  // LDS panel of the gathered vector (default: all of a CU's LDS)
+constexpr int SELL_WG_PER_CU = 160 / SELL_LDS_KB;
+static_assert(SELL_WG_PER_CU * SELL_LDS_KB == 160, "the panel divides the CU's LDS");
 constexpr int SELL_SIGMA = 4096;     // sorting window (segments)
 // entries per lane in flight per step: the passes are bound by the bytes in flight per CU (one 1024-thread
 // workgroup per CU, every step's loads issued together). Measured on one box (round 3, CG it/s): real-typed
@@ -58,7 +63,7 @@ template <typename T>
 constexpr int sell_width() { return SELL_XBYTES / (int) sizeof(T); }
 // workgroups per pass: equal-cost chunk ranges, one per CU (one resident workgroup per CU with a full-LDS panel;
 // 512 / 768 / 1024 measured 8 / 14 / 18 % slower on config 3, round 4)
-inline int64_t sell_target_blocks() { return 256; }
+inline int64_t sell_target_blocks() { return 256 * SELL_WG_PER_CU; }
 
 struct sell_chunk {
     int64_t off;    // first entry (entry j of slot l at off + 64 j + l)
@@ -125,7 +130,7 @@ __device__ __forceinline__ T sell_val(const vals_t<T> &val, int64_t k) {
 // (the kernel expansion of the sparse poly / rbf K·p, expand.hip, runs MODE 1 over the CSC and MODE 2
 // over the CSR of the same data as the factored linear path's two MODE 0 passes)
 template <typename T, bool LDSX, bool F22, int KC = 1, int MODE = 0>
-__global__ __launch_bounds__(SELL_NT) void sell_spmv_kernel(const sell_chunk *__restrict__ chunks,
+__global__ __launch_bounds__(SELL_NT, 4 * SELL_WG_PER_CU) void sell_spmv_kernel(const sell_chunk *__restrict__ chunks,
                                                             const int32_t *__restrict__ perm,
                                                             const typename sell_idx<LDSX>::type *__restrict__ idx,
                                                             vals_t<T> val, const int32_t *__restrict__ bchunk,

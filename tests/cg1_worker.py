@@ -2,6 +2,7 @@
 
 usage: python cg1_worker.py CASE RANK WORLD PORT OUTDIR VARIANT
 """
+import datetime
 import os
 import sys
 
@@ -22,7 +23,8 @@ def main():
     import plssvm_sparse_fp22_amd as pm
 
     pm._abi.lib()
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=90))  # a lost peer fails the case, not the suite
     kernel, dtype, _, _, _, _, algo, env, _ = lc.CASES[name]
     os.environ.update(env)
     s = lc.load(name)

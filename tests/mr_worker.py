@@ -9,6 +9,7 @@ Writes q, one K·p (add = -1 and +1), the kernel part, and learn() (alpha, bias,
 
 usage: python mr_worker.py CASE RANK WORLD PORT OUTDIR
 """
+import datetime
 import os
 import sys
 
@@ -28,7 +29,8 @@ def main():
     import plssvm_sparse_fp22_amd as pm
 
     pm._abi.lib()
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=90))  # a lost peer fails the case, not the suite
     budget = BUDGET.get(case, {}).get(rank)
     if budget is not None:
         os.environ["PLSSVM_MI_MEM_BUDGET"] = budget

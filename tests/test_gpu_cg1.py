@@ -98,7 +98,7 @@ def test_one_reduction_cg_long_trace_world2(name, tmp_path):
     outs = []
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=240)
+            out, _ = p.communicate(timeout=150)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()

@@ -46,7 +46,7 @@ def run_group(case, world, tmp_path):
     outs = []
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=240)
+            out, _ = p.communicate(timeout=150)
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
