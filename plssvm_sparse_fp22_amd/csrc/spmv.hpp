@@ -51,8 +51,11 @@ constexpr int SELL_SIGMA = 4096;     // sorting window (segments)
 // values 4 / 6 / 8 entries: config 3 6 777 / 7 011 / 7 203, 3-RBF 958 / 961 / 969; packed FP22 (8-byte loads
 // per value) config 5 778 / 771 / 761 — so 8 for real values, 4 for FP22 (round 2, before the row-block pass
 // and the 16-bit pair loads, measured 4 best for both)
+#ifndef SELL_SU_REAL
+#define SELL_SU_REAL 8  // A/B variants only (tools/variants.sh)
+#endif
 template <bool F22>
-constexpr int sell_unroll() { return F22 ? 4 : 8; }
+constexpr int sell_unroll() { return F22 ? 4 : SELL_SU_REAL; }
 // LDS-panel passes: the 16-bit panel indices of entries 2t, 2t+1 of a slot are adjacent, so one 32-bit load per lane
 // (256 B per wave-instruction) fetches two (chunk widths padded to even); packed FP22 values likewise, one 12-byte
 // load per lane (3 words at 4-byte alignment) decodes two. (Pairing real values too measured no gain, round 2.)
