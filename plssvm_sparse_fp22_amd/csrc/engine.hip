@@ -145,7 +145,9 @@ void engine<T>::comm_init(int rank_, int world_, const void *uid) {
     }
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof(id));
-    comm_aborted = false;
+    // an aborted context stays aborted: a peer that failed before this rank got here will never join the rendezvous
+    // below, and resetting the flag would leave this thread blocked in ncclCommInitRank (device_group's failure protocol)
+    if (comm_aborted) throw mi_error(-3, "the group was aborted by another rank");
     {
         ncclComm_t c = nullptr;
         const ncclResult_t rc = ncclCommInitRank(&c, world, id, rank);  // blocks until every rank joined
