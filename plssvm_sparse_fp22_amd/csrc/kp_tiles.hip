@@ -145,14 +145,17 @@ __device__ __forceinline__ void glds16_buf(const void *base, void *lds_dst, uint
 template <typename T, int KERNEL>
 constexpr int kp_waves_per_eu() { return 3; }
 
-// fp64: chunk kc+1's DMA is issued after chunk kc's LDS reads, fp32: right after the barrier. Same box, round 6
-// (profiles/r06_kp_dma_order_ab.json): config 2 (fp64 RBF) 39.51 / 39.58 ms against 39.62 / 39.67 ms with the DMA first,
-// configs[3] (fp32 linear) 1 913 ms against 1 782 ms. KP_DMA_AFTER_READS=0 / 1 forces one order (A/B variants only)
+// fp64 RBF: chunk kc+1's DMA is issued after chunk kc's LDS reads; every other instance: right after the barrier.
+// Same box, round 6 (profiles/r06_kp_dma_order_ab.json): config 2 (fp64 RBF) 39.51 / 39.58 ms against 39.62 / 39.67 ms
+// with the DMA first; fp64 linear 37.18 / 37.23 against 36.67 / 36.67 ms, fp64 poly 38.72 / 38.76 against 38.58 /
+// 38.58 ms, configs[3] (fp32 linear) 1 913 against 1 782 ms. KP_DMA_AFTER_READS=0 / 1 forces one order (A/B only)
 #ifndef KP_DMA_AFTER_READS
 #define KP_DMA_AFTER_READS 2
 #endif
-template <typename T>
-constexpr bool kp_dma_after_reads() { return KP_DMA_AFTER_READS == 2 ? sizeof(T) == 8 : KP_DMA_AFTER_READS == 1; }
+template <typename T, int KERNEL>
+constexpr bool kp_dma_after_reads() {
+    return KP_DMA_AFTER_READS == 2 ? (sizeof(T) == 8 && KERNEL == 2) : KP_DMA_AFTER_READS == 1;
+}
 
 template <typename T, int KERNEL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_per_eu<T, KERNEL>(), kp_waves_per_eu<T, KERNEL>()))) void kp_tile_kernel(kfun<T> kf, const T *__restrict__ XT,
@@ -266,13 +269,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
     for (int64_t kc = 0; kc < nk; ++kc) {
         if (kc > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // chunk kc visible to all waves; every wave is done reading chunk kc-1
-        if (!kp_dma_after_reads<T>() && kc + 1 < nk) issue(kc + 1, (int) ((kc + 1) & 1));
+        if (!kp_dma_after_reads<T, KERNEL>() && kc + 1 < nk) issue(kc + 1, (int) ((kc + 1) & 1));
         const T *A = smem + OFF_PAN + (2 * (kc & 1)) * PANEL;
         const T *B = A + PANEL;
-        // fp64: the whole chunk's operands come out of LDS before chunk kc+1's DMA is issued — the compiler cannot tell
-        // the DMA's LDS target from the buffer being read, so an LDS read issued after the DMA waits for it (vmcnt(0))
-        // and the prefetch sits on each wave's critical path instead of under its MFMAs (fp32 measured faster with the
-        // DMA first, see kp_dma_after_reads)
+        // fp64 RBF: the whole chunk's operands come out of LDS before chunk kc+1's DMA is issued — the compiler cannot
+        // tell the DMA's LDS target from the buffer being read, so an LDS read issued after the DMA waits for it
+        // (vmcnt(0)) and the prefetch sits on each wave's critical path instead of under its MFMAs (the other instances
+        // measured faster with the DMA first, see kp_dma_after_reads)
         T a[BK / 4][4], b[BK / 4][4];
 #pragma unroll
         for (int ks = 0; ks < BK / 4; ++ks) {
@@ -282,7 +285,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kp_waves_pe
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) b[ks][nt] = B[kr * KP_TILE + wc * 64 + nt * 16 + (lane & 15)];
         }
-        if (kp_dma_after_reads<T>() && kc + 1 < nk) issue(kc + 1, (int) ((kc + 1) & 1));
+        if (kp_dma_after_reads<T, KERNEL>() && kc + 1 < nk) issue(kc + 1, (int) ((kc + 1) & 1));
 #pragma unroll
         for (int ks = 0; ks < BK / 4; ++ks)
 #pragma unroll
